@@ -1,0 +1,205 @@
+"""Trainer-step benchmark: fused packed-GRPO loss head on MI355X (BASELINE.json configs[1], C2).
+
+Workload per rank (weak scaling): one packed micro-batch of T = 65536 tokens (32 rollouts x 2048,
+prompt 256) of Qwen2.5-1.5B-shaped logits [1, T, 151936] bf16, synthetic, resident in HBM.
+One step = what rl_step does for a micro-batch after the model forward (rl/__init__.py:199-377):
+fused HIP forward (log-softmax + gather + entropy + PPO/KL loss + stats + dlogits), the
+autograd backward (upstream-gradient check on device), the one D2H read of the statistics,
+and for N > 1 the per-pass sample-count exchange of the DP loop (finetune_loop.py:613,
+all-reduce of one int64 over RCCL).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...     (one rank per GPU)
+
+Prints ONE JSON line (rank 0).  roofline.achieved = algorithmic bytes per launch
+(T*V*2 read + T*V*2 dlogits write + 37*T side data) / the average duration
+of the prl_grpo_forward launch measured with HIP events on its stream.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+for _p in (str(ROOT), str(ROOT / "pipelinerl-swe_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md); measured float4 copy 6290 GB/s
+SIDE_BYTES_PER_TOKEN = 37  # ids 8 + old 4 + ref 4 + adv 4 + w 4 + mask 1 + lp/H/tok_loss 12
+
+
+def make_workload(T: int, V: int, seq: int, prompt: int, seed: int, device):
+    g = torch.Generator(device=device).manual_seed(seed)
+    logits = torch.empty((1, T, V), dtype=torch.bfloat16, device=device)
+    chunk = 4096
+    for a in range(0, T, chunk):  # chunked generation keeps the fp32 temporary small
+        b = min(T, a + chunk)
+        logits[0, a:b] = (torch.randn((b - a, V), generator=g, device=device) * 3.0).to(torch.bfloat16)
+    nseq = T // seq
+    pos = torch.arange(T, device=device) % seq
+    ids = torch.randint(0, 151643, (1, T), generator=g, device=device)
+    labels = torch.where(pos[None] >= prompt, ids, torch.full_like(ids, -100))
+    rewards = torch.repeat_interleave(torch.randint(0, 2, (nseq,), generator=g, device=device).float(), seq)[None]
+    lab = (labels != -100).float()
+    old = (torch.randn((1, T), generator=g, device=device) - 12.0) * lab
+    fields = {
+        "input_ids": ids, "labels": labels, "rewards": rewards, "advantages": rewards - rewards.mean(),
+        "ref_logprobs": old.clone(), "old_logprobs": old,
+        "group_tokens": torch.full((1, T), float(seq), device=device),
+        "num_labels": torch.full((1, T), float(seq - prompt), device=device),
+        "overflow": torch.zeros((1, T), device=device),
+    }
+    return logits.requires_grad_(True), {k: v.contiguous() for k, v in fields.items()}
+
+
+def cpu_baseline(rows: int, V: int, threads: int) -> dict:
+    """Oracle (numpy restatement of rl_step's loss head incl. gradient) on a bounded sample."""
+    from oracle import grpo_oracle, synth
+
+    T = rows + 1
+    b = synth.packed_rl_batch(11, [T], [1], id_range=151643, eos=151643)
+    lg = synth.to_bf16(np.random.default_rng(0).normal(0, 3.0, (1, T, V))).astype(np.float32)
+    m = b["labels"] != -100
+    b["old_logprobs"] = np.where(m, -12.0, 0).astype(np.float32)
+    b["ref_logprobs"] = b["old_logprobs"].copy()
+    cfg = dict(policy_loss="ppo", epsilon=4.0, kl_coef=0.0, final_kl_coef=0.0, batch_size=256,
+               clamp_log_ratio_ref_new_value=5)
+    t0 = time.perf_counter()
+    grpo_oracle.rl_step_oracle(lg, b, cfg, 0, 10, dtype=np.float32, threads=threads, row_chunk=16)
+    dt = time.perf_counter() - t0
+    return {"value": round(rows / dt, 1), "unit": "tokens/s", "cores": threads, "kind": "port",
+            "sample": f"{rows} packed rows x V={V}, fwd+grad, numpy float32 oracle, {threads} threads, {dt:.2f} s"}
+
+
+def load_traffic(T: int, V: int) -> tuple[float | None, str | None]:
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if one exists for this shape."""
+    for p in sorted((ROOT / "profiles").glob("*pmc_traffic.json"), reverse=True):
+        try:
+            d = json.loads(p.read_text())
+        except Exception:
+            continue
+        if d.get("T") == T and d.get("V") == V and d.get("bytes_per_launch"):
+            return float(d["bytes_per_launch"]), p.name
+    return None, None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--tokens", type=int, default=65536)
+    ap.add_argument("--vocab", type=int, default=151936)
+    ap.add_argument("--cpu-rows", type=int, default=2048)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from pipelinerl_amd import _native
+    from pipelinerl_amd.finetune.rl.fused import GrpoParams, grpo_loss
+
+    _native.load()
+    T, V = args.tokens, args.vocab
+    logits, fields = make_workload(T, V, seq=2048, prompt=256, seed=1234 + rank, device=dev)
+    # GRPO defaults: conf/finetune/base.yaml:92-105 + grpo.yaml (ppo, eps 4, kl 0, C 5)
+    params = GrpoParams(policy_loss="ppo", epsilon=4.0, kl_coef=0.0, entropy_coef=0.0, clamp_log_ratio=5.0,
+                        temperature=1.0, batch_size=4096.0)
+    samples = torch.zeros(1, dtype=torch.int64, device=dev)
+    fwd_ev = []
+
+    def step(timed: bool):
+        logits.grad = None
+        if timed:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        loss, stats, _ = grpo_loss(logits, fields, params)
+        if timed:
+            e1.record()
+            fwd_ev.append((e0, e1))
+        loss.backward()
+        host = stats.cpu()  # the one statistics read-back per micro-batch
+        if world > 1:
+            samples.fill_(T // 2048)
+            dist.all_reduce(samples)
+        return host
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in fwd_ev]))
+    k_max = torch.tensor([kern_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        dist.all_reduce(k_max, op=dist.ReduceOp.MAX)
+    elapsed = float(t_max)
+    kern_ms = float(k_max)
+
+    if rank == 0:
+        ms_per_step = elapsed / args.steps * 1e3
+        tokens_total = T * world * args.steps
+        alg_bytes = 2.0 * T * V * 2 + SIDE_BYTES_PER_TOKEN * T
+        achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+        traffic, tsrc = load_traffic(T, V)
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            threads = min(os.cpu_count() or 1, 16)
+            cpu = cpu_baseline(args.cpu_rows, V, threads)
+        out = {
+            "metric": "trainer tokens/s (packed GRPO) at 1/2/4/8 MI355X; loss-kernel HBM GB/s",
+            "value": round(tokens_total / elapsed, 1),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic packed rollouts (randn*3 bf16 logits, 32 x 2048-token sequences, 256-token prompts)",
+            "config": {"workload": "C2: fused GRPO loss head fwd+grad, Qwen2.5-1.5B vocab, packed micro-batch",
+                       "tokens_per_rank": T, "vocab": V, "logits_dtype": "bf16", "policy_loss": "ppo",
+                       "parallelism": f"dp{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic, "kernel": "grpo_fwd_resident<19> (+stats/finalize) per prl_grpo_forward",
+                         "kernel_ms": round(kern_ms, 4), "algorithmic_bytes": alg_bytes,
+                         "traffic_source": tsrc},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,189 @@
+/* prl_hip.h — C ABI of the MI355X GRPO trainer-step library (libprl_hip.so).
+ *
+ * Plain C: device pointers, sizes and a hipStream_t (passed as void*).  No torch types.
+ * Every entry point returns 0 on success or a PRL_E* / hipError_t-derived code; nothing
+ * throws across the ABI.  All buffers are caller-owned device memory.  The library keeps no
+ * global state besides a per-device property cache.
+ *
+ * Reference interfaces replaced (paths under the reference repo, ServiceNow/PipelineRL-SWE):
+ *   prl_grpo_forward   <- rl_step loss head + stats + autograd backward
+ *                         pipelinerl/finetune/rl/__init__.py:130-377 (ATen ops :200-366)
+ *                         and pipelinerl/finetune/rl/utils.py:25-30,66-87 (masked sums)
+ *   prl_grpo_backward  <- the autograd backward of the same graph (loss.backward() at
+ *                         pipelinerl/finetune_loop.py:620-629) when the upstream gradient
+ *                         differs from the one assumed by the fused forward
+ *   prl_flatten_bf16 / prl_unflatten_bf16
+ *                      <- per-parameter `parameter.data.bfloat16()` + dist.broadcast loop
+ *                         of WeightUpdateManager.send_weight_update
+ *                         (pipelinerl/finetune_loop.py:202-205, :246-247) and the actor's
+ *                         per-tensor receive buffers (pipelinerl/vllm1.py:84-93)
+ *   prl_grad_sqnorm    <- clip_grad_norm_'s global norm (finetune_loop.py:642-643)
+ */
+#ifndef PRL_HIP_H
+#define PRL_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PRL_ABI_VERSION 1
+
+/* error codes (besides hipError_t values, which are < 1000) */
+#define PRL_OK 0
+#define PRL_E_INVALID 1001      /* bad argument: shape, null pointer, alignment */
+#define PRL_E_UNSUPPORTED 1002  /* dtype / layout not supported */
+#define PRL_E_WORKSPACE 1003    /* workspace too small */
+
+/* dtypes */
+#define PRL_F32 0
+#define PRL_BF16 1
+
+/* policy losses (rl/__init__.py:269-283) */
+#define PRL_PPO 0
+#define PRL_REINFORCE 1
+
+/* statistics written by prl_grpo_forward into stats[PRL_NSTAT] (double) */
+enum PrlStat {
+  PRL_S_LOSS_SUM = 0,      /* sum nz(token_loss * mask)   -> policy_loss_total = -this */
+  PRL_S_VALUE_LOSS,        /* sum nz(0.5 (v-r)^2 w mask) */
+  PRL_S_REWARD,            /* sum nz(r / nl * mask) ... per-label-normalised sums */
+  PRL_S_ENTROPY,
+  PRL_S_OLD_LP,
+  PRL_S_NEW_LP,
+  PRL_S_REF_LP,
+  PRL_S_ADVANTAGE,
+  PRL_S_KL,
+  PRL_S_POLICY_LOSS,
+  PRL_S_SURR1,
+  PRL_S_SURR2,
+  PRL_S_RATIO,             /* sum nz(ratio/nl) */
+  PRL_S_RATIO_SUM,         /* sum nz(ratio) */
+  PRL_S_RATIO_SQ_SUM,      /* sum nz(ratio^2) */
+  PRL_S_RATIO_REF_NEW,
+  PRL_S_RATIO_REF_OLD,
+  PRL_S_CLAMP_REF_NEW,
+  PRL_S_CLAMP_NEW_OLD,
+  PRL_S_TOKEN_WEIGHT,
+  PRL_S_VALUE_MEAN,
+  PRL_S_VALUE_MSE,
+  PRL_S_NUM_NANS,          /* count isnan(token_loss), all positions */
+  PRL_S_NUM_OUT,           /* count mask */
+  PRL_S_BAD_LP,            /* count non-finite new log-probs, all positions  (assert :209) */
+  PRL_S_BAD_LRRN,          /* count non-finite ref-new log ratio             (assert :237) */
+  PRL_S_BAD_KL,            /* count non-finite approx KL                     (assert :264) */
+  PRL_S_BAD_GT,            /* count group_tokens <= 0 when group-normalising (assert :222) */
+  PRL_S_BAD_ID,            /* count target ids outside [0, V)   (torch.gather IndexError :208) */
+  PRL_S_MAX_REWARD,        /* masked max/min (NaN-propagating, like torch.max) */
+  PRL_S_MIN_REWARD,
+  PRL_S_MAX_ADV,
+  PRL_S_MIN_ADV,
+  PRL_S_MAX_KL,
+  PRL_S_MIN_KL,
+  PRL_S_MAX_W,
+  PRL_S_MIN_W,
+  PRL_S_MAX_VALUE,
+  PRL_S_MIN_VALUE,
+  PRL_NSTAT
+};
+
+/* Inputs: a [B, L] batch of packed (B = 1) or padded (B >= 1) rollouts and its logits
+ * [B, L, V] (row stride ld elements, batch stride L*ld).  Row t of sequence b is scored
+ * against input_ids[b, t+1]; rows t = L-1 carry no loss.  Token fields are the
+ * PipelineBatchEncoding tensors (pipelinerl/finetune/types.py:48-75), float32 [B, L]. */
+typedef struct PrlGrpoBatch {
+  const void* logits;          /* [B, L, V] bf16 or f32 */
+  int32_t logits_dtype;        /* PRL_BF16 | PRL_F32 */
+  int32_t _pad0;
+  int64_t B, L, V, ld;         /* ld = row stride in elements (>= V) */
+  const int64_t* input_ids;    /* [B, L] */
+  const int64_t* labels;       /* [B, L], -100 = masked */
+  const float* rewards;
+  const float* advantages;
+  const float* ref_logprobs;
+  const float* old_logprobs;
+  const float* group_tokens;
+  const float* num_labels;
+  const float* overflow;
+  const float* values;         /* [B, L] value-head output or NULL */
+} PrlGrpoBatch;
+
+typedef struct PrlGrpoParams {
+  int32_t policy_loss;         /* PRL_PPO | PRL_REINFORCE */
+  int32_t use_advantages;
+  int32_t relu_log_p_weights;
+  int32_t group_normalization;
+  int32_t overlong_filtering;
+  int32_t write_grad;          /* 1: prl_grpo_forward also writes dlogits */
+  float epsilon;
+  float kl_coef;               /* already linearly decayed (rl/__init__.py:265-266) */
+  float entropy_coef;          /* already linearly decayed */
+  float clamp_log_ratio;       /* clamp_log_ratio_ref_new_value */
+  float temperature;
+  float batch_size;            /* token weight = 1 / batch_size unless group-normalised */
+  float value_loss_coef;
+  float grad_scale;            /* upstream d(final_loss) assumed for dlogits / dvalues */
+} PrlGrpoParams;
+
+/* Outputs.  Per-token arrays have B*(L-1) entries (row q = b*(L-1) + t). */
+typedef struct PrlGrpoOutputs {
+  float* new_logprobs;
+  float* entropy;
+  float* lse;                  /* log-sum-exp of logits/temperature (natural log) */
+  float* token_loss;           /* (pol - kl_c kl + ent_c H) * w  (unmasked) */
+  float* g_lp;                 /* d final / d new_lp  at grad_scale */
+  float* g_h;                  /* d final / d entropy at grad_scale */
+  float* dvalues;              /* [B, L] or NULL (required when values != NULL) */
+  void* dlogits;               /* [B, L, V], same dtype/ld as logits, or NULL */
+  double* stats;               /* [PRL_NSTAT] */
+} PrlGrpoOutputs;
+
+int prl_abi_version(void);
+const char* prl_error_string(int code);
+
+/* Bytes of device workspace prl_grpo_forward needs on `device` (per-block partial sums). */
+int prl_grpo_workspace_bytes(int device, size_t* bytes);
+
+/* Fused loss head: log-softmax + gather + entropy over V, importance ratio x advantage
+ * policy loss (PPO / REINFORCE), KL-to-reference (Schulman k3), token weights, masked
+ * statistics, and (write_grad) dlogits for upstream gradient grad_scale.
+ * One read of the logits and (write_grad) one write of dlogits. */
+int prl_grpo_forward(const PrlGrpoBatch* batch, const PrlGrpoParams* params,
+                     const PrlGrpoOutputs* out, void* workspace, size_t workspace_bytes,
+                     void* stream);
+
+/* Gradient pass from the per-row lse / entropy / g_lp / g_h saved by prl_grpo_forward (at
+ * params->grad_scale), for an upstream gradient read ON DEVICE from *upstream (NULL = 1.0):
+ *   dlogits = (*upstream) * d final / d logits.
+ * If params->write_grad is set, dlogits already holds the gradient for upstream == 1 and
+ * the kernel returns without touching memory when *upstream == 1 (no host sync needed to
+ * decide).  Rows with zero coefficients are written as zeros without reading the logits. */
+int prl_grpo_backward(const PrlGrpoBatch* batch, const PrlGrpoParams* params,
+                      const float* lse, const float* entropy, const float* g_lp,
+                      const float* g_h, const float* upstream, void* dlogits, void* stream);
+
+/* Number of statistics (PRL_NSTAT) compiled into the library: bindings check it. */
+int prl_grpo_nstat(void);
+
+/* Weight broadcast staging: copy n tensors (f32 or bf16, contiguous) into one bf16 buffer
+ * at the given element offsets (dst_offsets[i], bf16 elements; 8-element aligned for the
+ * vector path), converting with round-to-nearest-even; and the inverse into bf16 or f32
+ * destinations.  srcs/dsts/dtypes/numels/offsets are HOST arrays of length n. */
+int prl_flatten_bf16(const void* const* srcs, const int32_t* dtypes, const int64_t* numels,
+                     const int64_t* dst_offsets, int32_t n, void* dst, void* stream);
+int prl_unflatten_bf16(const void* src, void* const* dsts, const int32_t* dtypes,
+                       const int64_t* numels, const int64_t* src_offsets, int32_t n,
+                       void* stream);
+
+/* Sum of squares of n device tensors (f32 or bf16) accumulated into *out (device f64).
+ * *out is overwritten. */
+int prl_grad_sqnorm(const void* const* srcs, const int32_t* dtypes, const int64_t* numels,
+                    int32_t n, double* out, void* workspace, size_t workspace_bytes,
+                    void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PRL_HIP_H */

@@ -1,0 +1,77 @@
+"""Build libprl_hip.so (HIP, gfx950 only) in-tree with hipcc.
+
+    python -m pipelinerl_amd._build [--resource-usage]
+
+The library is the C-ABI declared in include/prl_hip.h.  It is built next to this file so
+it travels with the repository snapshot to the GPU box (a JIT cache would not).
+"""
+
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+REPO = PKG.parents[1]
+INCLUDE = REPO / "include"
+CSRC = PKG / "csrc"
+LIB = PKG / "libprl_hip.so"
+ARCH = "gfx950"
+SOURCES = ["grpo_loss.hip", "flat_pack.hip"]
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and Path(cand).exists():
+            return cand
+    raise RuntimeError("hipcc not found: the MI355X library cannot be built")
+
+
+def _stale() -> bool:
+    if not LIB.exists():
+        return True
+    mt = LIB.stat().st_mtime
+    deps = list(CSRC.glob("*.hip")) + list(CSRC.glob("*.h")) + [INCLUDE / "prl_hip.h", Path(__file__)]
+    return any(d.stat().st_mtime > mt for d in deps)
+
+
+def build(force: bool = False, resource_usage: bool = False, verbose: bool = False) -> Path:
+    if not force and not resource_usage and not _stale():
+        return LIB
+    cc = hipcc()
+    objdir = PKG / "build"
+    objdir.mkdir(exist_ok=True)
+    flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", f"-I{INCLUDE}", f"-I{CSRC}",
+             "-Wall", "-Wno-unused-function"]
+    if resource_usage:
+        flags.append("-Rpass-analysis=kernel-resource-usage")
+
+    def compile_one(src: str):
+        obj = objdir / (Path(src).stem + ".o")
+        cmd = [cc, *flags, "-c", str(CSRC / src), "-o", str(obj)]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-8000:]}")
+        return obj, r.stderr
+
+    with ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
+        results = list(ex.map(compile_one, SOURCES))
+    if resource_usage or verbose:
+        for (_, err), src in zip(results, SOURCES):
+            (objdir / (Path(src).stem + ".resource.txt")).write_text(err)
+    tmp = LIB.with_suffix(".so.tmp")
+    cmd = [cc, "-shared", f"--offload-arch={ARCH}", "-o", str(tmp), *[str(o) for o, _ in results]]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stderr[-8000:]}")
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    out = build(force=True, resource_usage="--resource-usage" in sys.argv, verbose=True)
+    print(out)

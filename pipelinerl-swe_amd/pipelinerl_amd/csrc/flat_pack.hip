@@ -1,0 +1,211 @@
+// Weight-broadcast staging for MI355X: many parameter tensors <-> one flat bf16 buffer.
+//
+// Replaces the reference's per-parameter `parameter.data.bfloat16()` + one dist.broadcast
+// per tensor (pipelinerl/finetune_loop.py:202-205, :246-247) and the actor's per-tensor
+// receive buffers (pipelinerl/vllm1.py:84-93).  The trainer packs every parameter into
+// one bf16 bucket buffer (HBM-bound, 16-B vector accesses, round-to-nearest-even), RCCL
+// broadcasts large buckets, and the actor unpacks into its parameters.
+//
+// Launch shape: tensors are processed in groups of kGroup; blockIdx.y = tensor in group,
+// blockIdx.x grid-strides over that tensor's elements (descriptor table passed by value,
+// so no host->device copy and the launch is graph-capturable).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "grpo_common.h"
+#include "prl_hip.h"
+
+namespace prl {
+
+constexpr int kGroup = 32;
+
+struct PackGroup {
+  const void* src[kGroup];
+  void* dst[kGroup];
+  int64_t numel[kGroup];
+  int64_t off[kGroup];
+  int32_t dtype[kGroup];
+  int32_t n;
+};
+
+__device__ __forceinline__ float load_as_f(const void* p, int dt, int64_t i) {
+  return dt == PRL_F32 ? static_cast<const float*>(p)[i] : bf_to_f(static_cast<const uint16_t*>(p)[i]);
+}
+
+// flatten: group.src[i] (f32|bf16) -> flat bf16 at group.off[i]
+__global__ __launch_bounds__(256) void flatten_bf16_kernel(PackGroup g, uint16_t* __restrict__ flat) {
+  const int t = blockIdx.y;
+  if (t >= g.n) return;
+  const int64_t n = g.numel[t];
+  const int dt = g.dtype[t];
+  uint16_t* out = flat + g.off[t];
+  const void* src = g.src[t];
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const bool vec = ((g.off[t] & 7) == 0) && ((reinterpret_cast<uintptr_t>(src) & 15) == 0);
+  int64_t done = 0;
+  if (vec) {
+    const int64_t nv = n >> 3;
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
+      u32x4 o;
+      if (dt == PRL_BF16) {
+        o = reinterpret_cast<const u32x4*>(src)[v];
+      } else {
+        const f32x4 a = reinterpret_cast<const f32x4*>(src)[2 * v];
+        const f32x4 b = reinterpret_cast<const f32x4*>(src)[2 * v + 1];
+        o[0] = pack_bf16x2(a[0], a[1]);
+        o[1] = pack_bf16x2(a[2], a[3]);
+        o[2] = pack_bf16x2(b[0], b[1]);
+        o[3] = pack_bf16x2(b[2], b[3]);
+      }
+      reinterpret_cast<u32x4*>(out)[v] = o;
+    }
+    done = nv << 3;
+  }
+  for (int64_t i = done + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    out[i] = dt == PRL_BF16 ? static_cast<const uint16_t*>(src)[i] : f_to_bf(static_cast<const float*>(src)[i]);
+}
+
+// unflatten: flat bf16 at group.off[i] -> group.dst[i] (f32|bf16)
+__global__ __launch_bounds__(256) void unflatten_bf16_kernel(PackGroup g, const uint16_t* __restrict__ flat) {
+  const int t = blockIdx.y;
+  if (t >= g.n) return;
+  const int64_t n = g.numel[t];
+  const int dt = g.dtype[t];
+  const uint16_t* in = flat + g.off[t];
+  void* dst = g.dst[t];
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const bool vec = ((g.off[t] & 7) == 0) && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0);
+  int64_t done = 0;
+  if (vec) {
+    const int64_t nv = n >> 3;
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
+      const u32x4 x = reinterpret_cast<const u32x4*>(in)[v];
+      if (dt == PRL_BF16) {
+        reinterpret_cast<u32x4*>(dst)[v] = x;
+      } else {
+        f32x4 a = {bf_lo(x[0]), bf_hi(x[0]), bf_lo(x[1]), bf_hi(x[1])};
+        f32x4 b = {bf_lo(x[2]), bf_hi(x[2]), bf_lo(x[3]), bf_hi(x[3])};
+        reinterpret_cast<f32x4*>(dst)[2 * v] = a;
+        reinterpret_cast<f32x4*>(dst)[2 * v + 1] = b;
+      }
+    }
+    done = nv << 3;
+  }
+  for (int64_t i = done + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint16_t x = in[i];
+    if (dt == PRL_BF16)
+      static_cast<uint16_t*>(dst)[i] = x;
+    else
+      static_cast<float*>(dst)[i] = bf_to_f(x);
+  }
+}
+
+// sum of squares (double accumulation; one double atomic per block)
+__global__ __launch_bounds__(256) void sqnorm_kernel(PackGroup g, double* __restrict__ out) {
+  const int t = blockIdx.y;
+  if (t >= g.n) return;
+  const int64_t n = g.numel[t];
+  const int dt = g.dtype[t];
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  double acc = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const float v = load_as_f(g.src[t], dt, i);
+    acc += (double)v * (double)v;
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  __shared__ double part[4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) part[wid] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(out, part[0] + part[1] + part[2] + part[3]);
+}
+
+static int grid_x_for(const PackGroup& g) {
+  int64_t mx = 1;
+  for (int i = 0; i < g.n; ++i) mx = g.numel[i] > mx ? g.numel[i] : mx;
+  int64_t blocks = (mx / 8 + 255) / 256;
+  if (blocks < 1) blocks = 1;
+  if (blocks > 1024) blocks = 1024;
+  return (int)blocks;
+}
+
+}  // namespace prl
+
+using namespace prl;
+
+extern "C" {
+
+int prl_flatten_bf16(const void* const* srcs, const int32_t* dtypes, const int64_t* numels,
+                     const int64_t* dst_offsets, int32_t n, void* dst, void* stream) {
+  if (n < 0 || (n > 0 && (!srcs || !dtypes || !numels || !dst_offsets || !dst))) return PRL_E_INVALID;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  for (int base = 0; base < n; base += kGroup) {
+    PackGroup g{};
+    g.n = (n - base) < kGroup ? (n - base) : kGroup;
+    for (int i = 0; i < g.n; ++i) {
+      if (dtypes[base + i] != PRL_F32 && dtypes[base + i] != PRL_BF16) return PRL_E_UNSUPPORTED;
+      if (numels[base + i] < 0 || dst_offsets[base + i] < 0) return PRL_E_INVALID;
+      g.src[i] = srcs[base + i];
+      g.dtype[i] = dtypes[base + i];
+      g.numel[i] = numels[base + i];
+      g.off[i] = dst_offsets[base + i];
+    }
+    hipLaunchKernelGGL(flatten_bf16_kernel, dim3(grid_x_for(g), g.n), dim3(256), 0, s, g,
+                       static_cast<uint16_t*>(dst));
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+  }
+  return PRL_OK;
+}
+
+int prl_unflatten_bf16(const void* src, void* const* dsts, const int32_t* dtypes, const int64_t* numels,
+                       const int64_t* src_offsets, int32_t n, void* stream) {
+  if (n < 0 || (n > 0 && (!src || !dsts || !dtypes || !numels || !src_offsets))) return PRL_E_INVALID;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  for (int base = 0; base < n; base += kGroup) {
+    PackGroup g{};
+    g.n = (n - base) < kGroup ? (n - base) : kGroup;
+    for (int i = 0; i < g.n; ++i) {
+      if (dtypes[base + i] != PRL_F32 && dtypes[base + i] != PRL_BF16) return PRL_E_UNSUPPORTED;
+      if (numels[base + i] < 0 || src_offsets[base + i] < 0) return PRL_E_INVALID;
+      g.dst[i] = dsts[base + i];
+      g.dtype[i] = dtypes[base + i];
+      g.numel[i] = numels[base + i];
+      g.off[i] = src_offsets[base + i];
+    }
+    hipLaunchKernelGGL(unflatten_bf16_kernel, dim3(grid_x_for(g), g.n), dim3(256), 0, s, g,
+                       static_cast<const uint16_t*>(src));
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+  }
+  return PRL_OK;
+}
+
+int prl_grad_sqnorm(const void* const* srcs, const int32_t* dtypes, const int64_t* numels, int32_t n,
+                    double* out, void* workspace, size_t workspace_bytes, void* stream) {
+  (void)workspace;
+  (void)workspace_bytes;
+  if (!out || n < 0 || (n > 0 && (!srcs || !dtypes || !numels))) return PRL_E_INVALID;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipError_t e = hipMemsetAsync(out, 0, sizeof(double), s);
+  if (e != hipSuccess) return (int)e;
+  for (int base = 0; base < n; base += kGroup) {
+    PackGroup g{};
+    g.n = (n - base) < kGroup ? (n - base) : kGroup;
+    for (int i = 0; i < g.n; ++i) {
+      if (dtypes[base + i] != PRL_F32 && dtypes[base + i] != PRL_BF16) return PRL_E_UNSUPPORTED;
+      g.src[i] = srcs[base + i];
+      g.dtype[i] = dtypes[base + i];
+      g.numel[i] = numels[base + i];
+    }
+    int gx = grid_x_for(g) * 8;
+    if (gx > 1024) gx = 1024;
+    hipLaunchKernelGGL(sqnorm_kernel, dim3(gx, g.n), dim3(256), 0, s, g, out);
+    e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+  }
+  return PRL_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,693 @@
+// Fused GRPO loss head for MI355X (gfx950).  HBM-bound: one read of the [rows x V] logits,
+// one write of dlogits, ~45 B of per-token side data.  No MFMA.
+//
+// Reference: pipelinerl/finetune/rl/__init__.py:199-366 (ATen op chain over [1, T, V]) and
+// its autograd backward.  Kernels:
+//   grpo_fwd_resident<NV>  bf16 logits, V % 8 == 0 (Qwen2.5: V = 151936 / 152064).
+//       Persistent grid, one 1024-thread workgroup per CU, one vocab row per iteration.
+//       The whole row (V*2 B = 297 KiB) is held in VGPRs (NV x 16 B per lane), so the
+//       gradient pass re-reads nothing.  Software pipeline: while the gradient of row r is
+//       written, vector k of row r+grid is loaded into the register that vector k of row r
+//       just vacated, so every CU keeps ~300 KiB of loads in flight across the row seam.
+//       Row reduction: per-lane online (max, sum 2^y, sum 2^y y) with lazy rebase, wave
+//       shuffles, then one LDS exchange (double-buffered by row parity: one barrier/row).
+//   grpo_fwd_stream<T,VEC> any dtype / V: same math, row re-read for the gradient pass.
+//   grpo_bwd_stream<T,VEC> gradient-only pass from the saved per-row coefficients.
+//   grpo_stats_partial     the ~38 masked statistics of rl/__init__.py:315-375 and the
+//                          value-head gradient, from the per-row outputs (light: ~60 B/row)
+//   grpo_finalize          deterministic fold of the per-workgroup statistic partials.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <utility>
+
+#include "grpo_common.h"
+#include "prl_hip.h"
+
+namespace prl {
+
+// Combine the per-wave states in LDS: global max first, then one accumulation pass (one
+// exp2 per wave, short live ranges).  A NaN max anywhere poisons the row.
+template <int NW>
+__device__ __forceinline__ Lse block_combine(const float (*red)[3], float c) {
+  float M = red[0][0];
+  bool bad = M != M;
+#pragma unroll
+  for (int w = 1; w < NW; ++w) {
+    const float m = red[w][0];
+    M = fmaxf(M, m);
+    bad |= m != m;
+  }
+  float S = 0.f, W = 0.f;
+#pragma unroll 4
+  for (int w = 0; w < NW; ++w) {
+    const float d = (red[w][0] - M) * c;
+    const float f = fexp2(d);
+    const float sw = red[w][1];
+    S = __builtin_fmaf(sw, f, S);
+    W = __builtin_fmaf(f, __builtin_fmaf(sw, d, red[w][2]), W);
+  }
+  if (bad) S = __builtin_nanf("");
+  return Lse{M, S, W};
+}
+
+// per-row epilogue shared by the forward kernels: every lane computes the (uniform) token
+// values and gradient coefficients; `writer` stores the per-row outputs.
+__device__ __forceinline__ TokGrad row_epilogue(const KArgs& a, int64_t q, int64_t tok, float lp,
+                                                float H, float lse, bool writer) {
+  const TokVals v = token_values(a, tok, lp, H);
+  const TokGrad g = token_grad(a, v);
+  if (writer) {
+    a.o_lp[q] = lp;
+    a.o_ent[q] = H;
+    a.o_lse[q] = lse;
+    a.o_tok[q] = v.tl;
+    a.o_glp[q] = g.g_lp;
+    a.o_gh[q] = g.g_h;
+  }
+  return g;
+}
+
+// buffer descriptor over one row (wave-uniform inputs only); out-of-range lanes read 0 and
+// their stores are dropped by the hardware bounds check
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void* p, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+constexpr int kAuxNT = 2;           // nontemporal: the logits / dlogits stream once
+constexpr uint32_t kPadBf16x2 = 0xF1CAF1CAu;  // two bf16 -1.0e30: contributes 2^-huge = 0
+
+template <int NV>
+__global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
+  constexpr int BLOCK = 1024, NW = BLOCK / 64;
+  constexpr int VSTRIDE = BLOCK * 16;  // bytes between a lane's consecutive vectors
+  __shared__ float red[2][NW][3];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int64_t nrows = a.B * (a.L - 1);
+  const int nvec = (int)(a.V >> 3);
+  const int64_t row_bytes = a.V * 2;
+  const float c = kLog2e / a.temperature;
+  const float inv_t = 1.0f / a.temperature;
+  const uint16_t* __restrict__ lg = static_cast<const uint16_t*>(a.logits);
+  uint16_t* __restrict__ dl = static_cast<uint16_t*>(a.dlogits);
+  const int voff = tid * 16;
+  const bool last_ok = (NV - 1) * BLOCK + tid < nvec;  // only vector NV-1 can be partial
+
+  u32x4 buf[NV];
+  int64_t q = blockIdx.x;
+  if (q < nrows) {
+    int64_t lrow, tok;
+    row_of(a, q, lrow, tok);
+    const auto rs = row_rsrc(lg + lrow * a.ld, row_bytes);
+#pragma unroll
+    for (int k = 0; k < NV; ++k)
+      buf[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, k * VSTRIDE, kAuxNT));
+  }
+  int par = 0;
+  for (; q < nrows; q += gridDim.x, par ^= 1) {
+    int64_t lrow, tok;
+    row_of(a, q, lrow, tok);
+    const int64_t tid_raw = a.input_ids[tok];
+    const bool bad_id = (uint64_t)tid_raw >= (uint64_t)a.V;
+    const int64_t tgt = bad_id ? -1 : tid_raw;  // -1: never matches a column below
+    const float xt = bad_id ? __builtin_nanf("") : bf_to_f(lg[lrow * a.ld + tgt]);
+
+    // ---- pass 1: row statistics from registers
+    Lse st = lse_empty();
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      u32x4 v = buf[k];
+      if (k == NV - 1 && !last_ok) v = u32x4{kPadBf16x2, kPadBf16x2, kPadBf16x2, kPadBf16x2};
+      float x[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        x[2 * j] = bf_lo(v[j]);
+        x[2 * j + 1] = bf_hi(v[j]);
+      }
+      lse_add<8>(st, x, c);
+    }
+    st = wave_reduce_lse(st, c);
+    if (lane == 0) {
+      red[par][wid][0] = st.m;
+      red[par][wid][1] = st.s;
+      red[par][wid][2] = st.w;
+    }
+    __syncthreads();
+    const Lse tot = block_combine<NW>(red[par], c);
+    const float l2s = log2f(tot.s);
+    const float K = tot.m * c + l2s;
+    const float lse = tot.m * inv_t + kLn2 * l2s;
+    const float H = kLn2 * (l2s - tot.w / tot.s);
+    const float lp = xt * inv_t - lse;
+    const TokGrad core = row_epilogue(a, q, tok, lp, H, lse, tid == 0);
+    // Make the packed row opaque here so the compiler re-unpacks it in pass 2 instead of
+    // keeping pass 1's unpacked floats alive (8 instead of 4 VGPRs per vector -> spills).
+#pragma unroll
+    for (int k = 0; k < NV; ++k) asm volatile("" : "+v"(buf[k]));
+
+    // ---- pass 2: gradient from registers; the next row streams into the freed registers
+    const int64_t qn = q + gridDim.x;
+    const bool has_next = qn < nrows;
+    int64_t nlrow = lrow;
+    if (has_next) {
+      int64_t nt;
+      row_of(a, qn, nlrow, nt);
+    }
+    const auto rn = row_rsrc(lg + nlrow * a.ld, has_next ? row_bytes : 0);
+    if (a.write_grad) {
+      const auto ws = row_rsrc(dl + lrow * a.ld, row_bytes);
+      const float alpha = -(core.g_lp + core.g_h * H) * inv_t;
+      const float beta = -core.g_h * kLn2 * inv_t;
+      const float gadd = core.g_lp * inv_t;
+      const int tv = tgt < 0 ? -1 : (int)(tgt >> 3);
+      const int te = (int)(tgt & 7);
+      const int kt = tv < 0 ? -1 : tv / BLOCK;
+      const int lt = tv - (kt < 0 ? 0 : kt) * BLOCK;
+      const bool zero_row = (core.g_lp == 0.f && core.g_h == 0.f);
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        u32x4 o;
+        if (zero_row) {
+          o = u32x4{0u, 0u, 0u, 0u};
+        } else {
+          float d[8];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float x0 = bf_lo(buf[k][j]), x1 = bf_hi(buf[k][j]);
+            const float t0 = __builtin_fmaf(x0, c, -K), t1 = __builtin_fmaf(x1, c, -K);
+            const float p0 = fexp2(t0), p1 = fexp2(t1);
+            d[2 * j] = p0 * __builtin_fmaf(beta, t0, alpha);
+            d[2 * j + 1] = p1 * __builtin_fmaf(beta, t1, alpha);
+          }
+          if (k == kt && tid == lt) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) d[j] += (j == te) ? gadd : 0.f;
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(d[2 * j], d[2 * j + 1]);
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, o),
+                                               ws, voff, k * VSTRIDE, kAuxNT);
+        buf[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rn, voff, k * VSTRIDE, kAuxNT));
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < NV; ++k)
+        buf[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rn, voff, k * VSTRIDE, kAuxNT));
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// generic streaming path: T = float (PRL_F32) or uint16_t (bf16); VEC elements per access
+template <typename T, int VEC>
+struct RowIO;
+template <>
+struct RowIO<uint16_t, 8> {
+  static __device__ __forceinline__ void load(const uint16_t* row, int64_t gv, float (&x)[8]) {
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row) + gv);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      x[2 * j] = bf_lo(v[j]);
+      x[2 * j + 1] = bf_hi(v[j]);
+    }
+  }
+  static __device__ __forceinline__ void store(uint16_t* row, int64_t gv, const float (&d)[8]) {
+    u32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(d[2 * j], d[2 * j + 1]);
+    __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(row) + gv);
+  }
+};
+template <>
+struct RowIO<float, 4> {
+  static __device__ __forceinline__ void load(const float* row, int64_t gv, float (&x)[4]) {
+    const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(row) + gv);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x[j] = v[j];
+  }
+  static __device__ __forceinline__ void store(float* row, int64_t gv, const float (&d)[4]) {
+    f32x4 o = {d[0], d[1], d[2], d[3]};
+    __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(row) + gv);
+  }
+};
+template <>
+struct RowIO<uint16_t, 1> {
+  static __device__ __forceinline__ void load(const uint16_t* row, int64_t gv, float (&x)[1]) { x[0] = bf_to_f(row[gv]); }
+  static __device__ __forceinline__ void store(uint16_t* row, int64_t gv, const float (&d)[1]) { row[gv] = f_to_bf(d[0]); }
+};
+template <>
+struct RowIO<float, 1> {
+  static __device__ __forceinline__ void load(const float* row, int64_t gv, float (&x)[1]) { x[0] = row[gv]; }
+  static __device__ __forceinline__ void store(float* row, int64_t gv, const float (&d)[1]) { row[gv] = d[0]; }
+};
+
+template <typename T>
+__device__ __forceinline__ float scalar_logit(const T* row, int64_t j);
+template <>
+__device__ __forceinline__ float scalar_logit<uint16_t>(const uint16_t* row, int64_t j) { return bf_to_f(row[j]); }
+template <>
+__device__ __forceinline__ float scalar_logit<float>(const float* row, int64_t j) { return row[j]; }
+
+// gradient of one vector: d_j = p_j (alpha + beta t_j) (+ gadd at the target column)
+template <int VEC>
+__device__ __forceinline__ void grad_vec(const float (&x)[VEC], float (&d)[VEC], float c, float K,
+                                         float alpha, float beta, int64_t base, int64_t tgt,
+                                         float gadd) {
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) {
+    const float t = __builtin_fmaf(x[j], c, -K);
+    d[j] = fexp2(t) * __builtin_fmaf(beta, t, alpha);
+    if (base + j == tgt) d[j] += gadd;
+  }
+}
+
+template <typename T, int VEC>
+__global__ __launch_bounds__(256) void grpo_fwd_stream(KArgs a) {
+  constexpr int BLOCK = 256, NW = BLOCK / 64;
+  __shared__ float red[2][NW][3];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int64_t nrows = a.B * (a.L - 1);
+  const int64_t nvec = a.V / VEC;
+  const float c = kLog2e / a.temperature;
+  const float inv_t = 1.0f / a.temperature;
+  const T* lg = static_cast<const T*>(a.logits);
+  T* dl = static_cast<T*>(a.dlogits);
+  int par = 0;
+  for (int64_t q = blockIdx.x; q < nrows; q += gridDim.x, par ^= 1) {
+    int64_t lrow, tok;
+    row_of(a, q, lrow, tok);
+    const T* row = lg + lrow * a.ld;
+    const int64_t tid_raw = a.input_ids[tok];
+    const bool bad_id = (uint64_t)tid_raw >= (uint64_t)a.V;
+    const int64_t tgt = bad_id ? -1 : tid_raw;
+    const float xt = bad_id ? __builtin_nanf("") : scalar_logit<T>(row, tgt);
+    Lse st = lse_empty();
+    for (int64_t gv = tid; gv < nvec; gv += BLOCK) {
+      float x[VEC];
+      RowIO<T, VEC>::load(row, gv, x);
+      lse_add<VEC>(st, x, c);
+    }
+    st = wave_reduce_lse(st, c);
+    if (lane == 0) {
+      red[par][wid][0] = st.m;
+      red[par][wid][1] = st.s;
+      red[par][wid][2] = st.w;
+    }
+    __syncthreads();
+    const Lse tot = block_combine<NW>(red[par], c);
+    const float l2s = log2f(tot.s);
+    const float K = tot.m * c + l2s;
+    const float lse = tot.m * inv_t + kLn2 * l2s;
+    const float H = kLn2 * (l2s - tot.w / tot.s);
+    const float lp = xt * inv_t - lse;
+    const TokGrad core = row_epilogue(a, q, tok, lp, H, lse, tid == 0);
+    if (a.write_grad) {
+      T* drow = dl + lrow * a.ld;
+      const float alpha = -(core.g_lp + core.g_h * H) * inv_t;
+      const float beta = -core.g_h * kLn2 * inv_t;
+      const float gadd = core.g_lp * inv_t;
+      const bool zero_row = (core.g_lp == 0.f && core.g_h == 0.f);
+      for (int64_t gv = tid; gv < nvec; gv += BLOCK) {
+        float d[VEC];
+        if (zero_row) {
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) d[j] = 0.f;
+        } else {
+          float x[VEC];
+          RowIO<T, VEC>::load(row, gv, x);
+          grad_vec<VEC>(x, d, c, K, alpha, beta, gv * VEC, tgt, gadd);
+        }
+        RowIO<T, VEC>::store(drow, gv, d);
+      }
+    }
+  }
+}
+
+// gradient pass from saved per-row coefficients for the upstream gradient *up (device);
+// skip_if_one: dlogits already holds the gradient for *up == 1 (fused forward)
+template <typename T, int VEC>
+__global__ __launch_bounds__(256) void grpo_bwd_stream(KArgs a, const float* lse_in,
+                                                       const float* ent_in, const float* glp_in,
+                                                       const float* gh_in, const float* up,
+                                                       int skip_if_one) {
+  constexpr int BLOCK = 256;
+  const float scale = up ? *up : 1.0f;
+  if (skip_if_one && scale == 1.0f) return;
+  const int tid = threadIdx.x;
+  const int64_t nrows = a.B * (a.L - 1);
+  const int64_t nvec = a.V / VEC;
+  const float c = kLog2e / a.temperature;
+  const float inv_t = 1.0f / a.temperature;
+  const T* lg = static_cast<const T*>(a.logits);
+  T* dl = static_cast<T*>(a.dlogits);
+  for (int64_t q = blockIdx.x; q < nrows; q += gridDim.x) {
+    int64_t lrow, tok;
+    row_of(a, q, lrow, tok);
+    const T* row = lg + lrow * a.ld;
+    T* drow = dl + lrow * a.ld;
+    const int64_t tid_raw = a.input_ids[tok];
+    const int64_t tgt = (uint64_t)tid_raw >= (uint64_t)a.V ? -1 : tid_raw;
+    const float g_lp = glp_in[q] * scale, g_h = gh_in[q] * scale;
+    const float H = ent_in[q];
+    const float K = lse_in[q] * kLog2e;  // K = m c + log2 s = LSE * log2(e)
+    const float alpha = -(g_lp + g_h * H) * inv_t;
+    const float beta = -g_h * kLn2 * inv_t;
+    const float gadd = g_lp * inv_t;
+    const bool zero_row = (g_lp == 0.f && g_h == 0.f);
+    for (int64_t gv = tid; gv < nvec; gv += BLOCK) {
+      float d[VEC];
+      if (zero_row) {
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) d[j] = 0.f;
+      } else {
+        float x[VEC];
+        RowIO<T, VEC>::load(row, gv, x);
+        grad_vec<VEC>(x, d, c, K, alpha, beta, gv * VEC, tgt, gadd);
+      }
+      RowIO<T, VEC>::store(drow, gv, d);
+    }
+  }
+}
+
+// Statistics (rl/__init__.py:315-375) and value-head gradient from the per-row outputs.
+// Block b owns rows [b*chunk, (b+1)*chunk); each thread folds its rows in a fixed order,
+// then the block folds threads in index order: deterministic for a given row count.
+constexpr int kStatThreads = 256;
+__global__ __launch_bounds__(kStatThreads) void grpo_stats_partial(KArgs a, int64_t chunk) {
+  __shared__ double sh[kStatThreads][PRL_NSTAT + 1];
+  const int tid = threadIdx.x;
+  const int64_t nrows = a.B * (a.L - 1);
+  double acc[PRL_NSTAT];
+#pragma unroll
+  for (int i = 0; i < PRL_NSTAT; ++i) acc[i] = stat_identity(i);
+  const int64_t r0 = (int64_t)blockIdx.x * chunk;
+  const int64_t r1 = r0 + chunk < nrows ? r0 + chunk : nrows;
+  const bool has_v = a.values != nullptr;
+  for (int64_t q = r0 + tid; q < r1; q += kStatThreads) {
+    int64_t lrow, tok;
+    row_of(a, q, lrow, tok);
+    const float lp = a.o_lp[q], H = a.o_ent[q];
+    const TokVals v = token_values(a, tok, lp, H);
+    const bool m = v.m;
+    const float reward = a.rewards[tok], ref = a.ref_lp[tok], old = a.old_lp[tok];
+    const float nl = a.num_labels[tok];
+    const int64_t tidv = a.input_ids[tok];
+    const float vp = has_v ? a.values[tok - 1] : 0.f;
+    float vl = 0.f;
+    if (has_v) {
+      const float dvr = vp - reward;
+      vl = 0.5f * (dvr * dvr) * v.w;  // :304
+      a.o_dv[tok - 1] = (m && __builtin_isfinite(vl)) ? a.gscale * a.value_coef * v.w * dvr : 0.f;
+    }
+    const float C = a.clampC;
+    float c[PRL_NSTAT];
+    // masked sums: rl/utils.py mask_sum -> m ? nan_to_num(v) : 0  (v / nl order kept)
+    c[PRL_S_LOSS_SUM] = m ? nz(v.tl) : 0.f;
+    c[PRL_S_VALUE_LOSS] = m ? nz(vl) : 0.f;
+    c[PRL_S_REWARD] = m ? nz(reward / nl) : 0.f;
+    c[PRL_S_ENTROPY] = m ? nz(H / nl) : 0.f;
+    c[PRL_S_OLD_LP] = m ? nz(old / nl) : 0.f;
+    c[PRL_S_NEW_LP] = m ? nz(lp / nl) : 0.f;
+    c[PRL_S_REF_LP] = m ? nz(ref / nl) : 0.f;
+    c[PRL_S_ADVANTAGE] = m ? nz(v.adv / nl) : 0.f;
+    c[PRL_S_KL] = m ? nz(v.kl / nl) : 0.f;
+    c[PRL_S_POLICY_LOSS] = m ? nz(v.pol / nl) : 0.f;
+    c[PRL_S_SURR1] = m ? nz(v.s1 / nl) : 0.f;
+    c[PRL_S_SURR2] = m ? nz(v.s2 / nl) : 0.f;
+    c[PRL_S_RATIO] = m ? nz(v.ratio_used / nl) : 0.f;
+    c[PRL_S_RATIO_SUM] = m ? nz(v.ratio_used) : 0.f;
+    c[PRL_S_RATIO_SQ_SUM] = m ? nz(v.ratio_used * v.ratio_used) : 0.f;
+    c[PRL_S_RATIO_REF_NEW] = m ? nz(expf(v.lrrn) / nl) : 0.f;
+    c[PRL_S_RATIO_REF_OLD] = m ? nz(expf(ref - old) / nl) : 0.f;
+    c[PRL_S_CLAMP_REF_NEW] = m ? nz((fabsf(v.lrrn) > C ? 1.f : 0.f) / nl) : 0.f;  // :254
+    c[PRL_S_CLAMP_NEW_OLD] = m ? nz((v.ind_no ? 1.f : 0.f) / nl) : 0.f;
+    c[PRL_S_TOKEN_WEIGHT] = m ? nz(v.w / nl) : 0.f;
+    c[PRL_S_VALUE_MEAN] = (m && has_v) ? nz(vp / nl) : 0.f;
+    c[PRL_S_VALUE_MSE] = (m && has_v) ? nz(((vp - reward) * (vp - reward)) / nl) : 0.f;
+    c[PRL_S_NUM_NANS] = (v.tl != v.tl) ? 1.f : 0.f;
+    c[PRL_S_NUM_OUT] = m ? 1.f : 0.f;
+    c[PRL_S_BAD_LP] = __builtin_isfinite(lp) ? 0.f : 1.f;
+    c[PRL_S_BAD_LRRN] = __builtin_isfinite(v.lrrn) ? 0.f : 1.f;
+    c[PRL_S_BAD_KL] = __builtin_isfinite(v.kl) ? 0.f : 1.f;
+    c[PRL_S_BAD_GT] = (a.group_norm && !(a.group_tokens[tok] > 0.f)) ? 1.f : 0.f;
+    c[PRL_S_BAD_ID] = ((uint64_t)tidv >= (uint64_t)a.V) ? 1.f : 0.f;
+    const float ninf = -__builtin_inff(), pinf = __builtin_inff();
+    c[PRL_S_MAX_REWARD] = m ? reward : ninf;
+    c[PRL_S_MIN_REWARD] = m ? reward : pinf;
+    c[PRL_S_MAX_ADV] = m ? v.adv : ninf;
+    c[PRL_S_MIN_ADV] = m ? v.adv : pinf;
+    c[PRL_S_MAX_KL] = m ? v.kl : ninf;
+    c[PRL_S_MIN_KL] = m ? v.kl : pinf;
+    c[PRL_S_MAX_W] = m ? v.w : ninf;
+    c[PRL_S_MIN_W] = m ? v.w : pinf;
+    c[PRL_S_MAX_VALUE] = (m && has_v) ? vp : ninf;
+    c[PRL_S_MIN_VALUE] = (m && has_v) ? vp : pinf;
+#pragma unroll
+    for (int i = 0; i < PRL_NSTAT; ++i) acc[i] = stat_fold(i, acc[i], (double)c[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < PRL_NSTAT; ++i) sh[tid][i] = acc[i];
+  __syncthreads();
+  if (tid < PRL_NSTAT) {
+    double r = stat_identity(tid);
+    for (int t = 0; t < kStatThreads; ++t) r = stat_fold(tid, r, sh[t][tid]);
+    a.partials[(int64_t)blockIdx.x * PRL_NSTAT + tid] = r;
+  }
+}
+
+__global__ void grpo_finalize(const double* __restrict__ partials, int nblocks,
+                              double* __restrict__ stats) {
+  const int i = threadIdx.x;
+  if (i >= PRL_NSTAT) return;
+  double acc = stat_identity(i);
+  for (int b = 0; b < nblocks; ++b) acc = stat_fold(i, acc, partials[(int64_t)b * PRL_NSTAT + i]);
+  stats[i] = acc;
+}
+
+// ---------------------------------------------------------------------------------------
+// host side
+struct DevInfo {
+  int cus = 0;
+};
+static DevInfo g_dev[64];
+
+static int device_cus(int dev) {
+  if (dev < 0 || dev >= 64) return 256;
+  if (g_dev[dev].cus == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    g_dev[dev].cus = n;
+  }
+  return g_dev[dev].cus;
+}
+
+static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+static int fill_args(KArgs& a, const PrlGrpoBatch* b, const PrlGrpoParams* p) {
+  if (!b || !p) return PRL_E_INVALID;
+  if (b->B < 1 || b->L < 1 || b->V < 1 || b->ld < b->V) return PRL_E_INVALID;
+  if (!b->logits || !b->input_ids || !b->labels || !b->rewards || !b->advantages || !b->ref_logprobs ||
+      !b->old_logprobs || !b->group_tokens || !b->num_labels || !b->overflow)
+    return PRL_E_INVALID;
+  if (b->logits_dtype != PRL_BF16 && b->logits_dtype != PRL_F32) return PRL_E_UNSUPPORTED;
+  if (p->policy_loss != PRL_PPO && p->policy_loss != PRL_REINFORCE) return PRL_E_INVALID;
+  a = KArgs{};
+  a.logits = b->logits;
+  a.B = b->B;
+  a.L = b->L;
+  a.V = b->V;
+  a.ld = b->ld;
+  a.input_ids = b->input_ids;
+  a.labels = b->labels;
+  a.rewards = b->rewards;
+  a.advantages = b->advantages;
+  a.ref_lp = b->ref_logprobs;
+  a.old_lp = b->old_logprobs;
+  a.group_tokens = b->group_tokens;
+  a.num_labels = b->num_labels;
+  a.overflow = b->overflow;
+  a.values = b->values;
+  a.policy = p->policy_loss;
+  a.use_adv = p->use_advantages;
+  a.relu = p->relu_log_p_weights;
+  a.group_norm = p->group_normalization;
+  a.overlong = p->overlong_filtering;
+  a.write_grad = p->write_grad;
+  a.eps = p->epsilon;
+  a.kl_c = p->kl_coef;
+  a.ent_c = p->entropy_coef;
+  a.clampC = p->clamp_log_ratio;
+  a.temperature = p->temperature;
+  a.batch_size = p->batch_size;
+  a.value_coef = p->value_loss_coef;
+  a.gscale = p->grad_scale;
+  return PRL_OK;
+}
+
+constexpr int kMaxNV = 24;
+static int resident_nv(int64_t nvec) {
+  const int64_t nv = (nvec + 1023) / 1024;
+  return nv <= kMaxNV ? (int)nv : 0;
+}
+
+template <int NV>
+static hipError_t launch_resident(const KArgs& a, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(grpo_fwd_resident<NV>, dim3(grid), dim3(1024), 0, s, a);
+  return hipGetLastError();
+}
+
+template <int... NVs>
+static hipError_t launch_resident_table(int nv, const KArgs& a, int grid, hipStream_t s,
+                                        std::integer_sequence<int, NVs...>) {
+  hipError_t e = hipErrorInvalidValue;
+  ((nv == NVs + 1 ? (e = launch_resident<NVs + 1>(a, grid, s), true) : false) || ...);
+  return e;
+}
+
+static hipError_t launch_resident_nv(int nv, const KArgs& a, int grid, hipStream_t s) {
+  return launch_resident_table(nv, a, grid, s, std::make_integer_sequence<int, kMaxNV>{});
+}
+
+}  // namespace prl
+
+using namespace prl;
+
+extern "C" {
+
+int prl_abi_version(void) { return PRL_ABI_VERSION; }
+
+const char* prl_error_string(int code) {
+  switch (code) {
+    case PRL_OK: return "ok";
+    case PRL_E_INVALID: return "invalid argument";
+    case PRL_E_UNSUPPORTED: return "unsupported dtype or layout";
+    case PRL_E_WORKSPACE: return "workspace too small";
+    default: return hipGetErrorString(static_cast<hipError_t>(code));
+  }
+}
+
+int prl_grpo_workspace_bytes(int device, size_t* bytes) {
+  (void)device;
+  if (!bytes) return PRL_E_INVALID;
+  *bytes = sizeof(double) * (size_t)kMaxGrid * PRL_NSTAT;
+  return PRL_OK;
+}
+
+int prl_grpo_forward(const PrlGrpoBatch* batch, const PrlGrpoParams* params,
+                     const PrlGrpoOutputs* out, void* workspace, size_t workspace_bytes,
+                     void* stream) {
+  KArgs a;
+  int rc = fill_args(a, batch, params);
+  if (rc) return rc;
+  if (!out || !out->new_logprobs || !out->entropy || !out->lse || !out->token_loss || !out->g_lp ||
+      !out->g_h || !out->stats)
+    return PRL_E_INVALID;
+  if (batch->values && !out->dvalues) return PRL_E_INVALID;
+  if (params->write_grad && !out->dlogits) return PRL_E_INVALID;
+  if (!workspace || workspace_bytes < sizeof(double) * (size_t)kMaxGrid * PRL_NSTAT) return PRL_E_WORKSPACE;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  a.o_lp = out->new_logprobs;
+  a.o_ent = out->entropy;
+  a.o_lse = out->lse;
+  a.o_tok = out->token_loss;
+  a.o_glp = out->g_lp;
+  a.o_gh = out->g_h;
+  a.o_dv = out->dvalues;
+  a.dlogits = out->dlogits;
+  a.partials = static_cast<double*>(workspace);
+  const size_t es = batch->logits_dtype == PRL_BF16 ? 2 : 4;
+  hipError_t e;
+  if (batch->values) {
+    e = hipMemsetAsync(out->dvalues, 0, sizeof(float) * (size_t)(batch->B * batch->L), s);
+    if (e != hipSuccess) return (int)e;
+  }
+  if (params->write_grad) {  // rows t = L-1 carry no loss: zero them (pitch = one sequence)
+    char* last = static_cast<char*>(out->dlogits) + (size_t)(batch->L - 1) * batch->ld * es;
+    e = hipMemset2DAsync(last, (size_t)batch->L * batch->ld * es, 0, (size_t)batch->V * es,
+                         (size_t)batch->B, s);
+    if (e != hipSuccess) return (int)e;
+  }
+  const int64_t nrows = batch->B * (batch->L - 1);
+  int dev = 0;
+  hipGetDevice(&dev);
+  const int cus = device_cus(dev);
+  int grid = 0;
+  if (nrows > 0) {
+    const bool bf16 = batch->logits_dtype == PRL_BF16;
+    const bool vec_ok_bf = bf16 && batch->V % 8 == 0 && batch->ld % 8 == 0 && aligned16(batch->logits) &&
+                           (!params->write_grad || aligned16(out->dlogits));
+    const int nv = vec_ok_bf ? resident_nv(batch->V / 8) : 0;  // row <= 24*16 KiB
+    if (nv > 0) {
+      grid = (int)(nrows < cus ? nrows : cus);
+      e = launch_resident_nv(nv, a, grid, s);
+    } else {
+      const int64_t want = (int64_t)cus * 4;
+      grid = (int)(nrows < want ? nrows : want);
+      if (grid > kMaxGrid) grid = kMaxGrid;
+      if (vec_ok_bf) {
+        hipLaunchKernelGGL((grpo_fwd_stream<uint16_t, 8>), dim3(grid), dim3(256), 0, s, a);
+      } else if (bf16) {
+        hipLaunchKernelGGL((grpo_fwd_stream<uint16_t, 1>), dim3(grid), dim3(256), 0, s, a);
+      } else if (batch->V % 4 == 0 && batch->ld % 4 == 0 && aligned16(batch->logits) &&
+                 (!params->write_grad || aligned16(out->dlogits))) {
+        hipLaunchKernelGGL((grpo_fwd_stream<float, 4>), dim3(grid), dim3(256), 0, s, a);
+      } else {
+        hipLaunchKernelGGL((grpo_fwd_stream<float, 1>), dim3(grid), dim3(256), 0, s, a);
+      }
+      e = hipGetLastError();
+    }
+    if (e != hipSuccess) return (int)e;
+  }
+  // statistics + value gradient: fixed row chunks per block (deterministic)
+  int sblocks = 0;
+  if (nrows > 0) {
+    int64_t chunk = (nrows + kMaxGrid - 1) / kMaxGrid;
+    if (chunk < 1024) chunk = 1024;
+    sblocks = (int)((nrows + chunk - 1) / chunk);
+    hipLaunchKernelGGL(grpo_stats_partial, dim3(sblocks), dim3(kStatThreads), 0, s, a, chunk);
+    e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+  }
+  hipLaunchKernelGGL(grpo_finalize, dim3(1), dim3(64), 0, s, a.partials, sblocks, out->stats);
+  return (int)hipGetLastError();
+}
+
+int prl_grpo_backward(const PrlGrpoBatch* batch, const PrlGrpoParams* params, const float* lse,
+                      const float* entropy, const float* g_lp, const float* g_h, const float* upstream,
+                      void* dlogits, void* stream) {
+  KArgs a;
+  int rc = fill_args(a, batch, params);
+  if (rc) return rc;
+  if (!lse || !entropy || !g_lp || !g_h || !dlogits) return PRL_E_INVALID;
+  a.dlogits = dlogits;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int skip = params->write_grad ? 1 : 0;
+  if (!skip) {  // rows t = L-1 carry no loss
+    const size_t es = batch->logits_dtype == PRL_BF16 ? 2 : 4;
+    char* last = static_cast<char*>(dlogits) + (size_t)(batch->L - 1) * batch->ld * es;
+    hipError_t e = hipMemset2DAsync(last, (size_t)batch->L * batch->ld * es, 0, (size_t)batch->V * es,
+                                    (size_t)batch->B, s);
+    if (e != hipSuccess) return (int)e;
+  }
+  const int64_t nrows = batch->B * (batch->L - 1);
+  if (nrows == 0) return PRL_OK;
+  int dev = 0;
+  hipGetDevice(&dev);
+  const int64_t want = (int64_t)device_cus(dev) * 8;
+  const int grid = (int)(nrows < want ? nrows : want);
+  const bool bf16 = batch->logits_dtype == PRL_BF16;
+  if (bf16 && batch->V % 8 == 0 && batch->ld % 8 == 0 && aligned16(batch->logits) && aligned16(dlogits)) {
+    hipLaunchKernelGGL((grpo_bwd_stream<uint16_t, 8>), dim3(grid), dim3(256), 0, s, a, lse, entropy, g_lp, g_h, upstream, skip);
+  } else if (bf16) {
+    hipLaunchKernelGGL((grpo_bwd_stream<uint16_t, 1>), dim3(grid), dim3(256), 0, s, a, lse, entropy, g_lp, g_h, upstream, skip);
+  } else if (batch->V % 4 == 0 && batch->ld % 4 == 0 && aligned16(batch->logits) && aligned16(dlogits)) {
+    hipLaunchKernelGGL((grpo_bwd_stream<float, 4>), dim3(grid), dim3(256), 0, s, a, lse, entropy, g_lp, g_h, upstream, skip);
+  } else {
+    hipLaunchKernelGGL((grpo_bwd_stream<float, 1>), dim3(grid), dim3(256), 0, s, a, lse, entropy, g_lp, g_h, upstream, skip);
+  }
+  return (int)hipGetLastError();
+}
+
+int prl_grpo_nstat(void) { return PRL_NSTAT; }
+
+}  // extern "C"

@@ -1,0 +1,211 @@
+"""GRPO / PPO / REINFORCE objective on MI355X — mirror of pipelinerl/finetune/rl/__init__.py.
+
+Drop-in surface (same names, arguments, return values and errors as the reference):
+  RLConfig            rl/__init__.py:38-99   (unknown keys ignored, like pydantic there)
+  linear_decay_coef   rl/__init__.py:113-127
+  rl_step             rl/__init__.py:130-377 -> (loss tensor, dict[str, float])
+  populate_rl_data    rl/__init__.py:380-501
+  prepare_rl_fields   rl/__init__.py:504-525
+
+rl_step runs the model forward WITHOUT ``labels`` (the reference passes them, which makes HF
+compute and discard a full fp32 cross-entropy over [T, V]; rl/__init__.py:183-197), then the
+fused HIP loss head (fused.py).  It syncs with the device once, to read the ~40 statistics
+(the reference issues ~30 ``.item()`` calls).
+"""
+
+from __future__ import annotations
+
+import logging
+import math
+from typing import Any
+
+import numpy as np
+import torch
+from pydantic import BaseModel, Field
+
+from ..types import PipelineBatchEncoding
+from .fused import GrpoParams, grpo_loss, prepare_fields
+from ..._native import S
+
+logger = logging.getLogger(__name__)
+
+RL_DATA_COLUMNS = ["overflow", "group_tokens", "num_labels", "rewards", "advantages", "old_logprobs",
+                   "ref_logprobs"]
+
+
+class RLConfig(BaseModel):
+    policy_loss: str = Field(default="ppo", description="Policy Loss to use for RL")
+    use_advantages: bool = Field(default=True)
+    epsilon: float = Field(default=0.2)
+    batch_size: int = Field(default=0)
+    reward_minus_kl_coef: float = Field(default=0.0)
+    kl_coef: float = Field(default=0.1)
+    final_kl_coef: float = Field(default=0.1)
+    entropy_bonus: float = Field(default=0.0)
+    final_entropy_bonus: float = Field(default=0.0)
+    relu_log_p_weights: bool = Field(default=False)
+    clamp_log_ratio_ref_new_value: float = Field(default=10)
+    divide_advantage_by_std: bool = Field(default=True)
+    overlong_filtering: bool = Field(default=False)
+    group_normalization: bool = Field(default=False)
+    temperature: float = Field(default=1.0)
+    filter_zero_advantage_groups: bool = Field(default=False)
+    value_loss_coef: float = Field(default=0.0)
+
+
+def linear_decay_coef(current_step: int, max_step: int, initial_coef: float, final_coef: float) -> float:
+    return initial_coef + (final_coef - initial_coef) * current_step / max_step
+
+
+def _num_sequences_device(batch: PipelineBatchEncoding) -> torch.Tensor | int:
+    """rl/__init__.py:158-181 without a host sync (packed: #(position_ids == 0), index 0 forced)."""
+    if batch.is_packed:
+        pos = batch.position_ids[0]
+        return (pos == 0).sum() + (pos[0] != 0).to(torch.long)
+    return int(batch.labels.shape[0])
+
+
+def rl_step(model, batch: PipelineBatchEncoding, current_step: int, max_step: int,
+            config: RLConfig) -> tuple[torch.Tensor, dict[str, float]]:
+    """One RL micro-batch: model forward + fused loss head.  Returns (loss, stats)."""
+    if config.policy_loss not in ("ppo", "reinforce"):
+        raise ValueError(f"Unknown algorithm {config.policy_loss}")
+    has_value_head = hasattr(model, "value_head")
+
+    model_inputs = {"input_ids": batch.input_ids, "attention_mask": batch.attention_mask}
+    if batch.is_packed:
+        model_inputs["position_ids"] = batch.position_ids
+    if getattr(batch, "pixel_values", None) is not None:
+        model_inputs["pixel_values"] = batch.pixel_values
+    if getattr(batch, "image_grid_thw", None) is not None:
+        model_inputs["image_grid_thw"] = batch.image_grid_thw
+    outputs = model(**model_inputs)
+    logits = outputs.logits
+    values = outputs.value if has_value_head else None
+
+    ent_c = linear_decay_coef(current_step, max_step, config.entropy_bonus, config.final_entropy_bonus)
+    kl_c = linear_decay_coef(current_step, max_step, config.kl_coef, config.final_kl_coef)
+    params = GrpoParams(
+        policy_loss=config.policy_loss, use_advantages=config.use_advantages,
+        relu_log_p_weights=config.relu_log_p_weights, group_normalization=config.group_normalization,
+        overlong_filtering=config.overlong_filtering, epsilon=config.epsilon, kl_coef=kl_c, entropy_coef=ent_c,
+        clamp_log_ratio=float(config.clamp_log_ratio_ref_new_value), temperature=config.temperature,
+        batch_size=float(config.batch_size), value_loss_coef=config.value_loss_coef if has_value_head else 0.0)
+    fields = prepare_fields(batch, logits.device)
+    loss, stats_dev, _ = grpo_loss(logits, fields, params, values)
+
+    nseq = _num_sequences_device(batch)
+    if isinstance(nseq, torch.Tensor):
+        host = torch.cat([stats_dev, nseq.to(stats_dev.device, torch.float64).reshape(1)]).cpu().numpy()
+        num_sequences = int(host[-1])
+    else:
+        host = stats_dev.cpu().numpy()
+        num_sequences = nseq
+    return loss, build_stats(host, batch, params, kl_c, ent_c, num_sequences, has_value_head)
+
+
+def build_stats(h: np.ndarray, batch, params: GrpoParams, kl_c: float, ent_c: float, num_sequences: int,
+                has_value_head: bool) -> dict[str, float]:
+    """Assertions (in the reference's order) and the stats dict of rl/__init__.py:315-375."""
+    if batch.is_packed and num_sequences <= 0:
+        raise AssertionError("No sequences found in packed batch")
+    if h[S["BAD_ID"]] > 0:
+        raise RuntimeError("index out of bounds in gather: a target token id is outside [0, vocab)")
+    if h[S["BAD_LP"]] > 0:
+        raise AssertionError(f"new_logprobs is not finite: {int(h[S['BAD_LP']])} non-finite values")
+    if params.group_normalization and h[S["BAD_GT"]] > 0:
+        raise AssertionError("group_tokens must be greater than zero for group normalization")
+    if h[S["BAD_LRRN"]] > 0:
+        raise AssertionError(f"log_ratio_ref_new is not finite: {int(h[S['BAD_LRRN']])} non-finite values")
+    if h[S["BAD_KL"]] > 0:
+        raise AssertionError(f"approx_kl is not finite: {int(h[S['BAD_KL']])} non-finite values")
+    policy_loss_total = np.float32(-h[S["LOSS_SUM"]])
+    final = float(np.float32(policy_loss_total + np.float32(params.value_loss_coef) * np.float32(h[S["VALUE_LOSS"]]))) \
+        if has_value_head else float(policy_loss_total)
+    if not math.isfinite(final):
+        raise AssertionError(f"Non-finite loss detected: {final}")
+    input_size = int(batch.input_ids.numel())
+    if h[S["NUM_OUT"]] == 0:
+        return {"input_size": float(input_size)}
+    f = lambda k: float(h[S[k]])  # noqa: E731
+    stats = {
+        "loss": final, "max_loss": final, "min_loss": final,
+        "reward": f("REWARD"), "max_reward": f("MAX_REWARD"), "min_reward": f("MIN_REWARD"),
+        "entropy": f("ENTROPY"), "old_logprobs": f("OLD_LP"), "new_logprobs": f("NEW_LP"),
+        "ref_logprobs": f("REF_LP"), "advantage": f("ADVANTAGE"), "max_advantage": f("MAX_ADV"),
+        "min_advantage": f("MIN_ADV"), "kl": f("KL"), "max_kl": f("MAX_KL"), "min_kl": f("MIN_KL"),
+        "policy_loss": f("POLICY_LOSS"), "surr1": f("SURR1"), "surr2": f("SURR2"),
+        "ratio_new_old": f("RATIO"), "ratio_new_old_sum": f("RATIO_SUM"),
+        "ratio_new_old_squared_sum": f("RATIO_SQ_SUM"), "ratio_ref_new": f("RATIO_REF_NEW"),
+        "ratio_ref_old": f("RATIO_REF_OLD"), "clamp_log_ratio_ref_new_indicator": f("CLAMP_REF_NEW"),
+        "clamp_log_ratio_new_old_indicator": f("CLAMP_NEW_OLD"), "num_nans": int(h[S["NUM_NANS"]]),
+        "token_weight": f("TOKEN_WEIGHT"), "max_token_weight": f("MAX_W"), "min_token_weight": f("MIN_W"),
+        "kl_coef": num_sequences * kl_c, "entropy_bonus_coef": num_sequences * ent_c,
+        "num_output_tokens_sum": int(h[S["NUM_OUT"]]), "input_size": input_size,
+    }
+    if has_value_head:
+        stats["value_mean"] = f("VALUE_MEAN")
+        stats["value_max"] = f("MAX_VALUE")
+        stats["value_min"] = f("MIN_VALUE")
+        stats["value_loss"] = float(np.float32(h[S["VALUE_LOSS"]]))
+        stats["value_mse"] = f("VALUE_MSE")
+    return stats
+
+
+# ---------------------------------------------------------------------------------------------
+# preprocessing-side RL fields (run in the preprocessor workers, CPU)
+
+def populate_rl_data(dataset: list[dict[str, Any]], eos_token_id: int, config: RLConfig) -> list[dict[str, Any]]:
+    """Group advantages, group_tokens, overflow and num_labels (rl/__init__.py:380-501).
+
+    Groups are keyed by (group_id, step_index); mean and sample std (ddof=1, NaN for a single
+    rollout) of each rollout's first-token reward; advantage = r - mean, or
+    (r - mean) / (nan_to_num(std) + 1e-4) when divide_advantage_by_std.
+    """
+    keys = [f"{e['group_id']}_{e['step_index']}" for e in dataset]
+    first_reward: dict[tuple[str, Any], float] = {}
+    for k, e in zip(keys, dataset):
+        r0 = e["rewards"][0]
+        prev = first_reward.setdefault((k, e["rollout_index"]), r0)
+        assert prev == r0, "rewards must be the same for every step of a rollout"
+    groups: dict[str, list[int]] = {}
+    for i, k in enumerate(keys):
+        groups.setdefault(k, []).append(i)
+    gstats = {}
+    for k, idx in groups.items():
+        rs = np.array([dataset[i]["rewards"][0] for i in idx], dtype=np.float64)
+        ns = np.array([len(dataset[i]["input_ids"]) for i in idx], dtype=np.float64)
+        std = float(rs.std(ddof=1)) if rs.size > 1 else float("nan")
+        gstats[k] = (float(rs.mean()), std, float(ns.mean()))
+    zero_var = sum(1 for m, s, _ in gstats.values() if not (s >= 1e-6))
+    if zero_var:
+        logger.warning(f"Found {zero_var} groups with zero variance!")
+    for k, e in zip(keys, dataset):
+        mean, std, gt = gstats[k]
+        if config.divide_advantage_by_std:
+            denom = (0.0 if math.isnan(std) else std) + 1e-4
+            e["advantages"] = [(r - mean) / denom for r in e["rewards"]]
+        else:
+            e["advantages"] = [(r - mean) for r in e["rewards"]]
+        n = len(e["input_ids"])
+        e["group_tokens"] = [gt] * n
+        e["overflow"] = [0.0 if eos_token_id in e["input_ids"] else 1.0] * len(e["overflow"])
+        e["num_labels"] = [sum(1 for lab in e["labels"] if lab != -100)] * n
+    return dataset
+
+
+def prepare_rl_fields(encoding: dict[str, Any], reward: float, old_logprobs: list[float],
+                      ref_logprobs: list[float]) -> dict[str, Any]:
+    """Per-token reward / log-prob fields for one rollout (rl/__init__.py:504-525)."""
+    labels = encoding["labels"]
+    n_target = sum(1 for t in labels if t != -100)
+    assert n_target == len(old_logprobs), f"Target tokens: {n_target}, old logprobs: {len(old_logprobs)}"
+    n = len(labels)
+    encoding["rewards"] = [reward] * n
+    encoding["advantages"] = [0.0] * n
+    encoding["old_logprobs"] = [0] * (n - len(old_logprobs)) + list(old_logprobs)
+    encoding["ref_logprobs"] = [0] * (n - len(ref_logprobs)) + list(ref_logprobs)
+    encoding["overflow"] = [0] * n
+    encoding["group_tokens"] = [0] * n
+    encoding["num_labels"] = [1 if t != -100 else 0 for t in labels]
+    return encoding

@@ -1,0 +1,51 @@
+"""The C-ABI library loads without a GPU and exports every symbol include/prl_hip.h declares;
+the Python binding's statistic table matches the header's enum."""
+
+import ctypes
+import re
+
+from conftest import ROOT
+
+
+def test_library_exports_header_symbols():
+    from pipelinerl_amd import _native
+
+    lib = _native.load()
+    declared = _native.header_symbols()
+    assert len(declared) >= 9
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert lib.prl_abi_version() == 1
+    assert lib.prl_grpo_nstat() == _native.NSTAT
+    assert lib.prl_error_string(1001).decode() == "invalid argument"
+    nbytes = ctypes.c_size_t(0)
+    assert lib.prl_grpo_workspace_bytes(0, ctypes.byref(nbytes)) == 0 and nbytes.value > 0
+
+
+def test_stat_enum_matches_header():
+    from pipelinerl_amd import _native
+
+    text = (ROOT / "include" / "prl_hip.h").read_text()
+    body = text[text.index("enum PrlStat {"):text.index("PRL_NSTAT\n")]
+    names = re.findall(r"PRL_S_(\w+)", body)
+    assert names == _native.STATS
+
+
+def test_struct_layouts():
+    from pipelinerl_amd import _native
+
+    assert ctypes.sizeof(_native.PrlGrpoBatch) == 8 + 4 + 4 + 4 * 8 + 10 * 8
+    assert ctypes.sizeof(_native.PrlGrpoParams) == 6 * 4 + 8 * 4
+    assert ctypes.sizeof(_native.PrlGrpoOutputs) == 9 * 8
+
+
+def test_invalid_arguments_rejected_without_gpu():
+    from pipelinerl_amd import _native
+
+    lib = _native.load()
+    b = _native.PrlGrpoBatch()
+    p = _native.PrlGrpoParams()
+    o = _native.PrlGrpoOutputs()
+    # null pointers / zero shapes are rejected before any device call
+    assert lib.prl_grpo_forward(ctypes.byref(b), ctypes.byref(p), ctypes.byref(o), None, 0, None) == 1001
+    assert lib.prl_flatten_bf16(None, None, None, None, -1, None, None) == 1001

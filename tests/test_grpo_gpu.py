@@ -1,0 +1,282 @@
+"""GPU parity of the fused GRPO loss head (HIP, through the C ABI) against the reference.
+
+Anchors: golden vectors produced by the reference rl_step (tests/golden/make_golden.py) and the
+pinned numpy oracle (oracle/grpo_oracle.py).  Tolerances (BASELINE.json north_star):
+  fp32 logits: loss / stats / log-probs / entropy within 1e-4 (relative to max(1, |x|)),
+               dlogits within 1e-6 + 1e-4 |d|;
+  bf16 logits: vs an fp32 computation on the same bf16 values: 1e-4 on log-probs / entropy,
+               dlogits (stored bf16) within 1e-2 relative + 1e-8 absolute;
+               vs the reference's own bf16 path: 1e-2 relative.
+"""
+
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, load_f1
+from gpu_helpers import LogitsModel, rel_close, to_batch
+from oracle import grpo_oracle, synth
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _run(logits, b, cfg, step, max_step, values=None, scale=1.0):
+    from pipelinerl_amd.finetune.rl import RLConfig, rl_step
+
+    model = LogitsModel(logits, values)
+    loss, stats = rl_step(model, to_batch(b), step, max_step, RLConfig(**cfg))
+    (loss * scale).backward() if scale != 1.0 else loss.backward()
+    torch.cuda.synchronize()
+    out = dict(loss=float(loss.item()), stats=stats, dlogits=model.logits.grad.float().cpu().numpy())
+    if values is not None:
+        out["dvalues"] = model.value_head.grad.float().cpu().numpy()
+    return out
+
+
+def _rows(logits, b, cfg, step, max_step, values=None):
+    from pipelinerl_amd.finetune.rl import RLConfig, linear_decay_coef
+    from pipelinerl_amd.finetune.rl.fused import GrpoParams, grpo_loss, prepare_fields
+
+    c = RLConfig(**cfg)
+    p = GrpoParams(policy_loss=c.policy_loss, use_advantages=c.use_advantages,
+                   relu_log_p_weights=c.relu_log_p_weights, group_normalization=c.group_normalization,
+                   overlong_filtering=c.overlong_filtering, epsilon=c.epsilon,
+                   kl_coef=linear_decay_coef(step, max_step, c.kl_coef, c.final_kl_coef),
+                   entropy_coef=linear_decay_coef(step, max_step, c.entropy_bonus, c.final_entropy_bonus),
+                   clamp_log_ratio=c.clamp_log_ratio_ref_new_value, temperature=c.temperature,
+                   batch_size=c.batch_size, value_loss_coef=c.value_loss_coef if values is not None else 0.0)
+    batch = to_batch(b)
+    _, _, rows = grpo_loss(logits, prepare_fields(batch, logits.device), p, values)
+    r = rows.cpu().numpy()
+    B, L = np.asarray(b["labels"]).shape
+    return r[0].reshape(B, L - 1), r[1].reshape(B, L - 1)
+
+
+def _check_stats(got, want, rtol=1e-4, what=""):
+    assert set(got) == set(want), (what, set(got) ^ set(want))
+    for k, v in want.items():
+        assert abs(got[k] - v) <= rtol * max(1.0, abs(v)), (what, k, got[k], v)
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_f1_all_cases(dtype):
+    batches, out, cases = load_f1()
+    for i, c in enumerate(cases):
+        b = batches[c["batch"]]
+        lg = b["logits"] if dtype == "fp32" else synth.to_bf16(b["logits"])
+        tdt = torch.float32 if dtype == "fp32" else torch.bfloat16
+        logits = torch.tensor(lg, dtype=torch.float32).to(tdt).to(DEV)
+        vals = torch.tensor(b["values"], device=DEV) if c["value_head"] else None
+        r = _run(logits, b, c["cfg"], c["step"], c["max_step"], vals)
+        if dtype == "fp32":  # straight against the reference's own outputs
+            _check_stats(r["stats"], c["stats"], 1e-4, f"case{i}")
+            assert abs(r["loss"] - c["loss"]) <= 1e-4 * max(1, abs(c["loss"]))
+            ok, err = rel_close(r["dlogits"], out[f"case{i}__dlogits"], 1e-4, 1e-6)
+            assert ok, (i, err)
+            if c["value_head"]:
+                ok, err = rel_close(r["dvalues"], out[f"case{i}__dvalues"], 1e-4, 1e-7)
+                assert ok, (i, err)
+            lp, H = _rows(logits.detach(), b, c["cfg"], c["step"], c["max_step"], vals)
+            ok, err = rel_close(lp, out[f"case{i}__new_logprobs"], 1e-5, 1e-5)
+            assert ok, (i, "lp", err)
+            ok, err = rel_close(H, out[f"case{i}__entropy"], 1e-5, 1e-5)
+            assert ok, (i, "H", err)
+        else:  # bf16 logits: against the pinned oracle on the same bf16 values
+            o = grpo_oracle.rl_step_oracle(lg, b, c["cfg"], c["step"], c["max_step"],
+                                           values=b["values"] if c["value_head"] else None)
+            _check_stats(r["stats"], o["stats"], 1e-4, f"case{i}")
+            ok, err = rel_close(r["dlogits"], o["dlogits"], 1e-2, 1e-8)
+            assert ok, (i, err)
+
+
+def _f2():
+    meta = json.loads((GOLDEN / "f2_meta.json").read_text())
+    from test_oracle_golden import f2_batch
+    _, lg, b = f2_batch()
+    return meta, lg, b
+
+
+def test_f2_full_vocab_bf16_resident_path():
+    """V = 151936, bf16: the register-resident kernel (19 x 16 B per lane)."""
+    meta, lg, b = _f2()
+    out = np.load(GOLDEN / "f2_outputs.npz")
+    logits = torch.tensor(lg, dtype=torch.float32).to(torch.bfloat16).to(DEV)
+    r = _run(logits, b, meta["cfg"], meta["step"], meta["max_step"])
+    ref = meta["fp32"]  # reference fp32 path on the same bf16-rounded logits
+    assert abs(r["loss"] - ref["loss"]) <= 1e-4 * max(1, abs(ref["loss"]))
+    _check_stats(r["stats"], ref["stats"], 1e-4, "f2 fp32")
+    lp, H = _rows(logits.detach(), b, meta["cfg"], meta["step"], meta["max_step"])
+    assert rel_close(lp, out["fp32__new_logprobs"], 1e-4, 1e-4)[0]
+    assert rel_close(H, out["fp32__entropy"], 1e-4, 1e-4)[0]
+    # the reference's own bf16 path rounds log_softmax to bf16: relative 1e-2
+    assert rel_close(lp, out["bf16__new_logprobs"], 1e-2, 1e-2)[0]
+    assert rel_close(H, out["bf16__entropy"], 1e-2, 1e-2)[0]
+    d = r["dlogits"][0].astype(np.float64)
+    T = meta["T"]
+    tgt = b["input_ids"][0, 1:]
+    assert rel_close(d[np.arange(T - 1), tgt], out["fp32__d_target"], 1e-2, 1e-8)[0]
+    assert rel_close(d[:, :1024], out["fp32__d_cols"], 1e-2, 1e-9)[0]
+    assert np.all(d[T - 1] == 0)
+
+
+@pytest.mark.parametrize("V,dtype", [(1000, "bf16"), (1001, "bf16"), (1001, "fp32"), (8 * 1024 * 3 + 8, "bf16"),
+                                     (152064, "bf16")])
+def test_kernel_paths_vs_oracle(V, dtype):
+    """Resident (bf16, V % 8 == 0), streaming vector and scalar paths, ragged last vector."""
+    T = 29
+    b = synth.packed_rl_batch(3, [10, 12, 7], [3, 4, 2], id_range=V, eos=5)
+    rng = np.random.default_rng(V)
+    lg = rng.normal(0, 2.0, (1, T, V)).astype(np.float32)
+    if dtype == "bf16":
+        lg = synth.to_bf16(lg)
+    b["old_logprobs"] = np.where(b["labels"] != -100, rng.normal(-7, 1, (1, T)), 0).astype(np.float32)
+    b["ref_logprobs"] = np.where(b["labels"] != -100, rng.normal(-7, 1, (1, T)), 0).astype(np.float32)
+    cfg = dict(policy_loss="ppo", kl_coef=0.05, entropy_bonus=0.02, final_entropy_bonus=0.02, epsilon=0.2,
+               batch_size=3, temperature=0.9, clamp_log_ratio_ref_new_value=5)
+    tdt = torch.float32 if dtype == "fp32" else torch.bfloat16
+    logits = torch.tensor(lg).to(tdt).to(DEV)
+    r = _run(logits, b, cfg, 0, 10)
+    o = grpo_oracle.rl_step_oracle(lg, b, cfg, 0, 10)
+    _check_stats(r["stats"], o["stats"], 1e-4, f"V={V}")
+    lp, H = _rows(logits.detach(), b, cfg, 0, 10)
+    assert rel_close(lp, o["new_logprobs"], 1e-5, 1e-4)[0]
+    assert rel_close(H, o["entropy"], 1e-5, 1e-4)[0]
+    tol = (1e-2, 1e-8) if dtype == "bf16" else (1e-4, 1e-7)
+    ok, err = rel_close(r["dlogits"], o["dlogits"], *tol)
+    assert ok, err
+
+
+def test_upstream_gradient_scale_and_sentinel():
+    batches, _, cases = load_f1()
+    b = batches["packed"]
+    c = cases[5]
+    for scale in (0.0, 0.25, -3.0):
+        logits = torch.tensor(b["logits"], device=DEV)
+        r = _run(logits, b, c["cfg"], c["step"], c["max_step"], scale=scale)
+        o = grpo_oracle.rl_step_oracle(b["logits"], b, c["cfg"], c["step"], c["max_step"], grad_out=scale)
+        ok, err = rel_close(r["dlogits"], o["dlogits"], 1e-4, 1e-7)
+        assert ok, (scale, err)
+        if scale == 0.0:
+            assert np.all(r["dlogits"] == 0)
+
+
+def test_errors_match_reference():
+    from pipelinerl_amd.finetune.rl import RLConfig, rl_step
+
+    batches, _, _ = load_f1()
+    b = batches["packed"]
+    with pytest.raises(ValueError):
+        rl_step(LogitsModel(torch.tensor(b["logits"], device=DEV)), to_batch(b), 0, 10,
+                RLConfig(policy_loss="nope", batch_size=4))
+    lg = b["logits"].copy()
+    lg[0, 3, 5] = np.nan
+    with pytest.raises(AssertionError):
+        rl_step(LogitsModel(torch.tensor(lg, device=DEV)), to_batch(b), 0, 10, RLConfig(batch_size=4))
+    bad = dict(b)
+    bad["input_ids"] = b["input_ids"].copy()
+    bad["input_ids"][0, 4] = 10 ** 6
+    with pytest.raises(RuntimeError):
+        rl_step(LogitsModel(torch.tensor(b["logits"], device=DEV)), to_batch(bad), 0, 10, RLConfig(batch_size=4))
+    gn = dict(b)
+    gn["group_tokens"] = np.zeros_like(b["group_tokens"])
+    with pytest.raises(AssertionError):
+        rl_step(LogitsModel(torch.tensor(b["logits"], device=DEV)), to_batch(gn), 0, 10,
+                RLConfig(batch_size=4, group_normalization=True))
+    nl = dict(b)
+    nl["labels"] = np.full_like(b["labels"], -100)
+    loss, stats = rl_step(LogitsModel(torch.tensor(b["logits"], device=DEV)), to_batch(nl), 0, 10,
+                          RLConfig(batch_size=4))
+    assert stats == {"input_size": float(b["input_ids"].size)}
+    assert float(loss) == 0.0
+
+
+def test_c2_scale_properties():
+    """Config C2 size (65536 packed rows x 151936 vocab, bf16): sampled rows vs the oracle,
+    softmax-gradient rows sum to ~0, and the kernel is bitwise deterministic."""
+    from pipelinerl_amd.finetune.rl.fused import GrpoParams, grpo_loss, prepare_fields
+
+    T, V = 65536, 151936
+    g = torch.Generator(device=DEV).manual_seed(0)
+    logits = (torch.randn((1, T, V), generator=g, device=DEV, dtype=torch.float32) * 3).to(torch.bfloat16)
+    logits.requires_grad_(True)
+    seq = 2048
+    nseq = T // seq
+    pos = torch.arange(T, device=DEV) % seq
+    ids = torch.randint(0, 151643, (1, T), generator=g, device=DEV)
+    labels = torch.where(pos[None] >= 256, ids, torch.full_like(ids, -100))
+    f = {"input_ids": ids, "labels": labels,
+         "rewards": torch.repeat_interleave(torch.randint(0, 2, (nseq,), device=DEV).float(), seq)[None],
+         "ref_logprobs": torch.randn((1, T), device=DEV) - 8, "old_logprobs": torch.randn((1, T), device=DEV) - 8,
+         "group_tokens": torch.full((1, T), float(seq), device=DEV),
+         "num_labels": torch.full((1, T), float(seq - 256), device=DEV), "overflow": torch.zeros((1, T), device=DEV)}
+    f["advantages"] = f["rewards"] - 0.5
+    f = {k: v.contiguous() for k, v in f.items()}
+    p = GrpoParams(policy_loss="ppo", epsilon=4.0, kl_coef=0.001, entropy_coef=0.0, clamp_log_ratio=5.0,
+                   batch_size=256.0)
+    loss1, stats1, rows1 = grpo_loss(logits, prepare_fields(f, logits.device), p)
+    loss1.backward()
+    d1 = logits.grad
+    logits.grad = None
+    loss2, stats2, rows2 = grpo_loss(logits, prepare_fields(f, logits.device), p)
+    loss2.backward()
+    assert torch.equal(stats1, stats2) and torch.equal(rows1, rows2)
+    assert torch.equal(d1, logits.grad)
+    # sum_j d_j = 0 exactly for the softmax gradient; bf16 storage rounds each d_j by 2^-9
+    df = d1[0].float()
+    rowsum = df.sum(-1).abs()
+    absum = df.abs().sum(-1)
+    assert bool(torch.all(rowsum <= 4e-3 * absum + 1e-12)), float((rowsum / (absum + 1e-30)).max())
+    assert int((absum > 0).sum()) > 0
+    assert torch.all(d1[0, T - 1] == 0)
+    sample = torch.tensor([0, 1, 255, 256, 257, 4095, 30000, 65534], device=DEV)
+    lg_np = logits.detach()[0, sample].float().cpu().numpy()
+    fn = {k: v.cpu().numpy() for k, v in f.items()}
+    s = sample.cpu().numpy()
+    for j, t in enumerate(s):
+        tok = t + 1
+        lse, H, tlp = grpo_oracle.row_stats(lg_np[j:j + 1], np.array([fn["input_ids"][0, tok]]), None, 1.0)
+        r = rows1[:, t].cpu().numpy()
+        assert abs(r[0] - tlp[0]) <= 1e-4 * max(1, abs(tlp[0])), (t, r[0], tlp[0])
+        assert abs(r[1] - H[0]) <= 1e-4 * max(1, abs(H[0])), (t, r[1], H[0])
+        assert abs(r[2] - lse[0]) <= 1e-4 * max(1, abs(lse[0]))
+        dref = grpo_oracle.row_grad(lg_np[j:j + 1], np.array([fn["input_ids"][0, tok]]), lse, H,
+                                    np.array([r[4]]), np.array([r[5]]), 1.0)[0]
+        ok, err = rel_close(d1[0, t].float().cpu().numpy(), dref, 1e-2, 1e-9)
+        assert ok, (t, err)
+
+
+def test_flatten_unflatten_and_sqnorm():
+    import ctypes
+
+    from pipelinerl_amd import _native
+
+    lib = _native.load()
+    ts = [torch.randn(n, device=DEV, dtype=dt) for n, dt in
+          [(1000, torch.float32), (37, torch.bfloat16), (4096, torch.bfloat16), (8, torch.float32), (0, torch.float32)]]
+    offs, o = [], 0
+    for t in ts:
+        offs.append(o)
+        o += (t.numel() + 7) // 8 * 8
+    flat = torch.zeros(o, dtype=torch.bfloat16, device=DEV)
+    n = len(ts)
+    P = (ctypes.c_void_p * n)(*[t.data_ptr() for t in ts])
+    D = (ctypes.c_int32 * n)(*[1 if t.dtype == torch.bfloat16 else 0 for t in ts])
+    N = (ctypes.c_int64 * n)(*[t.numel() for t in ts])
+    Of = (ctypes.c_int64 * n)(*offs)
+    st = torch.cuda.current_stream().cuda_stream
+    _native.check(lib.prl_flatten_bf16(P, D, N, Of, n, flat.data_ptr(), st), "flatten")
+    for t, off in zip(ts, offs):
+        assert torch.equal(flat[off:off + t.numel()], t.to(torch.bfloat16))
+    outs = [torch.empty_like(t) for t in ts]
+    Q = (ctypes.c_void_p * n)(*[t.data_ptr() for t in outs])
+    _native.check(lib.prl_unflatten_bf16(flat.data_ptr(), Q, D, N, Of, n, st), "unflatten")
+    for t, u in zip(ts, outs):
+        assert torch.equal(u, t.to(torch.bfloat16).to(t.dtype))
+    res = torch.zeros(1, dtype=torch.float64, device=DEV)
+    _native.check(lib.prl_grad_sqnorm(P, D, N, n, ctypes.cast(res.data_ptr(), ctypes.POINTER(ctypes.c_double)),
+                                      None, 0, st), "sqnorm")
+    want = sum(float((t.double() ** 2).sum()) for t in ts)
+    assert abs(float(res) - want) <= 1e-9 * want
