@@ -100,7 +100,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--tokens", type=int, default=65536)
     ap.add_argument("--vocab", type=int, default=151936)
-    ap.add_argument("--cpu-rows", type=int, default=2048)
+    ap.add_argument("--cpu-rows", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
