@@ -1,0 +1,124 @@
+"""Trainer -> actor weight broadcast over a gloo "actor" group on CPU (world size 2 and 3).
+
+The trainer side is WeightUpdateManager (overlapped, both transports); the actor side is the
+WorkerExtension receive path.  A test-only packer (plain torch copies) stands in for the HIP
+flatten kernel, which needs a device; the GPU suite covers that kernel.
+"""
+
+import json
+import os
+import socket
+import sys
+from pathlib import Path
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+class TorchFlatPacker:
+    def flatten(self, tensors, offsets, flat):
+        for t, o in zip(tensors, offsets):
+            flat[o:o + t.numel()].copy_(t.reshape(-1))
+
+    def unflatten(self, flat, tensors, offsets):
+        for t, o in zip(tensors, offsets):
+            t.copy_(flat[o:o + t.numel()].view_as(t))
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def make_model(seed):
+    torch.manual_seed(seed)
+    m = torch.nn.Sequential(torch.nn.Embedding(37, 16), torch.nn.Linear(16, 24), torch.nn.LayerNorm(24),
+                            torch.nn.Linear(24, 37, bias=False))
+    return m.to(torch.bfloat16)
+
+
+def _trainer(port, world, transport, exp, versions, use_reference_pg):
+    sys.path[:0] = [str(ROOT), str(ROOT / "pipelinerl-swe_amd")]
+    from pipelinerl_amd import torch_utils
+    from pipelinerl_amd.streams import SingleStreamSpec, reset_streams_backend, set_streams_backend
+    from pipelinerl_amd.weight_update import WeightUpdateManager
+
+    reset_streams_backend()
+    set_streams_backend("files")
+    model = make_model(0)
+    pg = torch_utils.init_extra_process_group(group_name="actor", backend="gloo",
+                                              init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=world)
+    stream = SingleStreamSpec(exp_path=Path(exp), topic="weight_update_request")
+    mgr = WeightUpdateManager([], model, stream, pg, transport=transport, bucket_bytes=1000, overlap=True,
+                              packer=TorchFlatPacker())
+    for v in versions:
+        with torch.no_grad():
+            for p in model.parameters():
+                p.add_(0.125 * (v + 1))
+        mgr.send_weight_update(v)  # returns immediately (overlapped)
+    mgr.close()
+    torch.save({n: p.detach().clone() for n, p in model.named_parameters()}, Path(exp) / "trainer_params.pt")
+
+
+def _actor(port, world, idx, transport, exp, nupdates, use_reference_pg):
+    sys.path[:0] = [str(ROOT), str(ROOT / "pipelinerl-swe_amd")]
+    from pipelinerl_amd.actor import StandaloneWorker
+    from pipelinerl_amd.weight_update import ParameterInfo, WeightUpdateRequest
+
+    worker = StandaloneWorker(make_model(100 + idx), rank=0, device="cpu", backend="gloo")
+    if use_reference_pg:  # join with the REFERENCE's group helper: pins the store-key layout
+        sys.path.insert(0, "/root/reference")
+        from pipelinerl.torch_utils import init_extra_process_group as ref_init
+
+        worker.pg_rank = 1 + idx
+        worker.process_group = ref_init(group_name="actor", backend="gloo", init_method=f"tcp://127.0.0.1:{port}",
+                                        rank=worker.pg_rank, world_size=world)
+    else:
+        worker.init_actor_update_group(idx, 1, f"tcp://127.0.0.1:{port}", world)
+    names = [(n, list(p.shape)) for n, p in worker.model_runner.model.params.items()]
+    infos = [ParameterInfo(name=n, shape=s, dtype=str(torch.bfloat16)) for n, s in names]
+    for v in range(nupdates):
+        worker.receive_weight_update(WeightUpdateRequest(version=v, parameters_info=infos, transport=transport,
+                                                         bucket_bytes=1000 if transport == "bucketed" else 0))
+    torch.save({n: p.detach().clone() for n, p in worker.model_runner.model.params.items()},
+               Path(exp) / f"actor{idx}_params.pt")
+
+
+def _run(rank, port, world, transport, exp, use_reference_pg):
+    os.environ["OMP_NUM_THREADS"] = "1"
+    if rank == 0:
+        _trainer(port, world, transport, exp, [3, 7], use_reference_pg)
+    else:
+        _actor(port, world, rank - 1, transport, exp, 2, use_reference_pg)
+
+
+@pytest.mark.parametrize("transport,world", [("per_tensor", 2), ("bucketed", 2), ("bucketed", 3)])
+def test_broadcast_roundtrip(tmp_path, transport, world):
+    port = free_port()
+    mp.spawn(_run, args=(port, world, transport, str(tmp_path), False), nprocs=world, join=True)
+    want = torch.load(tmp_path / "trainer_params.pt")
+    for a in range(world - 1):
+        got = torch.load(tmp_path / f"actor{a}_params.pt")
+        assert set(got) == set(want)
+        for n in want:
+            assert torch.equal(got[n], want[n].to(torch.bfloat16)), n
+    lines = (tmp_path / "streams" / "weight_update_request" / "0" / "0" / "0.jsonl").read_text().splitlines()
+    msgs = [json.loads(x) for x in lines]
+    assert [m["version"] for m in msgs if m["kind"] == "weight_update_success"] == [3, 7]
+
+
+@pytest.mark.skipif(not Path("/root/reference/pipelinerl/torch_utils.py").exists(),
+                    reason="reference checkout not present (wire-compat check runs in the build container)")
+def test_actor_group_interoperates_with_reference_helper(tmp_path):
+    port = free_port()
+    mp.spawn(_run, args=(port, 2, "per_tensor", str(tmp_path), True), nprocs=2, join=True)
+    want = torch.load(tmp_path / "trainer_params.pt")
+    got = torch.load(tmp_path / "actor0_params.pt")
+    for n in want:
+        assert torch.equal(got[n], want[n].to(torch.bfloat16)), n
