@@ -1,0 +1,129 @@
+"""Model / tokenizer loading and atomic checkpoints (contract of
+pipelinerl/finetune/checkpoints.py:75-296).
+
+Directory layout (unchanged, so actors restart from ``finetune/current``):
+  <output_dir>/current/            HF save_pretrained (safetensors) + tokenizer
+  <output_dir>/intermediate/<step>/
+  <output_dir>/training_state/training_state.pt   optimizer, lr_scheduler, TrainingMetrics
+Every directory is written to ``~<name>`` first and renamed into place by rank 0.
+"""
+
+from __future__ import annotations
+
+import contextlib
+import logging
+import os
+import shutil
+import types
+from pathlib import Path
+from typing import Any
+
+import torch
+import torch.distributed as dist
+
+logger = logging.getLogger(__name__)
+
+WEIGHT_FILES = ("pytorch_model.bin", "model.safetensors", "pytorch_model.bin.index.json",
+                "model.safetensors.index.json")
+
+
+def _rank() -> int:
+    return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+
+
+def _barrier(group=None) -> None:
+    if dist.is_available() and dist.is_initialized():
+        dist.barrier(group=group)
+
+
+def load_tokenizer(config_name: str, fallback_eos: int | None = None):
+    try:
+        from transformers import AutoTokenizer
+
+        return AutoTokenizer.from_pretrained(config_name)
+    except Exception as e:  # no tokenizer files offline: only eos_token_id is needed on this path
+        logger.warning(f"tokenizer for {config_name} unavailable ({e}); using eos_token_id only")
+        return types.SimpleNamespace(eos_token_id=fallback_eos if fallback_eos is not None else 2,
+                                     save_pretrained=lambda *a, **k: None, padding_side="right")
+
+
+def has_weights(d: Path) -> bool:
+    return any((Path(d) / f).exists() for f in WEIGHT_FILES)
+
+
+def load_model(args, model_class: str, current_dir: Path, device: torch.device):
+    """HF causal LM from ``current_dir`` (resume) or ``args.config_name``; optional value head."""
+    from transformers import AutoConfig, AutoModelForCausalLM
+
+    src = str(current_dir) if has_weights(current_dir) else args.config_name
+    kw: dict[str, Any] = {}
+    if args.get("load_as_bf16", True):
+        kw["torch_dtype"] = torch.bfloat16
+    attn = args.get("attn_implementation", "sdpa")
+    kw["attn_implementation"] = "sdpa" if attn == "flash_attention_2" else attn
+    p = Path(src)
+    if p.exists() and not has_weights(p):  # a config-only directory: random init of that architecture
+        model = AutoModelForCausalLM.from_config(AutoConfig.from_pretrained(src), **kw)
+    else:
+        model = AutoModelForCausalLM.from_pretrained(src, **kw)
+    if args.get("gradient_checkpointing", False):
+        model.gradient_checkpointing_enable(
+            gradient_checkpointing_kwargs={"use_reentrant": bool(args.get("reentrant_checkpointing", False))})
+    if model_class == "causal-language-modeling-with-value-head":
+        from .value_model import AutoModelForCausalLMWithValueHead
+
+        model = AutoModelForCausalLMWithValueHead(model)
+    return model.to(device)
+
+
+@contextlib.contextmanager
+def temporary_folder_and_move(output_dir: Path, group=None):
+    output_dir = Path(output_dir).resolve()
+    tmp = output_dir.parent / ("~" + output_dir.name)
+    if _rank() == 0:
+        if tmp.exists():
+            shutil.rmtree(tmp)
+        tmp.mkdir(parents=True)
+    _barrier(group)
+    yield tmp
+    _barrier(group)
+    if _rank() == 0:
+        if output_dir.exists():
+            shutil.rmtree(output_dir)
+        os.rename(tmp, output_dir)
+
+
+def save_model_and_tokenizer(output_dir: Path, model, tokenizer, safe_serialization: bool = True, group=None):
+    with temporary_folder_and_move(output_dir, group) as tmp:
+        if _rank() == 0:
+            m = getattr(model, "module", model)
+            m.save_pretrained(tmp, safe_serialization=safe_serialization)
+            if hasattr(tokenizer, "save_pretrained"):
+                tokenizer.save_pretrained(tmp)
+
+
+def save_training_state(training_state_dir: Path, model, optimizer, lr_scheduler, extra: dict[str, Any],
+                        group=None):
+    with temporary_folder_and_move(training_state_dir, group) as tmp:
+        if _rank() == 0:
+            state = dict(extra)
+            state["optimizer_state"] = optimizer.state_dict()
+            state["lr_scheduler_state"] = lr_scheduler.state_dict()
+            torch.save(state, tmp / "training_state.pt")
+
+
+def load_training_state(training_state_dir: Path, model, optimizer, lr_scheduler, metrics):
+    """Restores optimizer / scheduler (in place) and returns metrics updated from the file."""
+    state = torch.load(Path(training_state_dir) / "training_state.pt", map_location="cpu", weights_only=True)
+    optimizer.load_state_dict(state.pop("optimizer_state"))
+    lr_scheduler.load_state_dict(state.pop("lr_scheduler_state"))
+    for k, v in state.items():
+        if hasattr(metrics, k):
+            setattr(metrics, k, v)
+    return metrics
+
+
+def remove_results(*dirs: Path) -> None:
+    for d in dirs:
+        if Path(d).exists():
+            shutil.rmtree(d)

@@ -72,9 +72,12 @@ def rl_step(model, batch: PipelineBatchEncoding, current_step: int, max_step: in
         raise ValueError(f"Unknown algorithm {config.policy_loss}")
     has_value_head = hasattr(model, "value_head")
 
-    model_inputs = {"input_ids": batch.input_ids, "attention_mask": batch.attention_mask}
     if batch.is_packed:
-        model_inputs["position_ids"] = batch.position_ids
+        # packed [1, T]: no 2-D mask, so the model derives block-causal attention from the
+        # per-sequence position_ids (what flash-attn varlen does for the reference)
+        model_inputs = {"input_ids": batch.input_ids, "position_ids": batch.position_ids}
+    else:
+        model_inputs = {"input_ids": batch.input_ids, "attention_mask": batch.attention_mask}
     if getattr(batch, "pixel_values", None) is not None:
         model_inputs["pixel_values"] = batch.pixel_values
     if getattr(batch, "image_grid_thw", None) is not None:

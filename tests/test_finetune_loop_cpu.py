@@ -1,0 +1,118 @@
+"""Data-parallel trainer loop on CPU (gloo, world sizes 1 and 2) with the test-only torch loss.
+
+Checks the reference protocol (finetune_loop.py:567-719): lockstep sample counts with
+sentinel batches, optimizer step exactly when the global count reaches samples_per_step,
+SamplesProcessed messages, checkpoint layout, and that the bucketed gradient all-reduce
+keeps replicas identical and (reduce=sum) equals one rank training on all the data.
+"""
+
+import json
+import os
+import socket
+import sys
+from pathlib import Path
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_main(rank, world, port, exp, steps, passes, extra):
+    sys.path[:0] = [str(ROOT), str(ROOT / "tests"), str(ROOT / "pipelinerl-swe_amd")]
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), OMP_NUM_THREADS="1")
+    import torch.distributed as dist
+
+    from cpu_rl_step import cpu_rl_step
+    from loop_helpers import loop_cfg
+    from pipelinerl_amd.finetune_loop import run_finetuning_loop
+    from pipelinerl_amd.streams import reset_streams_backend
+
+    reset_streams_backend()
+    exp = Path(exp)
+    cfg = loop_cfg(exp, exp / "tiny_qwen2", world, passes, steps, **extra)
+    captured = {}
+
+    def step(model, batch, cur, mx, config):
+        captured["model"] = model
+        return cpu_rl_step(model, batch, cur, mx, config)
+
+    m = run_finetuning_loop(cfg, step_fn=step)
+    torch.save({n: p.detach().clone() for n, p in captured["model"].named_parameters()},
+               exp / f"params_w{world}_r{rank}.pt")
+    (exp / f"metrics_w{world}_r{rank}.json").write_text(json.dumps({"steps": m.completed_steps, "samples": m.samples,
+                                                                    "passes": m.passes}))
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def _setup(tmp: Path, world: int, n_groups=4, attempts=4, seq_length=28):
+    sys.path[:0] = [str(ROOT / "tests")]
+    from loop_helpers import rollouts, tiny_model_dir, write_training_data
+    from pipelinerl_amd.streams import reset_streams_backend, set_streams_backend
+
+    reset_streams_backend()
+    set_streams_backend("files")
+    tiny_model_dir(tmp)
+    data = rollouts(n_groups, attempts)
+    total = len(data)
+    per_step = total // 2  # two optimizer steps
+    writes = write_training_data(tmp, data, world, seq_length, per_step // world)
+    reset_streams_backend()
+    return per_step, writes
+
+
+@pytest.mark.parametrize("world", [2])
+def test_dp_loop_matches_single_rank(tmp_path, world):
+    # world-2 run
+    exp2 = tmp_path / "w2"
+    exp2.mkdir()
+    per_step, writes = _setup(exp2, world)
+    assert any(b.sentinel for _, b in writes), "the packing should have produced sentinel batches"
+    mp.spawn(_rank_main, args=(world, free_port(), str(exp2), 2, per_step, {}), nprocs=world, join=True)
+    p0 = torch.load(exp2 / "params_w2_r0.pt")
+    p1 = torch.load(exp2 / "params_w2_r1.pt")
+    for n in p0:
+        assert torch.equal(p0[n], p1[n]), n  # replicas stay identical
+    m0 = json.loads((exp2 / "metrics_w2_r0.json").read_text())
+    assert m0["steps"] == 2 and m0["samples"] == 2 * per_step
+    # world-1 run on the same rollouts
+    exp1 = tmp_path / "w1"
+    exp1.mkdir()
+    _setup(exp1, 1)
+    mp.spawn(_rank_main, args=(1, free_port(), str(exp1), 2, per_step, {}), nprocs=1, join=True)
+    q = torch.load(exp1 / "params_w1_r0.pt")
+    worst = max(float((p0[n] - q[n]).abs().max()) for n in q)
+    assert worst < 2e-5, worst
+    # protocol outputs
+    msgs = [json.loads(x) for x in (exp2 / "streams" / "weight_update_request" / "0" / "0" / "0.jsonl").read_text()
+            .splitlines()]
+    counts = [m["samples_processed"] for m in msgs if m["kind"] == "samples_processed"]
+    assert counts[0] == 0 and counts == sorted(counts) and counts[-1] == 2 * per_step
+    fin = exp2 / "finetune"
+    assert (fin / "current" / "config.json").exists() and (fin / "training_state" / "training_state.pt").exists()
+    summary = json.loads((fin / "summary.json").read_text())
+    assert summary["completed_steps"] == 2 and summary["samples"] == 2 * per_step
+    lines = [json.loads(x) for x in (fin / "logs" / "metrics.jsonl").read_text().splitlines()]
+    assert {"rl/ess", "throughput/tokens_per_sec", "stats/grad_norm", "rl/loss"} <= set(lines[-1])
+
+
+def test_resume_from_training_state(tmp_path):
+    exp = tmp_path / "r"
+    exp.mkdir()
+    per_step, _ = _setup(exp, 1)
+    mp.spawn(_rank_main, args=(1, free_port(), str(exp), 1, per_step, {}), nprocs=1, join=True)
+    m = json.loads((exp / "metrics_w1_r0.json").read_text())
+    assert m["steps"] == 1
+    state = torch.load(exp / "finetune" / "training_state" / "training_state.pt", weights_only=True)
+    assert state["completed_steps"] == 1 and "optimizer_state" in state
