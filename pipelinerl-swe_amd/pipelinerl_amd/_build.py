@@ -39,16 +39,23 @@ def _stale() -> bool:
     return any(d.stat().st_mtime > mt for d in deps)
 
 
-def build(force: bool = False, resource_usage: bool = False, verbose: bool = False) -> Path:
-    if not force and not resource_usage and not _stale():
+VARIANT_DIR = PKG / "variants"
+
+
+def build(force: bool = False, resource_usage: bool = False, verbose: bool = False,
+          defines: dict[str, str] | None = None, out: Path | None = None) -> Path:
+    target = out or LIB
+    if out is None and not force and not resource_usage and not _stale():
         return LIB
     cc = hipcc()
-    objdir = PKG / "build"
-    objdir.mkdir(exist_ok=True)
+    objdir = PKG / "build" / (target.stem if out is not None else "main")
+    objdir.mkdir(parents=True, exist_ok=True)
     flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", f"-I{INCLUDE}", f"-I{CSRC}",
              "-Wall", "-Wno-unused-function"]
     if resource_usage:
         flags.append("-Rpass-analysis=kernel-resource-usage")
+    for k, v in (defines or {}).items():
+        flags.append(f"-D{k}={v}")
 
     def compile_one(src: str):
         obj = objdir / (Path(src).stem + ".o")
@@ -63,13 +70,20 @@ def build(force: bool = False, resource_usage: bool = False, verbose: bool = Fal
     if resource_usage or verbose:
         for (_, err), src in zip(results, SOURCES):
             (objdir / (Path(src).stem + ".resource.txt")).write_text(err)
-    tmp = LIB.with_suffix(".so.tmp")
+    target.parent.mkdir(parents=True, exist_ok=True)
+    tmp = target.with_suffix(".so.tmp")
     cmd = [cc, "-shared", f"--offload-arch={ARCH}", "-o", str(tmp), *[str(o) for o, _ in results]]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr[-8000:]}")
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, target)
+    return target
+
+
+def build_variant(name: str, defines: dict[str, str]) -> Path:
+    """An experiment build (e.g. cache-policy A/B) at variants/libprl_hip_<name>.so; load it
+    with PRL_LIB=<path>."""
+    return build(defines=defines, out=VARIANT_DIR / f"libprl_hip_{name}.so")
 
 
 if __name__ == "__main__":

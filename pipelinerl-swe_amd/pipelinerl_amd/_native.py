@@ -12,7 +12,7 @@ from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int32, c_int64
 from pathlib import Path
 
 _PKG = Path(__file__).resolve().parent
-LIB_PATH = _PKG / "libprl_hip.so"
+LIB_PATH = Path(os.environ["PRL_LIB"]) if os.environ.get("PRL_LIB") else _PKG / "libprl_hip.so"
 HEADER_PATH = _PKG.parents[1] / "include" / "prl_hip.h"
 
 PRL_F32, PRL_BF16 = 0, 1
@@ -95,7 +95,7 @@ def load():
     global _lib
     if _lib is not None:
         return _lib
-    if not LIB_PATH.exists() or os.environ.get("PRL_REBUILD"):
+    if (not LIB_PATH.exists() or os.environ.get("PRL_REBUILD")) and not os.environ.get("PRL_LIB"):
         try:
             from . import _build
             _build.build()

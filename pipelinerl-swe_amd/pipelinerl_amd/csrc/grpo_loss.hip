@@ -73,7 +73,16 @@ __device__ __forceinline__ TokGrad row_epilogue(const KArgs& a, int64_t q, int64
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void* p, int64_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
 }
-constexpr int kAuxNT = 2;           // nontemporal: the logits / dlogits stream once
+// cache policy of the row stream (aux bits of buffer_load/store: 2 = nt).  The logits and
+// dlogits are touched once per launch; the build can override for A/B experiments.
+#ifndef PRL_LOAD_AUX
+#define PRL_LOAD_AUX 2
+#endif
+#ifndef PRL_STORE_AUX
+#define PRL_STORE_AUX 2
+#endif
+constexpr int kLoadAux = PRL_LOAD_AUX;
+constexpr int kStoreAux = PRL_STORE_AUX;
 constexpr uint32_t kPadBf16x2 = 0xF1CAF1CAu;  // two bf16 -1.0e30: contributes 2^-huge = 0
 
 template <int NV>
@@ -100,7 +109,7 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
     const auto rs = row_rsrc(lg + lrow * a.ld, row_bytes);
 #pragma unroll
     for (int k = 0; k < NV; ++k)
-      buf[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, k * VSTRIDE, kAuxNT));
+      buf[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, k * VSTRIDE, kLoadAux));
   }
   int par = 0;
   for (; q < nrows; q += gridDim.x, par ^= 1) {
@@ -166,6 +175,11 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
 #pragma unroll
       for (int k = 0; k < NV; ++k) {
         u32x4 o;
+#ifdef PRL_COPY_CEILING
+        if (true) {  // structural ceiling experiment: same traffic and schedule, no gradient math
+          o = buf[k];
+        } else
+#endif
         if (zero_row) {
           o = u32x4{0u, 0u, 0u, 0u};
         } else {
@@ -186,13 +200,13 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
           for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(d[2 * j], d[2 * j + 1]);
         }
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, o),
-                                               ws, voff, k * VSTRIDE, kAuxNT);
-        buf[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rn, voff, k * VSTRIDE, kAuxNT));
+                                               ws, voff, k * VSTRIDE, kStoreAux);
+        buf[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rn, voff, k * VSTRIDE, kLoadAux));
       }
     } else {
 #pragma unroll
       for (int k = 0; k < NV; ++k)
-        buf[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rn, voff, k * VSTRIDE, kAuxNT));
+        buf[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rn, voff, k * VSTRIDE, kLoadAux));
     }
   }
 }

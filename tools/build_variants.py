@@ -1,0 +1,21 @@
+"""Build A/B experiment variants of libprl_hip.so into pipelinerl_amd/variants/ (git-ignored,
+travels to the GPU box).  Run a variant with PRL_LIB=<path> python bench.py ..."""
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "pipelinerl-swe_amd"))
+from pipelinerl_amd._build import build, build_variant  # noqa: E402
+
+VARIANTS = {
+    "ld_nt_st_nt": {"PRL_LOAD_AUX": "2", "PRL_STORE_AUX": "2"},
+    "ld_def_st_nt": {"PRL_LOAD_AUX": "0", "PRL_STORE_AUX": "2"},
+    "ld_nt_st_def": {"PRL_LOAD_AUX": "2", "PRL_STORE_AUX": "0"},
+    "ld_def_st_def": {"PRL_LOAD_AUX": "0", "PRL_STORE_AUX": "0"},
+    "copy_ceiling": {"PRL_COPY_CEILING": "1"},
+}
+
+if __name__ == "__main__":
+    build(force=True)
+    names = sys.argv[1:] or list(VARIANTS)
+    for n in names:
+        print(build_variant(n, VARIANTS[n]))
