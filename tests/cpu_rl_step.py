@@ -34,7 +34,8 @@ def cpu_rl_step(model, batch, current_step, max_step, config):
         r_used = torch.clamp(ratio, 0, 1 + config.epsilon)
         pol = lp * adv * r_used.detach()
     loss = -((pol - kl_c * kl + ent_c * ent) * w * mask).nan_to_num(0).sum()
+    nl = batch.num_labels[:, 1:]
     stats = {"loss": float(loss), "ratio_new_old_sum": float((r_used * mask).sum()),
              "ratio_new_old_squared_sum": float((r_used * r_used * mask).sum()),
-             "num_output_tokens_sum": int(mask.sum()), "entropy": float((ent * mask).sum())}
+             "num_output_tokens_sum": int(mask.sum()), "entropy": float((ent / nl * mask).nan_to_num(0).sum())}
     return loss, stats
