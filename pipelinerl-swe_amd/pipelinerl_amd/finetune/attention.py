@@ -1,0 +1,102 @@
+"""Packed-sequence (varlen) attention for the trainer's model forward.
+
+The reference trains packed micro-batches with flash-attn-2 varlen: one [1, T] row holding many
+rollouts, attention confined to each rollout (finetune/checkpoints.py:96-101, position_ids fed
+to the model at rl/__init__.py:188-189).  This registers an HF attention implementation
+``prl_varlen`` that does the same on ROCm with torch's flash-attention varlen
+(``torch.nn.attention.varlen.varlen_attn``), given cumulative sequence offsets computed ONCE
+per micro-batch on the host (``cu_seq_lens_q/k``, ``max_length_q/k`` — the FlashAttention
+kwargs HF propagates to every layer).  If varlen is unavailable for the inputs it runs causal
+SDPA per sequence (same result, no T x T mask either way).
+"""
+
+from __future__ import annotations
+
+import logging
+
+import torch
+import torch.nn.functional as F
+
+logger = logging.getLogger(__name__)
+
+PRL_VARLEN = "prl_varlen"
+_registered = False
+_varlen_ok: bool | None = None
+
+
+def varlen_attention_forward(module, query, key, value, attention_mask, scaling=None, dropout=0.0, **kwargs):
+    """HF attention interface: query/key/value [B, H, T, D] -> ([B, T, H, D], None)."""
+    cu = kwargs.get("cu_seq_lens_q")
+    if cu is None:  # not a packed call: plain causal SDPA semantics
+        from transformers.integrations.sdpa_attention import sdpa_attention_forward
+
+        return sdpa_attention_forward(module, query, key, value, attention_mask, scaling=scaling, dropout=dropout,
+                                      **kwargs)
+    B, Hq, T, D = query.shape
+    assert B == 1, "packed batches are [1, T]"
+    Hkv = key.shape[1]
+    q = query[0].transpose(0, 1)
+    k = key[0].transpose(0, 1)
+    v = value[0].transpose(0, 1)
+    if Hkv != Hq:
+        k = k.repeat_interleave(Hq // Hkv, dim=1)
+        v = v.repeat_interleave(Hq // Hkv, dim=1)
+    mx = int(kwargs["max_length_q"])
+    default_scale = D ** -0.5
+    global _varlen_ok
+    if (scaling is None or abs(scaling - default_scale) < 1e-12) and q.is_cuda and _varlen_ok is not False:
+        try:
+            from torch.nn.attention.varlen import varlen_attn
+
+            out = varlen_attn(q.contiguous(), k.contiguous(), v.contiguous(), cu, cu, mx, mx, is_causal=True)
+            _varlen_ok = True
+            return out.unsqueeze(0), None
+        except (RuntimeError, NotImplementedError) as e:
+            if _varlen_ok is None:
+                logger.warning(f"varlen flash attention unavailable ({e}); using per-sequence SDPA")
+            _varlen_ok = False
+    bounds = kwargs.get("cu_seq_lens_host")
+    if bounds is None:
+        bounds = cu.tolist()
+    outs = []
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        if b <= a:
+            continue
+        qi, ki, vi = (t[a:b].transpose(0, 1).unsqueeze(0) for t in (q, k, v))
+        outs.append(F.scaled_dot_product_attention(qi, ki, vi, is_causal=True, scale=scaling)[0].transpose(0, 1))
+    return torch.cat(outs, 0).unsqueeze(0), None
+
+
+def register() -> str:
+    global _registered
+    if not _registered:
+        from transformers import AttentionInterface
+        from transformers.masking_utils import AttentionMaskInterface, flash_attention_mask
+
+        AttentionInterface.register(PRL_VARLEN, varlen_attention_forward)
+        AttentionMaskInterface.register(PRL_VARLEN, flash_attention_mask)
+        _registered = True
+    return PRL_VARLEN
+
+
+def uses_varlen(model) -> bool:
+    cfg = getattr(model, "config", None)
+    return getattr(cfg, "_attn_implementation", None) == PRL_VARLEN
+
+
+def packed_kwargs(batch, device) -> dict:
+    """cu_seq_lens / max_length for a packed [1, T] batch, from host-side metadata."""
+    sb = batch.seq_boundaries
+    if sb is None or sb.numel() < 2:
+        pos = batch.position_ids[0].cpu()
+        starts = (pos == 0).nonzero().flatten().tolist()
+        if not starts or starts[0] != 0:
+            starts = [0] + starts
+        bounds = starts + [int(pos.numel())]
+    else:
+        bounds = [int(x) for x in sb.cpu().tolist()]
+    lens = [b - a for a, b in zip(bounds[:-1], bounds[1:])]
+    cu = torch.tensor(bounds, dtype=torch.int32).to(device, non_blocking=True)
+    mx = max(lens) if lens else 0
+    return {"cu_seq_lens_q": cu, "cu_seq_lens_k": cu, "max_length_q": mx, "max_length_k": mx,
+            "cu_seq_lens_host": bounds}

@@ -60,7 +60,11 @@ def load_model(args, model_class: str, current_dir: Path, device: torch.device):
     if args.get("load_as_bf16", True):
         kw["torch_dtype"] = torch.bfloat16
     attn = args.get("attn_implementation", "sdpa")
-    kw["attn_implementation"] = "sdpa" if attn == "flash_attention_2" else attn
+    if attn in ("flash_attention_2", "prl_varlen"):  # packed varlen attention (finetune/attention.py)
+        from .attention import register
+
+        attn = register()
+    kw["attn_implementation"] = attn
     p = Path(src)
     if p.exists() and not has_weights(p):  # a config-only directory: random init of that architecture
         model = AutoModelForCausalLM.from_config(AutoConfig.from_pretrained(src), **kw)

@@ -23,11 +23,13 @@ import numpy as np
 import torch
 from pydantic import BaseModel, Field
 
+from ..attention import packed_kwargs, uses_varlen
 from ..types import PipelineBatchEncoding
 from .fused import GrpoParams, grpo_loss, prepare_fields
 from ..._native import S
 
 logger = logging.getLogger(__name__)
+_warned: dict[str, bool] = {}
 
 RL_DATA_COLUMNS = ["overflow", "group_tokens", "num_labels", "rewards", "advantages", "old_logprobs",
                    "ref_logprobs"]
@@ -73,9 +75,16 @@ def rl_step(model, batch: PipelineBatchEncoding, current_step: int, max_step: in
     has_value_head = hasattr(model, "value_head")
 
     if batch.is_packed:
-        # packed [1, T]: no 2-D mask, so the model derives block-causal attention from the
-        # per-sequence position_ids (what flash-attn varlen does for the reference)
+        # packed [1, T]: attention must stay inside each rollout (flash-attn varlen in the
+        # reference).  The prl_varlen attention gets cu_seq_lens computed once on the host.
         model_inputs = {"input_ids": batch.input_ids, "position_ids": batch.position_ids}
+        if uses_varlen(model):
+            model_inputs.update(packed_kwargs(batch, batch.input_ids.device))
+        elif hasattr(model, "config") and not _warned.get("varlen"):
+            _warned["varlen"] = True
+            logger.warning("packed batch on a model without prl_varlen attention: rollouts may attend "
+                           "across sequence boundaries (load the model with attn_implementation="
+                           "'flash_attention_2' or 'prl_varlen')")
     else:
         model_inputs = {"input_ids": batch.input_ids, "attention_mask": batch.attention_mask}
     if getattr(batch, "pixel_values", None) is not None:

@@ -116,7 +116,7 @@ def run_data_loader(data_stream: SingleStreamSpec, batch_queue: Queue, device: t
                 if device.type == "cuda":
                     for name in type(b).model_fields:
                         v = getattr(b, name)
-                        if isinstance(v, torch.Tensor):
+                        if isinstance(v, torch.Tensor) and name != "seq_boundaries":  # host metadata
                             setattr(b, name, v.pin_memory().to(device, non_blocking=True))
                 batch_queue.put((b, ntok, nseq))
     except Exception as e:

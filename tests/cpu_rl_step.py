@@ -11,7 +11,10 @@ import torch.nn.functional as F
 
 def cpu_rl_step(model, batch, current_step, max_step, config):
     if batch.is_packed:
-        out = model(input_ids=batch.input_ids, position_ids=batch.position_ids)
+        from pipelinerl_amd.finetune.attention import packed_kwargs, uses_varlen
+
+        extra = packed_kwargs(batch, batch.input_ids.device) if uses_varlen(model) else {}
+        out = model(input_ids=batch.input_ids, position_ids=batch.position_ids, **extra)
     else:
         out = model(input_ids=batch.input_ids, attention_mask=batch.attention_mask)
     logits = out.logits[:, :-1].float() / config.temperature

@@ -62,7 +62,7 @@ def loop_cfg(exp: Path, model_dir: Path, world: int, passes: int, steps: int, **
 
     ft = dict(
         config_name=str(model_dir), model_class="causal-language-modeling", output_dir=str(exp / "finetune"),
-        load_as_bf16=False, attn_implementation="sdpa", gradient_checkpointing=False, optim="adamw_torch",
+        load_as_bf16=False, attn_implementation="flash_attention_2", gradient_checkpointing=False, optim="adamw_torch",
         learning_rate=1e-3, weight_decay=0.01, lr_scheduler_type="cosine", num_warmup_steps=0,
         max_train_steps=steps, interrupt_train_steps=-1, gradient_accumulation_passes=passes,
         train_batch_size=1, seq_parallel=1, seed=42, gradient_clipping_threshold=0.3, input="training_data",

@@ -20,8 +20,10 @@ def _tiny_model(tmp, dtype):
 
     d = tiny_model_dir(tmp)
     torch.manual_seed(0)
-    return AutoModelForCausalLM.from_config(AutoConfig.from_pretrained(d), torch_dtype=dtype,
-                                            attn_implementation="sdpa").cuda()
+    from pipelinerl_amd.finetune.attention import register
+
+    return AutoModelForCausalLM.from_config(AutoConfig.from_pretrained(d), dtype=dtype,
+                                            attn_implementation=register()).cuda()
 
 
 def test_rl_step_through_hf_model_matches_torch_reference(tmp_path):
@@ -69,3 +71,9 @@ def test_trainer_loop_one_gpu(tmp_path):
     lines = [json.loads(x) for x in (tmp_path / "finetune" / "logs" / "metrics.jsonl").read_text().splitlines()]
     assert all(np.isfinite(line["rl/loss"]) for line in lines)
     assert (tmp_path / "finetune" / "current" / "model.safetensors").exists()
+
+
+def test_varlen_attention_gpu(tmp_path):
+    from test_attention_cpu import check
+
+    check(tmp_path, "cuda")
