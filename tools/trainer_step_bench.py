@@ -1,0 +1,164 @@
+"""Trainer-step and loss-head comparisons on one MI355X (measurement tool).
+
+  --mode loss     fused HIP loss head vs the reference's ATen op chain (tools/aten_rl_step.py)
+                  on the same bf16 logits, fwd+bwd per packed micro-batch
+  --mode trainer  full trainer micro-batch step on a Qwen2.5-shaped model (random init, bf16,
+                  prl_varlen attention): forward, loss head (fused or ATen), backward, fused AdamW
+Prints one JSON line per measured configuration.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+import types
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "pipelinerl-swe_amd"), str(ROOT / "tools")]
+
+import torch  # noqa: E402
+
+QWEN = {  # published Qwen2.5 shapes (config.json of each checkpoint)
+    "0.5b": dict(hidden_size=896, intermediate_size=4864, num_hidden_layers=24, num_attention_heads=14,
+                 num_key_value_heads=2, vocab_size=151936, tie_word_embeddings=True),
+    "1.5b": dict(hidden_size=1536, intermediate_size=8960, num_hidden_layers=28, num_attention_heads=12,
+                 num_key_value_heads=2, vocab_size=151936, tie_word_embeddings=True),
+    "7b": dict(hidden_size=3584, intermediate_size=18944, num_hidden_layers=28, num_attention_heads=28,
+               num_key_value_heads=4, vocab_size=152064, tie_word_embeddings=False),
+}
+
+
+def packed_batch(T, seq, prompt, V, device, seed=0):
+    from pipelinerl_amd.finetune.types import PipelineBatchEncoding
+
+    g = torch.Generator().manual_seed(seed)
+    nseq = T // seq
+    pos = torch.arange(T) % seq
+    ids = torch.randint(0, min(V, 151643), (1, T), generator=g)
+    labels = torch.where(pos[None] >= prompt, ids, torch.full_like(ids, -100))
+    rewards = torch.repeat_interleave(torch.randint(0, 2, (nseq,), generator=g).float(), seq)[None]
+    lab = (labels != -100).float()
+    old = (torch.randn((1, T), generator=g) - 12.0) * lab
+    b = PipelineBatchEncoding(
+        input_ids=ids, labels=labels, attention_mask=torch.ones_like(ids), position_ids=pos[None],
+        rewards=rewards, advantages=rewards - rewards.mean(), ref_logprobs=old.clone(), old_logprobs=old,
+        group_tokens=torch.full((1, T), float(seq)), num_labels=torch.full((1, T), float(seq - prompt)),
+        overflow=torch.zeros((1, T)), seq_boundaries=torch.arange(0, T + 1, seq, dtype=torch.int32),
+        model_version=0, is_packed=True)
+    sb = b.seq_boundaries
+    b.to_device(device)
+    b.seq_boundaries = sb  # host metadata, as the trainer's loader keeps it
+    return b
+
+
+def timed(fn, steps, warmup):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
+def rl_cfg():
+    from pipelinerl_amd.finetune.rl import RLConfig
+
+    return RLConfig(policy_loss="ppo", epsilon=4.0, kl_coef=0.0, final_kl_coef=0.0, clamp_log_ratio_ref_new_value=5,
+                    batch_size=4096)
+
+
+def mode_loss(a):
+    from aten_rl_step import aten_loss_head
+    from pipelinerl_amd.finetune.rl import rl_step
+
+    V = a.vocab
+    batch = packed_batch(a.tokens, a.seq, a.prompt, V, "cuda")
+    g = torch.Generator(device="cuda").manual_seed(0)
+    logits = (torch.randn((1, a.tokens, V), generator=g, device="cuda") * 3).to(torch.bfloat16)
+    model = types.SimpleNamespace(config=None)
+    cfg = rl_cfg()
+    out = {}
+    for name in a.loss.split(","):
+        lg = logits.clone().requires_grad_(True)
+
+        def step():
+            lg.grad = None
+            if name == "fused":
+                m = types.SimpleNamespace(logits=lg)
+                loss, _ = rl_step(lambda **kw: m, batch, 0, 100, cfg)
+            else:
+                loss, _ = aten_loss_head(lg, batch, cfg)
+            loss.backward()
+
+        torch.cuda.reset_peak_memory_stats()
+        dt = timed(step, a.steps, a.warmup)
+        out[name] = {"ms": round(dt * 1e3, 3), "tokens_per_s": round(a.tokens / dt, 1),
+                     "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 1e9, 2)}
+        del lg
+        torch.cuda.empty_cache()
+    print(json.dumps({"mode": "loss", "T": a.tokens, "V": V, "dtype": "bf16", "results": out}), flush=True)
+
+
+def mode_trainer(a):
+    from aten_rl_step import aten_loss_head
+    from pipelinerl_amd.finetune.attention import packed_kwargs, register
+    from pipelinerl_amd.finetune.optim import get_optimizer
+    from pipelinerl_amd.finetune.rl import rl_step
+    from transformers import AutoModelForCausalLM, Qwen2Config
+
+    shapes = QWEN[a.model]
+    cfg_m = Qwen2Config(max_position_embeddings=32768, rope_theta=1e6, rms_norm_eps=1e-6, **shapes)
+    torch.manual_seed(0)
+    model = AutoModelForCausalLM.from_config(cfg_m, dtype=torch.bfloat16, attn_implementation=register()).cuda()
+    if a.grad_ckpt:
+        model.gradient_checkpointing_enable(gradient_checkpointing_kwargs={"use_reentrant": False})
+    model.train()
+    opt = get_optimizer("adamw_torch", model, 1e-6, 0.01)
+    batch = packed_batch(a.tokens, a.seq, a.prompt, shapes["vocab_size"], "cuda")
+    cfg = rl_cfg()
+    out = {}
+    for name in a.loss.split(","):
+        def step():
+            if name == "fused":
+                loss, _ = rl_step(model, batch, 0, 100, cfg)
+            else:
+                o = model(input_ids=batch.input_ids, position_ids=batch.position_ids,
+                          **packed_kwargs(batch, "cuda"))
+                loss, _ = aten_loss_head(o.logits, batch, cfg)
+            loss.backward()
+            torch.nn.utils.clip_grad_norm_(model.parameters(), 0.3)
+            opt.step()
+            opt.zero_grad(set_to_none=True)
+
+        torch.cuda.reset_peak_memory_stats()
+        try:
+            dt = timed(step, a.steps, a.warmup)
+            out[name] = {"ms_per_micro_batch_step": round(dt * 1e3, 2), "tokens_per_s": round(a.tokens / dt, 1),
+                         "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 1e9, 2)}
+        except torch.OutOfMemoryError as e:
+            out[name] = {"oom": str(e)[:200]}
+        opt.zero_grad(set_to_none=True)
+        torch.cuda.empty_cache()
+    print(json.dumps({"mode": "trainer", "model": f"Qwen2.5-{a.model} shapes (random init)", "T": a.tokens,
+                      "seq": a.seq, "grad_ckpt": a.grad_ckpt, "results": out}), flush=True)
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mode", choices=["loss", "trainer"], default="loss")
+    ap.add_argument("--model", choices=list(QWEN), default="1.5b")
+    ap.add_argument("--tokens", type=int, default=16384)
+    ap.add_argument("--vocab", type=int, default=151936)
+    ap.add_argument("--seq", type=int, default=2048)
+    ap.add_argument("--prompt", type=int, default=256)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--loss", default="fused,aten")
+    ap.add_argument("--grad-ckpt", action="store_true")
+    a = ap.parse_args()
+    mode_loss(a) if a.mode == "loss" else mode_trainer(a)
