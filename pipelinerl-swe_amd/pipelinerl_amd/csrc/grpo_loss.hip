@@ -469,13 +469,24 @@ __global__ __launch_bounds__(kStatThreads) void grpo_stats_partial(KArgs a, int6
   }
 }
 
-__global__ void grpo_finalize(const double* __restrict__ partials, int nblocks,
-                              double* __restrict__ stats) {
-  const int i = threadIdx.x;
-  if (i >= PRL_NSTAT) return;
-  double acc = stat_identity(i);
-  for (int b = 0; b < nblocks; ++b) acc = stat_fold(i, acc, partials[(int64_t)b * PRL_NSTAT + i]);
-  stats[i] = acc;
+// Fold the per-block partials: kFinLanes threads per statistic fold a strided subset in order,
+// then lane 0 folds those kFinLanes results in order (deterministic for a given block count).
+constexpr int kFinLanes = 16;
+__global__ __launch_bounds__(1024) void grpo_finalize(const double* __restrict__ partials, int nblocks,
+                                                      double* __restrict__ stats) {
+  __shared__ double sh[PRL_NSTAT][kFinLanes];
+  const int i = threadIdx.x / kFinLanes, j = threadIdx.x % kFinLanes;
+  if (i < PRL_NSTAT) {
+    double acc = stat_identity(i);
+    for (int b = j; b < nblocks; b += kFinLanes) acc = stat_fold(i, acc, partials[(int64_t)b * PRL_NSTAT + i]);
+    sh[i][j] = acc;
+  }
+  __syncthreads();
+  if (i < PRL_NSTAT && j == 0) {
+    double acc = stat_identity(i);
+    for (int k = 0; k < kFinLanes; ++k) acc = stat_fold(i, acc, sh[i][k]);
+    stats[i] = acc;
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -655,14 +666,15 @@ int prl_grpo_forward(const PrlGrpoBatch* batch, const PrlGrpoParams* params,
   // statistics + value gradient: fixed row chunks per block (deterministic)
   int sblocks = 0;
   if (nrows > 0) {
+    // ~256 rows per 256-thread block: one row per thread, enough blocks to fill the chip
     int64_t chunk = (nrows + kMaxGrid - 1) / kMaxGrid;
-    if (chunk < 1024) chunk = 1024;
+    if (chunk < kStatThreads) chunk = kStatThreads;
     sblocks = (int)((nrows + chunk - 1) / chunk);
     hipLaunchKernelGGL(grpo_stats_partial, dim3(sblocks), dim3(kStatThreads), 0, s, a, chunk);
     e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
   }
-  hipLaunchKernelGGL(grpo_finalize, dim3(1), dim3(64), 0, s, a.partials, sblocks, out->stats);
+  hipLaunchKernelGGL(grpo_finalize, dim3(1), dim3(PRL_NSTAT * kFinLanes), 0, s, a.partials, sblocks, out->stats);
   return (int)hipGetLastError();
 }
 

@@ -1,0 +1,162 @@
+"""Edge cases of the fused loss head on the GPU, each checked against the pinned oracle (or
+the reference's own semantics where the oracle has no rows to compare)."""
+
+import numpy as np
+import pytest
+import torch
+
+from gpu_helpers import LogitsModel, rel_close, to_batch
+from oracle import grpo_oracle, synth
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+CFG = dict(policy_loss="ppo", kl_coef=0.05, final_kl_coef=0.05, entropy_bonus=0.01, final_entropy_bonus=0.01,
+           epsilon=0.2, batch_size=3, clamp_log_ratio_ref_new_value=5)
+
+
+def _batch(T, V, seed=0, lens=None, prompts=None):
+    lens = lens or [T]
+    prompts = prompts or [min(2, x - 1) for x in lens]
+    b = synth.packed_rl_batch(seed, lens, prompts, id_range=V, eos=3)
+    rng = np.random.default_rng(seed)
+    m = b["labels"] != -100
+    b["old_logprobs"] = np.where(m, rng.normal(-6, 1, (1, T)), 0).astype(np.float32)
+    b["ref_logprobs"] = np.where(m, rng.normal(-6, 1, (1, T)), 0).astype(np.float32)
+    return b
+
+
+def _run(lg, b, cfg=CFG, dtype=torch.bfloat16, values=None, scale=1.0):
+    from pipelinerl_amd.finetune.rl import RLConfig, rl_step
+
+    model = LogitsModel(torch.tensor(lg, dtype=torch.float32).to(dtype).to(DEV),
+                        None if values is None else torch.tensor(values, device=DEV))
+    loss, stats = rl_step(model, to_batch(b), 0, 10, RLConfig(**cfg))
+    (loss * scale).backward()
+    torch.cuda.synchronize()
+    return float(loss.detach()), stats, model.logits.grad.float().cpu().numpy()
+
+
+def _cmp(lg, b, cfg=CFG, dtype=torch.bfloat16, values=None):
+    loss, stats, d = _run(lg, b, cfg, dtype, values)
+    o = grpo_oracle.rl_step_oracle(lg, b, cfg, 0, 10, values=values)
+    for k, v in o["stats"].items():
+        assert abs(stats[k] - v) <= 1e-4 * max(1.0, abs(v)), (k, stats[k], v)
+    tol = (1e-2, 1e-8) if dtype == torch.bfloat16 else (1e-4, 1e-7)
+    ok, err = rel_close(d, o["dlogits"], *tol)
+    assert ok, err
+    return stats, d
+
+
+def test_single_loss_row():
+    T, V = 2, 512
+    b = _batch(T, V, lens=[2], prompts=[1])
+    lg = synth.to_bf16(np.random.default_rng(1).normal(0, 2, (1, T, V))).astype(np.float32)
+    _cmp(lg, b)
+
+
+def test_no_rows_and_sentinel_batch():
+    from pipelinerl_amd.finetune.rl import RLConfig, rl_step
+    from pipelinerl_amd.finetune.utils import create_sentinel_batch
+
+    # L = 1: logits[:, :-1] is empty in the reference -> loss 0, stats {"input_size"}
+    b = _batch(1, 64, lens=[1], prompts=[0])
+    loss, stats, d = _run(np.zeros((1, 1, 64), np.float32), b)
+    assert loss == 0.0 and stats == {"input_size": 1.0} and np.all(d == 0)
+    # sentinel batch: all labels masked; the trainer multiplies the loss by 0
+    sb = create_sentinel_batch(DEV, None, 0)
+    model = LogitsModel(torch.randn(1, 8, 256, device=DEV, dtype=torch.bfloat16))
+    loss, stats = rl_step(model, sb, 0, 10, RLConfig(**CFG))
+    (loss * 0.0).backward()
+    assert stats == {"input_size": 8.0}
+    assert torch.count_nonzero(model.logits.grad) == 0
+
+
+@pytest.mark.parametrize("scale", [1e-3, 30.0, 2000.0])
+def test_extreme_magnitudes(scale):
+    T, V = 17, 4096
+    b = _batch(T, V, seed=2, lens=[9, 8], prompts=[2, 3])
+    lg = synth.to_bf16(np.random.default_rng(2).normal(0, scale, (1, T, V))).astype(np.float32)
+    _cmp(lg, b)
+
+
+@pytest.mark.parametrize("temperature", [0.05, 3.0])
+def test_temperature_extremes(temperature):
+    T, V = 13, 2048
+    b = _batch(T, V, seed=3)
+    lg = synth.to_bf16(np.random.default_rng(3).normal(0, 3, (1, T, V))).astype(np.float32)
+    _cmp(lg, b, dict(CFG, temperature=temperature))
+
+
+def test_neg_inf_logits_off_target():
+    """-inf logits (masked vocab entries): the reference's entropy is NaN for that row, the
+    token loss is NaN (counted by num_nans) and nan_to_num drops it from the sums."""
+    T, V = 9, 1024
+    b = _batch(T, V, seed=4)
+    lg = synth.to_bf16(np.random.default_rng(4).normal(0, 2, (1, T, V))).astype(np.float32)
+    tgt = b["input_ids"][0, 1:]
+    col = (tgt[3] + 1) % V
+    lg[0, 3, col] = -np.inf
+    loss, stats, d = _run(lg, b)
+    o = grpo_oracle.rl_step_oracle(lg, b, CFG, 0, 10)
+    assert stats["num_nans"] == o["stats"]["num_nans"] >= 1
+    assert abs(loss - o["loss"]) <= 1e-4 * max(1, abs(o["loss"]))
+    other = [r for r in range(T - 1) if r != 3]
+    ok, err = rel_close(d[0, other], o["dlogits"][0, other], 1e-2, 1e-8)
+    assert ok, err
+    assert np.all(d[0, 3] == 0)  # non-finite token loss: no gradient (the reference gets NaN here)
+
+
+@pytest.mark.parametrize("V", [24 * 8192, 24 * 8192 + 8, 24 * 8192 + 3])
+def test_vocab_size_limits(V):
+    """Largest register-resident vocab (NV = 24), the first streamed one, and a ragged one."""
+    T = 5
+    b = _batch(T, V, seed=5)
+    lg = synth.to_bf16(np.random.default_rng(5).normal(0, 2, (1, T, V))).astype(np.float32)
+    _cmp(lg, b)
+
+
+def test_strided_logits_rows():
+    """logits sliced out of a wider buffer (row stride > V) are consumed without a copy."""
+    from pipelinerl_amd.finetune.rl import RLConfig, rl_step
+
+    T, V, W = 11, 4096, 4096 + 64
+    b = _batch(T, V, seed=6)
+    full = synth.to_bf16(np.random.default_rng(6).normal(0, 2, (1, T, W))).astype(np.float32)
+    base = torch.tensor(full).to(torch.bfloat16).to(DEV).requires_grad_(True)
+    view = base[:, :, :V]
+    assert view.stride(1) == W
+
+    class M(torch.nn.Module):
+        def forward(self, **kw):
+            import types
+            return types.SimpleNamespace(logits=view)
+
+    loss, stats = rl_step(M(), to_batch(b), 0, 10, RLConfig(**CFG))
+    loss.backward()
+    o = grpo_oracle.rl_step_oracle(full[:, :, :V], b, CFG, 0, 10)
+    for k, v in o["stats"].items():
+        assert abs(stats[k] - v) <= 1e-4 * max(1.0, abs(v)), k
+    g = base.grad.float().cpu().numpy()
+    assert rel_close(g[:, :, :V], o["dlogits"], 1e-2, 1e-8)[0]
+    assert np.all(g[:, :, V:] == 0)
+
+
+def test_unpacked_bf16_value_head_ragged():
+    """[B, L] padded batch (collate layout), bf16, value head, rows of different lengths."""
+    B, L, V = 3, 16, 3000
+    rng = np.random.default_rng(7)
+    ids = rng.integers(0, V, (B, L))
+    labels = ids.copy()
+    lens = [16, 11, 6]
+    for i, n in enumerate(lens):
+        labels[i, :3] = -100
+        labels[i, n:] = -100
+    f = lambda v: np.asarray(v, np.float32)  # noqa: E731
+    b = dict(input_ids=ids, labels=labels, attention_mask=np.ones((B, L), np.int64), is_packed=False,
+             rewards=f(np.repeat([[1.0], [0.0], [1.0]], L, 1)), advantages=f(np.repeat([[0.3], [-0.6], [0.3]], L, 1)),
+             ref_logprobs=f(rng.normal(-7, 1, (B, L))), old_logprobs=f(rng.normal(-7, 1, (B, L))),
+             group_tokens=f(np.full((B, L), 11.0)), num_labels=f(np.repeat([[13.0], [8.0], [3.0]], L, 1)),
+             overflow=f(np.zeros((B, L))))
+    lg = synth.to_bf16(rng.normal(0, 2, (B, L, V))).astype(np.float32)
+    values = f(rng.normal(0.2, 0.3, (B, L)))
+    _cmp(lg, b, dict(CFG, value_loss_coef=0.1), values=values)
