@@ -135,6 +135,8 @@ typedef struct PrlGrpoOutputs {
   float* token_loss;           /* (pol - kl_c kl + ent_c H) * w  (unmasked) */
   float* g_lp;                 /* d final / d new_lp  at grad_scale */
   float* g_h;                  /* d final / d entropy at grad_scale */
+  float* row_max;              /* reference max m of the row (raw logit units) */
+  float* row_log2sum;          /* log2 sum_j 2^((x_j - m) log2(e) / temperature) */
   float* dvalues;              /* [B, L] or NULL (required when values != NULL) */
   void* dlogits;               /* [B, L, V], same dtype/ld as logits, or NULL */
   double* stats;               /* [PRL_NSTAT] */
@@ -154,15 +156,16 @@ int prl_grpo_forward(const PrlGrpoBatch* batch, const PrlGrpoParams* params,
                      const PrlGrpoOutputs* out, void* workspace, size_t workspace_bytes,
                      void* stream);
 
-/* Gradient pass from the per-row lse / entropy / g_lp / g_h saved by prl_grpo_forward (at
+/* Gradient pass from the per-row max / log2sum / entropy / g_lp / g_h saved by prl_grpo_forward (at
  * params->grad_scale), for an upstream gradient read ON DEVICE from *upstream (NULL = 1.0):
  *   dlogits = (*upstream) * d final / d logits.
  * If params->write_grad is set, dlogits already holds the gradient for upstream == 1 and
  * the kernel returns without touching memory when *upstream == 1 (no host sync needed to
  * decide).  Rows with zero coefficients are written as zeros without reading the logits. */
 int prl_grpo_backward(const PrlGrpoBatch* batch, const PrlGrpoParams* params,
-                      const float* lse, const float* entropy, const float* g_lp,
-                      const float* g_h, const float* upstream, void* dlogits, void* stream);
+                      const float* row_max, const float* row_log2sum, const float* entropy,
+                      const float* g_lp, const float* g_h, const float* upstream, void* dlogits,
+                      void* stream);
 
 /* Number of statistics (PRL_NSTAT) compiled into the library: bindings check it. */
 int prl_grpo_nstat(void);

@@ -55,7 +55,8 @@ class PrlGrpoParams(ctypes.Structure):
 class PrlGrpoOutputs(ctypes.Structure):
     _fields_ = [
         ("new_logprobs", c_void_p), ("entropy", c_void_p), ("lse", c_void_p),
-        ("token_loss", c_void_p), ("g_lp", c_void_p), ("g_h", c_void_p), ("dvalues", c_void_p),
+        ("token_loss", c_void_p), ("g_lp", c_void_p), ("g_h", c_void_p), ("row_max", c_void_p),
+        ("row_log2sum", c_void_p), ("dvalues", c_void_p),
         ("dlogits", c_void_p), ("stats", c_void_p),
     ]
 
@@ -67,7 +68,7 @@ _SIGNATURES = {
     "prl_grpo_forward": (c_int, [POINTER(PrlGrpoBatch), POINTER(PrlGrpoParams), POINTER(PrlGrpoOutputs),
                                  c_void_p, c_size_t, c_void_p]),
     "prl_grpo_backward": (c_int, [POINTER(PrlGrpoBatch), POINTER(PrlGrpoParams), c_void_p, c_void_p,
-                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "prl_grpo_nstat": (c_int, []),
     "prl_flatten_bf16": (c_int, [POINTER(c_void_p), POINTER(c_int32), POINTER(c_int64), POINTER(c_int64),
                                  c_int32, c_void_p, c_void_p]),

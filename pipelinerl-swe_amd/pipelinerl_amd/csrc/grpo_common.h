@@ -6,8 +6,10 @@
 //   y_j = (x_j - m) c,   s = sum 2^y_j,   w = sum 2^y_j * y_j          (per row)
 //   LSE = m/temperature + ln2 * log2(s)
 //   H   = ln2 * (log2(s) - w/s)                     (entropy, no cancellation vs LSE)
-//   lp_j = ln2 * (x_j c - K),  K = m c + log2(s)
-//   dlogit_j = p_j * (alpha + beta * t_j),  t_j = x_j c - K,  p_j = 2^t_j
+//   lp_j = ln2 * t_j,  t_j = (x_j - m) c - log2(s),  p_j = 2^t_j
+//   dlogit_j = p_j * (alpha + beta * t_j)
+// (x_j - m) is formed first (exact for bf16 inputs), so large logit ranges / small
+// temperatures keep full relative precision near the max (no rounding of m c).
 //              alpha = -(g_lp + g_h H)/temperature,  beta = -g_h ln2 / temperature
 //              plus g_lp/temperature at the target column.
 #pragma once
@@ -85,10 +87,9 @@ __device__ __forceinline__ void lse_add(Lse& st, const float (&x)[N], float c) {
 #pragma unroll
   for (int j = 1; j < N; ++j) vm = fmaxf(vm, x[j]);
   if ((vm - st.m) * c > kRescaleSlack) lse_rebase(st, vm, c);
-  const float mc = st.m * c;
 #pragma unroll
   for (int j = 0; j < N; ++j) {
-    const float y = __builtin_fmaf(x[j], c, -mc);
+    const float y = (x[j] - st.m) * c;
     const float e = fexp2(y);
     st.s += e;
     st.w = __builtin_fmaf(e, y, st.w);
@@ -141,7 +142,7 @@ struct KArgs {
   int policy, use_adv, relu, group_norm, overlong, write_grad;
   float eps, kl_c, ent_c, clampC, temperature, batch_size, value_coef, gscale;
   // outputs
-  float *o_lp, *o_ent, *o_lse, *o_tok, *o_glp, *o_gh, *o_dv;
+  float *o_lp, *o_ent, *o_lse, *o_tok, *o_glp, *o_gh, *o_max, *o_l2s, *o_dv;
   void* dlogits;
   double* partials;  // [gridDim.x][PRL_NSTAT]
 };

@@ -54,13 +54,15 @@ __device__ __forceinline__ Lse block_combine(const float (*red)[3], float c) {
 // per-row epilogue shared by the forward kernels: every lane computes the (uniform) token
 // values and gradient coefficients; `writer` stores the per-row outputs.
 __device__ __forceinline__ TokGrad row_epilogue(const KArgs& a, int64_t q, int64_t tok, float lp,
-                                                float H, float lse, bool writer) {
+                                                float H, float lse, float m, float l2s, bool writer) {
   const TokVals v = token_values(a, tok, lp, H);
   const TokGrad g = token_grad(a, v);
   if (writer) {
     a.o_lp[q] = lp;
     a.o_ent[q] = H;
     a.o_lse[q] = lse;
+    a.o_max[q] = m;
+    a.o_l2s[q] = l2s;
     a.o_tok[q] = v.tl;
     a.o_glp[q] = g.g_lp;
     a.o_gh[q] = g.g_h;
@@ -143,11 +145,11 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
     __syncthreads();
     const Lse tot = block_combine<NW>(red[par], c);
     const float l2s = log2f(tot.s);
-    const float K = tot.m * c + l2s;
-    const float lse = tot.m * inv_t + kLn2 * l2s;
+    const float M = tot.m;
+    const float lse = M * inv_t + kLn2 * l2s;
     const float H = kLn2 * (l2s - tot.w / tot.s);
-    const float lp = xt * inv_t - lse;
-    const TokGrad core = row_epilogue(a, q, tok, lp, H, lse, tid == 0);
+    const float lp = (xt - M) * inv_t - kLn2 * l2s;
+    const TokGrad core = row_epilogue(a, q, tok, lp, H, lse, M, l2s, tid == 0);
     // Make the packed row opaque here so the compiler re-unpacks it in pass 2 instead of
     // keeping pass 1's unpacked floats alive (8 instead of 4 VGPRs per vector -> spills).
 #pragma unroll
@@ -187,7 +189,7 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const float x0 = bf_lo(buf[k][j]), x1 = bf_hi(buf[k][j]);
-            const float t0 = __builtin_fmaf(x0, c, -K), t1 = __builtin_fmaf(x1, c, -K);
+            const float t0 = __builtin_fmaf(x0 - M, c, -l2s), t1 = __builtin_fmaf(x1 - M, c, -l2s);
             const float p0 = fexp2(t0), p1 = fexp2(t1);
             d[2 * j] = p0 * __builtin_fmaf(beta, t0, alpha);
             d[2 * j + 1] = p1 * __builtin_fmaf(beta, t1, alpha);
@@ -264,12 +266,12 @@ __device__ __forceinline__ float scalar_logit<float>(const float* row, int64_t j
 
 // gradient of one vector: d_j = p_j (alpha + beta t_j) (+ gadd at the target column)
 template <int VEC>
-__device__ __forceinline__ void grad_vec(const float (&x)[VEC], float (&d)[VEC], float c, float K,
-                                         float alpha, float beta, int64_t base, int64_t tgt,
+__device__ __forceinline__ void grad_vec(const float (&x)[VEC], float (&d)[VEC], float c, float M,
+                                         float l2s, float alpha, float beta, int64_t base, int64_t tgt,
                                          float gadd) {
 #pragma unroll
   for (int j = 0; j < VEC; ++j) {
-    const float t = __builtin_fmaf(x[j], c, -K);
+    const float t = __builtin_fmaf(x[j] - M, c, -l2s);
     d[j] = fexp2(t) * __builtin_fmaf(beta, t, alpha);
     if (base + j == tgt) d[j] += gadd;
   }
@@ -310,11 +312,11 @@ __global__ __launch_bounds__(256) void grpo_fwd_stream(KArgs a) {
     __syncthreads();
     const Lse tot = block_combine<NW>(red[par], c);
     const float l2s = log2f(tot.s);
-    const float K = tot.m * c + l2s;
-    const float lse = tot.m * inv_t + kLn2 * l2s;
+    const float M = tot.m;
+    const float lse = M * inv_t + kLn2 * l2s;
     const float H = kLn2 * (l2s - tot.w / tot.s);
-    const float lp = xt * inv_t - lse;
-    const TokGrad core = row_epilogue(a, q, tok, lp, H, lse, tid == 0);
+    const float lp = (xt - M) * inv_t - kLn2 * l2s;
+    const TokGrad core = row_epilogue(a, q, tok, lp, H, lse, M, l2s, tid == 0);
     if (a.write_grad) {
       T* drow = dl + lrow * a.ld;
       const float alpha = -(core.g_lp + core.g_h * H) * inv_t;
@@ -329,7 +331,7 @@ __global__ __launch_bounds__(256) void grpo_fwd_stream(KArgs a) {
         } else {
           float x[VEC];
           RowIO<T, VEC>::load(row, gv, x);
-          grad_vec<VEC>(x, d, c, K, alpha, beta, gv * VEC, tgt, gadd);
+          grad_vec<VEC>(x, d, c, M, l2s, alpha, beta, gv * VEC, tgt, gadd);
         }
         RowIO<T, VEC>::store(drow, gv, d);
       }
@@ -340,7 +342,7 @@ __global__ __launch_bounds__(256) void grpo_fwd_stream(KArgs a) {
 // gradient pass from saved per-row coefficients for the upstream gradient *up (device);
 // skip_if_one: dlogits already holds the gradient for *up == 1 (fused forward)
 template <typename T, int VEC>
-__global__ __launch_bounds__(256) void grpo_bwd_stream(KArgs a, const float* lse_in,
+__global__ __launch_bounds__(256) void grpo_bwd_stream(KArgs a, const float* max_in, const float* l2s_in,
                                                        const float* ent_in, const float* glp_in,
                                                        const float* gh_in, const float* up,
                                                        int skip_if_one) {
@@ -363,7 +365,7 @@ __global__ __launch_bounds__(256) void grpo_bwd_stream(KArgs a, const float* lse
     const int64_t tgt = (uint64_t)tid_raw >= (uint64_t)a.V ? -1 : tid_raw;
     const float g_lp = glp_in[q] * scale, g_h = gh_in[q] * scale;
     const float H = ent_in[q];
-    const float K = lse_in[q] * kLog2e;  // K = m c + log2 s = LSE * log2(e)
+    const float M = max_in[q], l2s = l2s_in[q];
     const float alpha = -(g_lp + g_h * H) * inv_t;
     const float beta = -g_h * kLn2 * inv_t;
     const float gadd = g_lp * inv_t;
@@ -376,7 +378,7 @@ __global__ __launch_bounds__(256) void grpo_bwd_stream(KArgs a, const float* lse
       } else {
         float x[VEC];
         RowIO<T, VEC>::load(row, gv, x);
-        grad_vec<VEC>(x, d, c, K, alpha, beta, gv * VEC, tgt, gadd);
+        grad_vec<VEC>(x, d, c, M, l2s, alpha, beta, gv * VEC, tgt, gadd);
       }
       RowIO<T, VEC>::store(drow, gv, d);
     }
@@ -605,7 +607,7 @@ int prl_grpo_forward(const PrlGrpoBatch* batch, const PrlGrpoParams* params,
   int rc = fill_args(a, batch, params);
   if (rc) return rc;
   if (!out || !out->new_logprobs || !out->entropy || !out->lse || !out->token_loss || !out->g_lp ||
-      !out->g_h || !out->stats)
+      !out->g_h || !out->row_max || !out->row_log2sum || !out->stats)
     return PRL_E_INVALID;
   if (batch->values && !out->dvalues) return PRL_E_INVALID;
   if (params->write_grad && !out->dlogits) return PRL_E_INVALID;
@@ -614,6 +616,8 @@ int prl_grpo_forward(const PrlGrpoBatch* batch, const PrlGrpoParams* params,
   a.o_lp = out->new_logprobs;
   a.o_ent = out->entropy;
   a.o_lse = out->lse;
+  a.o_max = out->row_max;
+  a.o_l2s = out->row_log2sum;
   a.o_tok = out->token_loss;
   a.o_glp = out->g_lp;
   a.o_gh = out->g_h;
@@ -678,13 +682,13 @@ int prl_grpo_forward(const PrlGrpoBatch* batch, const PrlGrpoParams* params,
   return (int)hipGetLastError();
 }
 
-int prl_grpo_backward(const PrlGrpoBatch* batch, const PrlGrpoParams* params, const float* lse,
-                      const float* entropy, const float* g_lp, const float* g_h, const float* upstream,
-                      void* dlogits, void* stream) {
+int prl_grpo_backward(const PrlGrpoBatch* batch, const PrlGrpoParams* params, const float* row_max,
+                      const float* row_log2sum, const float* entropy, const float* g_lp, const float* g_h,
+                      const float* upstream, void* dlogits, void* stream) {
   KArgs a;
   int rc = fill_args(a, batch, params);
   if (rc) return rc;
-  if (!lse || !entropy || !g_lp || !g_h || !dlogits) return PRL_E_INVALID;
+  if (!row_max || !row_log2sum || !entropy || !g_lp || !g_h || !dlogits) return PRL_E_INVALID;
   a.dlogits = dlogits;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int skip = params->write_grad ? 1 : 0;
@@ -703,13 +707,13 @@ int prl_grpo_backward(const PrlGrpoBatch* batch, const PrlGrpoParams* params, co
   const int grid = (int)(nrows < want ? nrows : want);
   const bool bf16 = batch->logits_dtype == PRL_BF16;
   if (bf16 && batch->V % 8 == 0 && batch->ld % 8 == 0 && aligned16(batch->logits) && aligned16(dlogits)) {
-    hipLaunchKernelGGL((grpo_bwd_stream<uint16_t, 8>), dim3(grid), dim3(256), 0, s, a, lse, entropy, g_lp, g_h, upstream, skip);
+    hipLaunchKernelGGL((grpo_bwd_stream<uint16_t, 8>), dim3(grid), dim3(256), 0, s, a, row_max, row_log2sum, entropy, g_lp, g_h, upstream, skip);
   } else if (bf16) {
-    hipLaunchKernelGGL((grpo_bwd_stream<uint16_t, 1>), dim3(grid), dim3(256), 0, s, a, lse, entropy, g_lp, g_h, upstream, skip);
+    hipLaunchKernelGGL((grpo_bwd_stream<uint16_t, 1>), dim3(grid), dim3(256), 0, s, a, row_max, row_log2sum, entropy, g_lp, g_h, upstream, skip);
   } else if (batch->V % 4 == 0 && batch->ld % 4 == 0 && aligned16(batch->logits) && aligned16(dlogits)) {
-    hipLaunchKernelGGL((grpo_bwd_stream<float, 4>), dim3(grid), dim3(256), 0, s, a, lse, entropy, g_lp, g_h, upstream, skip);
+    hipLaunchKernelGGL((grpo_bwd_stream<float, 4>), dim3(grid), dim3(256), 0, s, a, row_max, row_log2sum, entropy, g_lp, g_h, upstream, skip);
   } else {
-    hipLaunchKernelGGL((grpo_bwd_stream<float, 1>), dim3(grid), dim3(256), 0, s, a, lse, entropy, g_lp, g_h, upstream, skip);
+    hipLaunchKernelGGL((grpo_bwd_stream<float, 1>), dim3(grid), dim3(256), 0, s, a, row_max, row_log2sum, entropy, g_lp, g_h, upstream, skip);
   }
   return (int)hipGetLastError();
 }

@@ -116,10 +116,12 @@ class GrpoLossFn(torch.autograd.Function):
         B, L, V = x.shape
         dev = x.device
         R = max(B * (L - 1), 1)
-        rows = torch.empty((6, R), dtype=torch.float32, device=dev)  # lp, H, lse, tok_loss, g_lp, g_h
+        # lp, H, lse, tok_loss, g_lp, g_h, row max, row log2-sum
+        rows = torch.empty((8, R), dtype=torch.float32, device=dev)
         stats = torch.empty(NSTAT, dtype=torch.float64, device=dev)
         write_grad = bool(logits.requires_grad)
-        dlogits = torch.empty_like(x) if write_grad else None
+        # same strides as the logits (a view with a wider row stride keeps its layout)
+        dlogits = torch.empty_strided(x.shape, x.stride(), dtype=x.dtype, device=dev) if write_grad else None
         vals = None
         dvalues = None
         if values is not None:
@@ -127,8 +129,7 @@ class GrpoLossFn(torch.autograd.Function):
             dvalues = torch.empty((B, L), dtype=torch.float32, device=dev)
         cb = _c_batch(x, fields, vals)
         cp = params.to_c(write_grad)
-        co = _native.PrlGrpoOutputs(rows[0].data_ptr(), rows[1].data_ptr(), rows[2].data_ptr(), rows[3].data_ptr(),
-                                    rows[4].data_ptr(), rows[5].data_ptr(), _ptr(dvalues), _ptr(dlogits),
+        co = _native.PrlGrpoOutputs(*[rows[i].data_ptr() for i in range(8)], _ptr(dvalues), _ptr(dlogits),
                                     stats.data_ptr())
         ws = _workspace(dev)
         stream = torch.cuda.current_stream(dev).cuda_stream
@@ -159,8 +160,8 @@ class GrpoLossFn(torch.autograd.Function):
             cp = ctx.params.to_c(True)
             r = ctx.rows
             stream = torch.cuda.current_stream(ctx.x.device).cuda_stream
-            _native.check(lib.prl_grpo_backward(ctypes.byref(cb), ctypes.byref(cp), r[2].data_ptr(), r[1].data_ptr(),
-                                                r[4].data_ptr(), r[5].data_ptr(), g.data_ptr(),
+            _native.check(lib.prl_grpo_backward(ctypes.byref(cb), ctypes.byref(cp), r[6].data_ptr(), r[7].data_ptr(),
+                                                r[1].data_ptr(), r[4].data_ptr(), r[5].data_ptr(), g.data_ptr(),
                                                 ctx.dlogits.data_ptr(), stream), "prl_grpo_backward")
             d_logits = ctx.dlogits if ctx.logits_dtype == ctx.dlogits.dtype else ctx.dlogits.to(ctx.logits_dtype)
         if ctx.dvalues is not None and ctx.needs_input_grad[1]:
@@ -171,5 +172,6 @@ class GrpoLossFn(torch.autograd.Function):
 
 def grpo_loss(logits: torch.Tensor, fields: dict, params: GrpoParams, values: torch.Tensor | None = None):
     """Returns (loss [float32 scalar, differentiable], stats [NSTAT] float64 device tensor,
-    rows [6, B*(L-1)] float32: new_logprobs, entropy, lse, token_loss, g_lp, g_h)."""
+    rows [8, B*(L-1)] float32: new_logprobs, entropy, lse, token_loss, g_lp, g_h, row max,
+    row log2-sum)."""
     return GrpoLossFn.apply(logits, values, fields, params)

@@ -36,7 +36,7 @@ def test_struct_layouts():
 
     assert ctypes.sizeof(_native.PrlGrpoBatch) == 8 + 4 + 4 + 4 * 8 + 10 * 8
     assert ctypes.sizeof(_native.PrlGrpoParams) == 6 * 4 + 8 * 4
-    assert ctypes.sizeof(_native.PrlGrpoOutputs) == 9 * 8
+    assert ctypes.sizeof(_native.PrlGrpoOutputs) == 11 * 8
 
 
 def test_invalid_arguments_rejected_without_gpu():
