@@ -66,9 +66,19 @@ def _nz(x: np.ndarray) -> np.ndarray:
 
 
 def _masked_sum(v: np.ndarray, m: np.ndarray) -> float:
-    """mask_sum: (values * mask).nan_to_num(0).sum() (utils.py:25-30)."""
+    """mask_sum: (values * mask).nan_to_num(0).sum() (utils.py:25-30); the reference reports the
+    float32 value of the sum (inf when it exceeds the float32 range)."""
     with np.errstate(invalid="ignore", over="ignore"):
-        return float(_nz(v * m).sum(dtype=np.float64))
+        return float(np.float32(_nz(v * m).sum(dtype=np.float64)))
+
+
+LN_FLT_MAX = float(np.log(np.finfo(np.float32).max))
+
+
+def _exp32(x: np.ndarray) -> np.ndarray:
+    """exp with float32 overflow semantics (the reference's token-level tensors are float32)."""
+    with np.errstate(over="ignore", invalid="ignore"):
+        return np.where(x > LN_FLT_MAX, np.inf, np.exp(np.minimum(x, LN_FLT_MAX)))
 
 
 def num_sequences_of(batch: dict) -> int:
@@ -183,7 +193,7 @@ def rl_step_oracle(logits: np.ndarray, batch: dict, config: dict, current_step: 
 
     with np.errstate(over="ignore", invalid="ignore", divide="ignore"):
         log_ratio_new_old = new_lp - old_lp  # :234-236
-        ratio = np.exp(log_ratio_new_old)
+        ratio = _exp32(log_ratio_new_old)
         log_ratio_ref_new = ref_lp - new_lp
         if not np.isfinite(log_ratio_ref_new).all():  # :237
             raise AssertionError(f"log_ratio_ref_new is not finite: {log_ratio_ref_new}")
@@ -254,8 +264,8 @@ def rl_step_oracle(logits: np.ndarray, batch: dict, config: dict, current_step: 
                 "ratio_new_old": S(ratio_used / num_labels),
                 "ratio_new_old_sum": S(ratio_used),
                 "ratio_new_old_squared_sum": S(ratio_used * ratio_used),
-                "ratio_ref_new": S(np.exp(log_ratio_ref_new) / num_labels),
-                "ratio_ref_old": S(np.exp(ref_lp - old_lp) / num_labels),
+                "ratio_ref_new": S(_exp32(log_ratio_ref_new) / num_labels),
+                "ratio_ref_old": S(_exp32(ref_lp - old_lp) / num_labels),
                 "clamp_log_ratio_ref_new_indicator": S(ind_ref / num_labels),
                 "clamp_log_ratio_new_old_indicator": S(ind_no / num_labels),
                 "num_nans": int(np.isnan(tok_loss).sum()),

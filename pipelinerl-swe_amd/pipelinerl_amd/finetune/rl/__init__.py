@@ -139,6 +139,10 @@ def build_stats(h: np.ndarray, batch, params: GrpoParams, kl_c: float, ent_c: fl
     input_size = int(batch.input_ids.numel())
     if h[S["NUM_OUT"]] == 0:
         return {"input_size": float(input_size)}
+    # the reference reports float32 values (.item() of float32 tensors): round the fp64
+    # accumulators, so a sum beyond the float32 range reads inf as it does there
+    with np.errstate(over="ignore"):
+        h = h.astype(np.float32).astype(np.float64)
     f = lambda k: float(h[S[k]])  # noqa: E731
     stats = {
         "loss": final, "max_loss": final, "min_loss": final,

@@ -1,0 +1,51 @@
+"""Turn two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE; separate runs, csv output) of
+bench.py into the per-launch HBM traffic JSON that bench.py's roofline reads.
+
+  python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write profiles/r01_pmc_traffic.json
+
+Corrections per /opt/skills/guides/MI355X_MICROARCH.md (HBM section, gfx950): FETCH_SIZE is in
+KB and counts 16-B/lane streaming reads at half rate (x1024 x2); WRITE_SIZE is in KB (x1024).
+"""
+
+from __future__ import annotations
+
+import csv
+import json
+import sys
+from pathlib import Path
+
+KERNEL = "grpo_fwd_resident<19>"
+T, V = 65536, 151936
+
+
+def per_launch(d: Path, counter: str) -> tuple[float, int]:
+    f = next(d.rglob("*counter_collection.csv"))
+    vals: dict[str, float] = {}
+    with open(f) as fh:
+        for r in csv.DictReader(fh):
+            if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == counter:
+                vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+    if not vals:
+        raise SystemExit(f"no {counter} rows for {KERNEL} in {f}")
+    return sum(vals.values()) / len(vals), len(vals)
+
+
+def main(fetch_dir: str, write_dir: str, out: str) -> None:
+    fkb, n = per_launch(Path(fetch_dir), "FETCH_SIZE")
+    wkb, _ = per_launch(Path(write_dir), "WRITE_SIZE")
+    rd, wr = fkb * 1024 * 2, wkb * 1024
+    alg = 2.0 * T * V * 2 + T * 37
+    res = {"kernel": f"prl::{KERNEL}", "T": T, "V": V, "dtype": "bf16",
+           "FETCH_SIZE_KB_per_launch": fkb, "WRITE_SIZE_KB_per_launch": wkb,
+           "read_bytes_corrected": rd, "write_bytes": wr, "bytes_per_launch": rd + wr,
+           "algorithmic_bytes": alg, "traffic_over_algorithmic": (rd + wr) / alg,
+           "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes, --output-format csv, "
+                     "bench.py --steps 3 --warmup 1 --no-cpu-baseline; FETCH_SIZE x1024 x2 (gfx950 half-count on "
+                     "16-B/lane streaming reads), WRITE_SIZE x1024; mean over launches",
+           "launches": n}
+    Path(out).write_text(json.dumps(res, indent=1))
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:4])
