@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PRL_ABI_VERSION 1
+#define PRL_ABI_VERSION 2
 
 /* error codes (besides hipError_t values, which are < 1000) */
 #define PRL_OK 0
@@ -155,6 +155,25 @@ int prl_grpo_workspace_bytes(int device, size_t* bytes);
 int prl_grpo_forward(const PrlGrpoBatch* batch, const PrlGrpoParams* params,
                      const PrlGrpoOutputs* out, void* workspace, size_t workspace_bytes,
                      void* stream);
+
+/* Row-selected vocab pass (label rows only; chunked lm_head + loss).
+ * batch->logits holds n rows [n, ld]; logits row i scores batch row row_ids[i] (device
+ * int64, q = b*(L-1) + t, each < B*(L-1)); B and L describe the whole batch, whose token
+ * fields are read at those rows.  Per-row outputs land at index row_ids[i] of the
+ * B*(L-1)-entry arrays; dlogits (write_grad) is [n, ld] and may alias batch->logits
+ * (every row is read before its gradient is stored).  No statistics (out->stats unused)
+ * and no value head (values must be NULL).  Replaces the [T, V] slice of the ATen chain
+ * rl/__init__.py:199-208 for the rows its mask (:152-153) keeps. */
+int prl_grpo_forward_rows(const PrlGrpoBatch* batch, const PrlGrpoParams* params,
+                          const int64_t* row_ids, int64_t n, const PrlGrpoOutputs* out,
+                          void* stream);
+
+/* Statistics (rl/__init__.py:315-375) and dvalues from the per-row new_logprobs / entropy
+ * arrays over all B*(L-1) rows (batch->logits may be NULL).  Rows never scored must hold
+ * finite values (e.g. 0): masked rows only enter num_nans and the finiteness counters. */
+int prl_grpo_stats(const PrlGrpoBatch* batch, const PrlGrpoParams* params,
+                   const PrlGrpoOutputs* out, void* workspace, size_t workspace_bytes,
+                   void* stream);
 
 /* Gradient pass from the per-row max / log2sum / entropy / g_lp / g_h saved by prl_grpo_forward (at
  * params->grad_scale), for an upstream gradient read ON DEVICE from *upstream (NULL = 1.0):

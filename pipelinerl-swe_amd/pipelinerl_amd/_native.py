@@ -15,6 +15,7 @@ _PKG = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ["PRL_LIB"]) if os.environ.get("PRL_LIB") else _PKG / "libprl_hip.so"
 HEADER_PATH = _PKG.parents[1] / "include" / "prl_hip.h"
 
+ABI_VERSION = 2
 PRL_F32, PRL_BF16 = 0, 1
 PRL_PPO, PRL_REINFORCE = 0, 1
 
@@ -69,6 +70,10 @@ _SIGNATURES = {
                                  c_void_p, c_size_t, c_void_p]),
     "prl_grpo_backward": (c_int, [POINTER(PrlGrpoBatch), POINTER(PrlGrpoParams), c_void_p, c_void_p,
                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "prl_grpo_forward_rows": (c_int, [POINTER(PrlGrpoBatch), POINTER(PrlGrpoParams), c_void_p, c_int64,
+                                      POINTER(PrlGrpoOutputs), c_void_p]),
+    "prl_grpo_stats": (c_int, [POINTER(PrlGrpoBatch), POINTER(PrlGrpoParams), POINTER(PrlGrpoOutputs),
+                               c_void_p, c_size_t, c_void_p]),
     "prl_grpo_nstat": (c_int, []),
     "prl_flatten_bf16": (c_int, [POINTER(c_void_p), POINTER(c_int32), POINTER(c_int64), POINTER(c_int64),
                                  c_int32, c_void_p, c_void_p]),
@@ -110,6 +115,8 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.prl_abi_version() != ABI_VERSION:
+        raise PrlError(f"libprl_hip.so has ABI {lib.prl_abi_version()}, binding expects {ABI_VERSION}: rebuild it")
     if lib.prl_grpo_nstat() != NSTAT:
         raise PrlError(f"libprl_hip.so has {lib.prl_grpo_nstat()} statistics, binding expects {NSTAT}")
     _lib = lib

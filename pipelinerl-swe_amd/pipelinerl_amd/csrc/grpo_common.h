@@ -145,6 +145,9 @@ struct KArgs {
   float *o_lp, *o_ent, *o_lse, *o_tok, *o_glp, *o_gh, *o_max, *o_l2s, *o_dv;
   void* dlogits;
   double* partials;  // [gridDim.x][PRL_NSTAT]
+  // row selection (prl_grpo_forward_rows): logits row i scores batch row row_ids[i]
+  const int64_t* row_ids;
+  int64_t nsel;
 };
 
 // Per-token quantities of rl/__init__.py:212-292 for one loss row.
@@ -264,6 +267,22 @@ __device__ __forceinline__ void row_of(const KArgs& a, int64_t q, int64_t& lrow,
   const int64_t t = q - b * Lm1;
   lrow = b * a.L + t;
   tok = lrow + 1;
+}
+
+// number of logits rows a forward kernel walks
+__device__ __forceinline__ int64_t fwd_rows(const KArgs& a) { return a.row_ids ? a.nsel : a.B * (a.L - 1); }
+
+// logits row i -> (logits row offset, token index, output row q)
+__device__ __forceinline__ void map_row(const KArgs& a, int64_t i, int64_t& lrow, int64_t& tok, int64_t& q) {
+  if (a.row_ids) {
+    q = a.row_ids[i];
+    int64_t full;
+    row_of(a, q, full, tok);
+    lrow = i;
+  } else {
+    q = i;
+    row_of(a, i, lrow, tok);
+  }
 }
 
 }  // namespace prl

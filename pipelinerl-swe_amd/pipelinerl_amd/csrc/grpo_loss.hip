@@ -93,7 +93,7 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
   constexpr int VSTRIDE = BLOCK * 16;  // bytes between a lane's consecutive vectors
   __shared__ float red[2][NW][3];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int64_t nrows = a.B * (a.L - 1);
+  const int64_t nrows = fwd_rows(a);
   const int nvec = (int)(a.V >> 3);
   const int64_t row_bytes = a.V * 2;
   const float c = kLog2e / a.temperature;
@@ -106,8 +106,8 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
   u32x4 buf[NV];
   int64_t q = blockIdx.x;
   if (q < nrows) {
-    int64_t lrow, tok;
-    row_of(a, q, lrow, tok);
+    int64_t lrow, tok, qo;
+    map_row(a, q, lrow, tok, qo);
     const auto rs = row_rsrc(lg + lrow * a.ld, row_bytes);
 #pragma unroll
     for (int k = 0; k < NV; ++k)
@@ -115,8 +115,8 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
   }
   int par = 0;
   for (; q < nrows; q += gridDim.x, par ^= 1) {
-    int64_t lrow, tok;
-    row_of(a, q, lrow, tok);
+    int64_t lrow, tok, qo;
+    map_row(a, q, lrow, tok, qo);
     const int64_t tid_raw = a.input_ids[tok];
     const bool bad_id = (uint64_t)tid_raw >= (uint64_t)a.V;
     const int64_t tgt = bad_id ? -1 : tid_raw;  // -1: never matches a column below
@@ -149,7 +149,7 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
     const float lse = M * inv_t + kLn2 * l2s;
     const float H = kLn2 * (l2s - tot.w / tot.s);
     const float lp = (xt - M) * inv_t - kLn2 * l2s;
-    const TokGrad core = row_epilogue(a, q, tok, lp, H, lse, M, l2s, tid == 0);
+    const TokGrad core = row_epilogue(a, qo, tok, lp, H, lse, M, l2s, tid == 0);
     // Make the packed row opaque here so the compiler re-unpacks it in pass 2 instead of
     // keeping pass 1's unpacked floats alive (8 instead of 4 VGPRs per vector -> spills).
 #pragma unroll
@@ -160,8 +160,8 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
     const bool has_next = qn < nrows;
     int64_t nlrow = lrow;
     if (has_next) {
-      int64_t nt;
-      row_of(a, qn, nlrow, nt);
+      int64_t nt, nq;
+      map_row(a, qn, nlrow, nt, nq);
     }
     const auto rn = row_rsrc(lg + nlrow * a.ld, has_next ? row_bytes : 0);
     if (a.write_grad) {
@@ -282,16 +282,16 @@ __global__ __launch_bounds__(256) void grpo_fwd_stream(KArgs a) {
   constexpr int BLOCK = 256, NW = BLOCK / 64;
   __shared__ float red[2][NW][3];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int64_t nrows = a.B * (a.L - 1);
+  const int64_t nrows = fwd_rows(a);
   const int64_t nvec = a.V / VEC;
   const float c = kLog2e / a.temperature;
   const float inv_t = 1.0f / a.temperature;
   const T* lg = static_cast<const T*>(a.logits);
   T* dl = static_cast<T*>(a.dlogits);
   int par = 0;
-  for (int64_t q = blockIdx.x; q < nrows; q += gridDim.x, par ^= 1) {
-    int64_t lrow, tok;
-    row_of(a, q, lrow, tok);
+  for (int64_t i = blockIdx.x; i < nrows; i += gridDim.x, par ^= 1) {
+    int64_t lrow, tok, q;
+    map_row(a, i, lrow, tok, q);
     const T* row = lg + lrow * a.ld;
     const int64_t tid_raw = a.input_ids[tok];
     const bool bad_id = (uint64_t)tid_raw >= (uint64_t)a.V;
@@ -510,10 +510,10 @@ static int device_cus(int dev) {
 
 static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
-static int fill_args(KArgs& a, const PrlGrpoBatch* b, const PrlGrpoParams* p) {
+static int fill_args(KArgs& a, const PrlGrpoBatch* b, const PrlGrpoParams* p, bool need_logits = true) {
   if (!b || !p) return PRL_E_INVALID;
   if (b->B < 1 || b->L < 1 || b->V < 1 || b->ld < b->V) return PRL_E_INVALID;
-  if (!b->logits || !b->input_ids || !b->labels || !b->rewards || !b->advantages || !b->ref_logprobs ||
+  if ((need_logits && !b->logits) || !b->input_ids || !b->labels || !b->rewards || !b->advantages || !b->ref_logprobs ||
       !b->old_logprobs || !b->group_tokens || !b->num_labels || !b->overflow)
     return PRL_E_INVALID;
   if (b->logits_dtype != PRL_BF16 && b->logits_dtype != PRL_F32) return PRL_E_UNSUPPORTED;
@@ -575,6 +575,72 @@ static hipError_t launch_resident_nv(int nv, const KArgs& a, int grid, hipStream
   return launch_resident_table(nv, a, grid, s, std::make_integer_sequence<int, kMaxNV>{});
 }
 
+// per-row outputs (+ dlogits); the row arrays are indexed by batch row q
+static int fill_outputs(KArgs& a, const PrlGrpoBatch* b, const PrlGrpoParams* p, const PrlGrpoOutputs* out,
+                        bool need_stats) {
+  if (!out || !out->new_logprobs || !out->entropy || !out->lse || !out->token_loss || !out->g_lp ||
+      !out->g_h || !out->row_max || !out->row_log2sum || (need_stats && !out->stats))
+    return PRL_E_INVALID;
+  if (b->values && !out->dvalues) return PRL_E_INVALID;
+  if (p->write_grad && !out->dlogits) return PRL_E_INVALID;
+  a.o_lp = out->new_logprobs;
+  a.o_ent = out->entropy;
+  a.o_lse = out->lse;
+  a.o_max = out->row_max;
+  a.o_l2s = out->row_log2sum;
+  a.o_tok = out->token_loss;
+  a.o_glp = out->g_lp;
+  a.o_gh = out->g_h;
+  a.o_dv = out->dvalues;
+  a.dlogits = out->dlogits;
+  return PRL_OK;
+}
+
+// the vocab pass over `nrows` logits rows: register-resident kernel when a bf16 row fits,
+// streaming kernels otherwise
+static hipError_t launch_rows(const KArgs& a, const PrlGrpoBatch* b, const PrlGrpoParams* p,
+                              const PrlGrpoOutputs* out, int64_t nrows, hipStream_t s) {
+  if (nrows <= 0) return hipSuccess;
+  int dev = 0;
+  hipGetDevice(&dev);
+  const int cus = device_cus(dev);
+  const bool bf16 = b->logits_dtype == PRL_BF16;
+  const bool vec_ok_bf = bf16 && b->V % 8 == 0 && b->ld % 8 == 0 && aligned16(b->logits) &&
+                         (!p->write_grad || aligned16(out->dlogits));
+  const int nv = vec_ok_bf ? resident_nv(b->V / 8) : 0;  // row <= 24*16 KiB
+  if (nv > 0) return launch_resident_nv(nv, a, (int)(nrows < cus ? nrows : cus), s);
+  const int64_t want = (int64_t)cus * 4;
+  int grid = (int)(nrows < want ? nrows : want);
+  if (grid > kMaxGrid) grid = kMaxGrid;
+  if (vec_ok_bf) {
+    hipLaunchKernelGGL((grpo_fwd_stream<uint16_t, 8>), dim3(grid), dim3(256), 0, s, a);
+  } else if (bf16) {
+    hipLaunchKernelGGL((grpo_fwd_stream<uint16_t, 1>), dim3(grid), dim3(256), 0, s, a);
+  } else if (b->V % 4 == 0 && b->ld % 4 == 0 && aligned16(b->logits) &&
+             (!p->write_grad || aligned16(out->dlogits))) {
+    hipLaunchKernelGGL((grpo_fwd_stream<float, 4>), dim3(grid), dim3(256), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((grpo_fwd_stream<float, 1>), dim3(grid), dim3(256), 0, s, a);
+  }
+  return hipGetLastError();
+}
+
+// statistics + value gradient over all batch rows: fixed row chunks per block (deterministic)
+static hipError_t launch_stats(const KArgs& a, int64_t nrows, double* stats, hipStream_t s) {
+  int sblocks = 0;
+  if (nrows > 0) {
+    // ~256 rows per 256-thread block: one row per thread, enough blocks to fill the chip
+    int64_t chunk = (nrows + kMaxGrid - 1) / kMaxGrid;
+    if (chunk < kStatThreads) chunk = kStatThreads;
+    sblocks = (int)((nrows + chunk - 1) / chunk);
+    hipLaunchKernelGGL(grpo_stats_partial, dim3(sblocks), dim3(kStatThreads), 0, s, a, chunk);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(grpo_finalize, dim3(1), dim3(PRL_NSTAT * kFinLanes), 0, s, a.partials, sblocks, stats);
+  return hipGetLastError();
+}
+
 }  // namespace prl
 
 using namespace prl;
@@ -606,23 +672,10 @@ int prl_grpo_forward(const PrlGrpoBatch* batch, const PrlGrpoParams* params,
   KArgs a;
   int rc = fill_args(a, batch, params);
   if (rc) return rc;
-  if (!out || !out->new_logprobs || !out->entropy || !out->lse || !out->token_loss || !out->g_lp ||
-      !out->g_h || !out->row_max || !out->row_log2sum || !out->stats)
-    return PRL_E_INVALID;
-  if (batch->values && !out->dvalues) return PRL_E_INVALID;
-  if (params->write_grad && !out->dlogits) return PRL_E_INVALID;
+  rc = fill_outputs(a, batch, params, out, true);
+  if (rc) return rc;
   if (!workspace || workspace_bytes < sizeof(double) * (size_t)kMaxGrid * PRL_NSTAT) return PRL_E_WORKSPACE;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  a.o_lp = out->new_logprobs;
-  a.o_ent = out->entropy;
-  a.o_lse = out->lse;
-  a.o_max = out->row_max;
-  a.o_l2s = out->row_log2sum;
-  a.o_tok = out->token_loss;
-  a.o_glp = out->g_lp;
-  a.o_gh = out->g_h;
-  a.o_dv = out->dvalues;
-  a.dlogits = out->dlogits;
   a.partials = static_cast<double*>(workspace);
   const size_t es = batch->logits_dtype == PRL_BF16 ? 2 : 4;
   hipError_t e;
@@ -637,49 +690,44 @@ int prl_grpo_forward(const PrlGrpoBatch* batch, const PrlGrpoParams* params,
     if (e != hipSuccess) return (int)e;
   }
   const int64_t nrows = batch->B * (batch->L - 1);
-  int dev = 0;
-  hipGetDevice(&dev);
-  const int cus = device_cus(dev);
-  int grid = 0;
-  if (nrows > 0) {
-    const bool bf16 = batch->logits_dtype == PRL_BF16;
-    const bool vec_ok_bf = bf16 && batch->V % 8 == 0 && batch->ld % 8 == 0 && aligned16(batch->logits) &&
-                           (!params->write_grad || aligned16(out->dlogits));
-    const int nv = vec_ok_bf ? resident_nv(batch->V / 8) : 0;  // row <= 24*16 KiB
-    if (nv > 0) {
-      grid = (int)(nrows < cus ? nrows : cus);
-      e = launch_resident_nv(nv, a, grid, s);
-    } else {
-      const int64_t want = (int64_t)cus * 4;
-      grid = (int)(nrows < want ? nrows : want);
-      if (grid > kMaxGrid) grid = kMaxGrid;
-      if (vec_ok_bf) {
-        hipLaunchKernelGGL((grpo_fwd_stream<uint16_t, 8>), dim3(grid), dim3(256), 0, s, a);
-      } else if (bf16) {
-        hipLaunchKernelGGL((grpo_fwd_stream<uint16_t, 1>), dim3(grid), dim3(256), 0, s, a);
-      } else if (batch->V % 4 == 0 && batch->ld % 4 == 0 && aligned16(batch->logits) &&
-                 (!params->write_grad || aligned16(out->dlogits))) {
-        hipLaunchKernelGGL((grpo_fwd_stream<float, 4>), dim3(grid), dim3(256), 0, s, a);
-      } else {
-        hipLaunchKernelGGL((grpo_fwd_stream<float, 1>), dim3(grid), dim3(256), 0, s, a);
-      }
-      e = hipGetLastError();
-    }
+  e = launch_rows(a, batch, params, out, nrows, s);
+  if (e != hipSuccess) return (int)e;
+  return (int)launch_stats(a, nrows, out->stats, s);
+}
+
+int prl_grpo_forward_rows(const PrlGrpoBatch* batch, const PrlGrpoParams* params, const int64_t* row_ids,
+                          int64_t n, const PrlGrpoOutputs* out, void* stream) {
+  KArgs a;
+  int rc = fill_args(a, batch, params);
+  if (rc) return rc;
+  if (batch->values) return PRL_E_UNSUPPORTED;
+  rc = fill_outputs(a, batch, params, out, false);
+  if (rc) return rc;
+  if (n < 0 || (n > 0 && !row_ids)) return PRL_E_INVALID;
+  if (n == 0) return PRL_OK;
+  a.row_ids = row_ids;
+  a.nsel = n;
+  return (int)launch_rows(a, batch, params, out, n, static_cast<hipStream_t>(stream));
+}
+
+int prl_grpo_stats(const PrlGrpoBatch* batch, const PrlGrpoParams* params, const PrlGrpoOutputs* out,
+                   void* workspace, size_t workspace_bytes, void* stream) {
+  KArgs a;
+  int rc = fill_args(a, batch, params, false);
+  if (rc) return rc;
+  if (!out || !out->new_logprobs || !out->entropy || !out->stats) return PRL_E_INVALID;
+  if (batch->values && !out->dvalues) return PRL_E_INVALID;
+  if (!workspace || workspace_bytes < sizeof(double) * (size_t)kMaxGrid * PRL_NSTAT) return PRL_E_WORKSPACE;
+  a.o_lp = out->new_logprobs;
+  a.o_ent = out->entropy;
+  a.o_dv = out->dvalues;
+  a.partials = static_cast<double*>(workspace);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (batch->values) {
+    hipError_t e = hipMemsetAsync(out->dvalues, 0, sizeof(float) * (size_t)(batch->B * batch->L), s);
     if (e != hipSuccess) return (int)e;
   }
-  // statistics + value gradient: fixed row chunks per block (deterministic)
-  int sblocks = 0;
-  if (nrows > 0) {
-    // ~256 rows per 256-thread block: one row per thread, enough blocks to fill the chip
-    int64_t chunk = (nrows + kMaxGrid - 1) / kMaxGrid;
-    if (chunk < kStatThreads) chunk = kStatThreads;
-    sblocks = (int)((nrows + chunk - 1) / chunk);
-    hipLaunchKernelGGL(grpo_stats_partial, dim3(sblocks), dim3(kStatThreads), 0, s, a, chunk);
-    e = hipGetLastError();
-    if (e != hipSuccess) return (int)e;
-  }
-  hipLaunchKernelGGL(grpo_finalize, dim3(1), dim3(PRL_NSTAT * kFinLanes), 0, s, a.partials, sblocks, out->stats);
-  return (int)hipGetLastError();
+  return (int)launch_stats(a, batch->B * (batch->L - 1), out->stats, s);
 }
 
 int prl_grpo_backward(const PrlGrpoBatch* batch, const PrlGrpoParams* params, const float* row_max,

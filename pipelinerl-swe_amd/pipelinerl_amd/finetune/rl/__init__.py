@@ -26,6 +26,7 @@ from pydantic import BaseModel, Field
 from ..attention import packed_kwargs, uses_varlen
 from ..types import PipelineBatchEncoding
 from .fused import GrpoParams, grpo_loss, prepare_fields
+from .fused_linear import linear_grpo_loss
 from ..._native import S
 
 logger = logging.getLogger(__name__)
@@ -53,6 +54,10 @@ class RLConfig(BaseModel):
     temperature: float = Field(default=1.0)
     filter_zero_advantage_groups: bool = Field(default=False)
     value_loss_coef: float = Field(default=0.0)
+    # build-only keys (absent from the reference; ignored there):
+    # lm_head + loss over the label rows only, in row chunks (fused_linear.py)
+    fused_lm_head: bool = Field(default=False)
+    lm_head_chunk_rows: int = Field(default=16384)
 
 
 def linear_decay_coef(current_step: int, max_step: int, initial_coef: float, final_coef: float) -> float:
@@ -91,9 +96,15 @@ def rl_step(model, batch: PipelineBatchEncoding, current_step: int, max_step: in
         model_inputs["pixel_values"] = batch.pixel_values
     if getattr(batch, "image_grid_thw", None) is not None:
         model_inputs["image_grid_thw"] = batch.image_grid_thw
-    outputs = model(**model_inputs)
-    logits = outputs.logits
-    values = outputs.value if has_value_head else None
+    fused_head = config.fused_lm_head and _lm_head_of(model, has_value_head) is not None
+    if fused_head:
+        hidden = _decoder_of(model)(**model_inputs).last_hidden_state
+        logits = hidden
+        values = None
+    else:
+        outputs = model(**model_inputs)
+        logits = outputs.logits
+        values = outputs.value if has_value_head else None
 
     ent_c = linear_decay_coef(current_step, max_step, config.entropy_bonus, config.final_entropy_bonus)
     kl_c = linear_decay_coef(current_step, max_step, config.kl_coef, config.final_kl_coef)
@@ -104,7 +115,11 @@ def rl_step(model, batch: PipelineBatchEncoding, current_step: int, max_step: in
         clamp_log_ratio=float(config.clamp_log_ratio_ref_new_value), temperature=config.temperature,
         batch_size=float(config.batch_size), value_loss_coef=config.value_loss_coef if has_value_head else 0.0)
     fields = prepare_fields(batch, logits.device)
-    loss, stats_dev, _ = grpo_loss(logits, fields, params, values)
+    if fused_head:
+        loss, stats_dev, _ = linear_grpo_loss(hidden, _lm_head_of(model, False).weight, fields, params,
+                                              config.lm_head_chunk_rows)
+    else:
+        loss, stats_dev, _ = grpo_loss(logits, fields, params, values)
 
     nseq = _num_sequences_device(batch)
     if isinstance(nseq, torch.Tensor):
@@ -114,6 +129,28 @@ def rl_step(model, batch: PipelineBatchEncoding, current_step: int, max_step: in
         host = stats_dev.cpu().numpy()
         num_sequences = nseq
     return loss, build_stats(host, batch, params, kl_c, ent_c, num_sequences, has_value_head)
+
+
+def _decoder_of(model):
+    dec = model.get_decoder() if hasattr(model, "get_decoder") else getattr(model, "model", None)
+    if dec is None:
+        raise ValueError("fused_lm_head needs a causal LM with a decoder (model.get_decoder())")
+    return dec
+
+
+def _lm_head_of(model, has_value_head: bool):
+    """The plain bias-free lm_head Linear, or None (with a one-time warning) when the model
+    does something else between the decoder and the logits."""
+    head = model.get_output_embeddings() if hasattr(model, "get_output_embeddings") else None
+    ok = (isinstance(head, torch.nn.Linear) and head.bias is None and not has_value_head
+          and getattr(getattr(model, "config", None), "final_logit_softcapping", None) is None)
+    if not ok:
+        if not _warned.get("fused_lm_head"):
+            _warned["fused_lm_head"] = True
+            logger.warning("fused_lm_head: model has no plain bias-free lm_head (or has a value head); "
+                           "using the full-logits loss head")
+        return None
+    return head
 
 
 def build_stats(h: np.ndarray, batch, params: GrpoParams, kl_c: float, ent_c: float, num_sequences: int,

@@ -1,0 +1,134 @@
+"""Label-row lm_head + GRPO loss head, chunked.
+
+The reference materialises logits for every packed position (``model(...)`` then
+``logits[:, :-1]``, rl/__init__.py:197-208) and back-propagates a full [T, V] dlogits
+through ``lm_head``.  Prompt rows (``labels[:, 1:] == -100``, :152-153) never carry a gradient
+and only enter the statistics through finiteness checks.  This function instead takes the
+final hidden states and the ``lm_head`` weight and, for the label rows only, in chunks of
+``chunk_rows``:
+
+  logits_c  = h_c @ W^T                      (hipBLASLt GEMM, [c, V])
+  prl_grpo_forward_rows(logits_c)            (HIP loss kernel; dlogits written in place)
+  dh_c      = dlogits_c @ W                  (GEMM)
+  dW       += dlogits_c^T @ h_c              (GEMM, fp32 accumulator)
+
+then one ``prl_grpo_stats`` pass over all rows.  Peak extra memory is one [c, V] chunk plus an
+fp32 [V, H] accumulator instead of two [T, V] tensors, and the three lm_head GEMMs and the
+loss kernel skip the prompt rows.  The backward scales the saved dh / dW by the upstream
+gradient on device.
+
+Semantics vs the reference: identical loss, statistics and gradients when the prompt rows'
+logits are finite.  Non-finite logits on a prompt row are not seen (the reference's finiteness
+assertion at :209 covers every row).  Opt-in: ``RLConfig.fused_lm_head``.
+"""
+
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from ... import _native
+from ..._native import NSTAT, PRL_BF16, PRL_F32
+from .fused import GrpoParams, _workspace
+
+_ADDMM_F32: dict[str, bool] = {}
+
+
+def _accumulate_dw(dw: torch.Tensor, dlg: torch.Tensor, hc: torch.Tensor) -> None:
+    """dw (fp32) += dlg^T @ hc with the bf16 GEMM accumulating into fp32 (addmm out_dtype)."""
+    key = str(dw.device)
+    if _ADDMM_F32.get(key, True) and dlg.dtype != torch.float32:
+        try:
+            torch.addmm(dw, dlg.t(), hc, torch.float32, out=dw)
+            _ADDMM_F32[key] = True
+            return
+        except (RuntimeError, NotImplementedError):
+            _ADDMM_F32[key] = False  # this build's BLAS has no bf16 -> fp32 path
+    dw.add_(torch.mm(dlg.t(), hc).float())
+
+
+def _c_batch(ptr: int, dtype: torch.dtype, B: int, L: int, V: int, ld: int, f: dict) -> _native.PrlGrpoBatch:
+    return _native.PrlGrpoBatch(
+        ptr, PRL_BF16 if dtype == torch.bfloat16 else PRL_F32, 0, B, L, V, ld,
+        f["input_ids"].data_ptr(), f["labels"].data_ptr(), f["rewards"].data_ptr(), f["advantages"].data_ptr(),
+        f["ref_logprobs"].data_ptr(), f["old_logprobs"].data_ptr(), f["group_tokens"].data_ptr(),
+        f["num_labels"].data_ptr(), f["overflow"].data_ptr(), None)
+
+
+class LinearGrpoLossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, hidden, weight, fields, params: GrpoParams, chunk_rows: int):
+        if hidden.device.type != "cuda":
+            raise RuntimeError("the fused lm_head + GRPO loss runs on a HIP device only (no CPU fallback)")
+        if hidden.dim() != 3 or weight.dim() != 2 or hidden.shape[-1] != weight.shape[1]:
+            raise ValueError(f"hidden [B, L, H] / weight [V, H] expected, got {tuple(hidden.shape)} / "
+                             f"{tuple(weight.shape)}")
+        lib = _native.load()
+        B, L, Hd = hidden.shape
+        V = weight.shape[0]
+        dev = hidden.device
+        Q = B * (L - 1)
+        w = weight.detach()
+        h2 = hidden.detach().reshape(B * L, Hd)
+        if w.dtype != h2.dtype:
+            h2 = h2.to(w.dtype)
+        write_grad = bool(hidden.requires_grad or weight.requires_grad)
+        # lp, H, lse, tok_loss, g_lp, g_h, row max, row log2-sum; unscored rows stay 0
+        rows = torch.zeros((8, max(Q, 1)), dtype=torch.float32, device=dev)
+        stats = torch.empty(NSTAT, dtype=torch.float64, device=dev)
+        dh = torch.zeros((B * L, Hd), dtype=h2.dtype, device=dev) if write_grad else None
+        dw = torch.zeros((V, Hd), dtype=torch.float32, device=dev) if write_grad else None
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        cp = params.to_c(write_grad)
+        if Q > 0:
+            mask = (fields["labels"][:, 1:] != -100).reshape(-1)
+            qsel = torch.nonzero(mask).reshape(-1)  # one host sync: the GEMM shapes need the count
+            hrow = qsel + torch.div(qsel, L - 1, rounding_mode="floor")  # q = b*(L-1)+t -> b*L+t
+            R = int(qsel.numel())
+            step = max(1, int(chunk_rows))
+            for a in range(0, R, step):
+                idx = hrow[a:a + step]
+                qc = qsel[a:a + step].contiguous()
+                hc = h2.index_select(0, idx)
+                lg = torch.mm(hc, w.t())  # [c, V] contiguous
+                cb = _c_batch(lg.data_ptr(), lg.dtype, B, L, V, V, fields)
+                co = _native.PrlGrpoOutputs(*[rows[i].data_ptr() for i in range(8)], None,
+                                            lg.data_ptr() if write_grad else None, None)
+                _native.check(lib.prl_grpo_forward_rows(ctypes.byref(cb), ctypes.byref(cp), qc.data_ptr(),
+                                                        qc.numel(), ctypes.byref(co), stream),
+                              "prl_grpo_forward_rows")
+                if write_grad:
+                    dh.index_copy_(0, idx, torch.mm(lg, w))
+                    _accumulate_dw(dw, lg, hc)
+                del lg, hc
+        cb = _c_batch(0, w.dtype, B, L, V, V, fields)
+        co = _native.PrlGrpoOutputs(*[rows[i].data_ptr() for i in range(8)], None, None, stats.data_ptr())
+        ws = _workspace(dev)
+        _native.check(lib.prl_grpo_stats(ctypes.byref(cb), ctypes.byref(cp), ctypes.byref(co), ws.data_ptr(),
+                                         ws.numel(), stream), "prl_grpo_stats")
+        loss = (-stats[0]).to(torch.float32)
+        ctx.mark_non_differentiable(stats, rows)
+        ctx.dh, ctx.dw = dh, dw
+        ctx.shape = (B, L, Hd)
+        ctx.h_dtype, ctx.w_dtype = hidden.dtype, weight.dtype
+        return loss, stats, rows
+
+    @staticmethod
+    def backward(ctx, g_loss, g_stats, g_rows):
+        d_hidden = d_weight = None
+        if g_loss is not None and ctx.dh is not None:
+            g = g_loss.detach().to(torch.float32)
+            if ctx.needs_input_grad[0]:
+                d_hidden = (ctx.dh.view(ctx.shape) * g.to(ctx.dh.dtype)).to(ctx.h_dtype)
+            if ctx.needs_input_grad[1]:
+                d_weight = (ctx.dw * g).to(ctx.w_dtype)
+        ctx.dh = ctx.dw = None
+        return d_hidden, d_weight, None, None, None
+
+
+def linear_grpo_loss(hidden: torch.Tensor, weight: torch.Tensor, fields: dict, params: GrpoParams,
+                     chunk_rows: int = 16384):
+    """(loss, stats [NSTAT] f64 device, rows [8, B*(L-1)]) of lm_head(hidden) -> GRPO loss head,
+    scoring only the label rows.  ``weight``: the lm_head weight [V, H] (no bias)."""
+    return LinearGrpoLossFn.apply(hidden, weight, fields, params, chunk_rows)

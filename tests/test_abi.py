@@ -15,7 +15,7 @@ def test_library_exports_header_symbols():
     assert len(declared) >= 9
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.prl_abi_version() == 1
+    assert lib.prl_abi_version() == _native.ABI_VERSION == 2
     assert lib.prl_grpo_nstat() == _native.NSTAT
     assert lib.prl_error_string(1001).decode() == "invalid argument"
     nbytes = ctypes.c_size_t(0)

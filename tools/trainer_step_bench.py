@@ -3,7 +3,9 @@
   --mode loss     fused HIP loss head vs the reference's ATen op chain (tools/aten_rl_step.py)
                   on the same bf16 logits, fwd+bwd per packed micro-batch
   --mode trainer  full trainer micro-batch step on a Qwen2.5-shaped model (random init, bf16,
-                  prl_varlen attention): forward, loss head (fused or ATen), backward, fused AdamW
+                  prl_varlen attention): forward, loss head, backward, clip, fused AdamW.  Loss heads:
+                  fused (HIP kernel on full logits), fused_head (label-row chunked lm_head + HIP
+                  kernel, RLConfig.fused_lm_head), aten (the reference's op chain)
 Prints one JSON line per measured configuration.
 """
 
@@ -65,11 +67,11 @@ def timed(fn, steps, warmup):
     return (time.perf_counter() - t0) / steps
 
 
-def rl_cfg():
+def rl_cfg(fused_head: bool = False, chunk: int = 16384):
     from pipelinerl_amd.finetune.rl import RLConfig
 
     return RLConfig(policy_loss="ppo", epsilon=4.0, kl_coef=0.0, final_kl_coef=0.0, clamp_log_ratio_ref_new_value=5,
-                    batch_size=4096)
+                    batch_size=4096, fused_lm_head=fused_head, lm_head_chunk_rows=chunk)
 
 
 def mode_loss(a):
@@ -120,11 +122,12 @@ def mode_trainer(a):
     model.train()
     opt = get_optimizer("adamw_torch", model, 1e-6, 0.01)
     batch = packed_batch(a.tokens, a.seq, a.prompt, shapes["vocab_size"], "cuda")
-    cfg = rl_cfg()
     out = {}
     for name in a.loss.split(","):
+        cfg = rl_cfg(name == "fused_head", a.chunk)
+
         def step():
-            if name == "fused":
+            if name in ("fused", "fused_head"):
                 loss, _ = rl_step(model, batch, 0, 100, cfg)
             else:
                 o = model(input_ids=batch.input_ids, position_ids=batch.position_ids,
@@ -160,5 +163,6 @@ if __name__ == "__main__":
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--loss", default="fused,aten")
     ap.add_argument("--grad-ckpt", action="store_true")
+    ap.add_argument("--chunk", type=int, default=16384, help="lm_head_chunk_rows for --loss fused_head")
     a = ap.parse_args()
     mode_loss(a) if a.mode == "loss" else mode_trainer(a)
