@@ -38,4 +38,18 @@ if __name__ == "__main__" and torch.cuda.is_available():
     for variant, name in [(0, "u4_plain"), (1, "u4_nt"), (2, "u8_nt")]:
         for grid in (1024, 2048, 4096, 8192):
             res[f"hip_{name}_g{grid}"] = timeit(lambda: lib.probe_copy(a.data_ptr(), b.data_ptr(), nbytes, grid, variant, st))
-    print(json.dumps({"bytes_read": nbytes, "bytes_written": nbytes, "GBps_ms": res}))
+    print(json.dumps({"bytes_read": nbytes, "bytes_written": nbytes, "GBps_ms": res}), flush=True)
+    if "--sweep" in sys.argv:
+        # size sweep (bytes per direction) of the best copy forms, plus one-direction streams.
+        # GB/s counts read + write bytes for copies, one direction for read-only / write-only.
+        sweep = {}
+        for sz in (512 << 20, 2 << 30, 8 << 30, nbytes):
+            for variant, name, grid in [(2, "u8_nt", 8192), (1, "u4_nt", 1024), (1, "u4_nt", 4096)]:
+                gbps, ms = timeit(lambda: lib.probe_copy(a.data_ptr(), b.data_ptr(), sz, grid, variant, st))
+                sweep[f"copy_{name}_g{grid}_{sz >> 20}MiB"] = [round(gbps * sz / nbytes, 1), ms]
+            for grid in (1024, 4096, 8192):
+                gbps, ms = timeit(lambda: lib.probe_copy(a.data_ptr(), b.data_ptr(), sz, grid, 3, st))
+                sweep[f"read_g{grid}_{sz >> 20}MiB"] = [round(gbps * sz / nbytes / 2, 1), ms]
+                gbps, ms = timeit(lambda: lib.probe_copy(a.data_ptr(), b.data_ptr(), sz, grid, 4, st))
+                sweep[f"write_g{grid}_{sz >> 20}MiB"] = [round(gbps * sz / nbytes / 2, 1), ms]
+        print(json.dumps({"sweep_GBps_ms": sweep}), flush=True)
