@@ -11,6 +11,11 @@ all-reduce of one int64 over RCCL).
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...     (one rank per GPU)
 
+At N > 1, after the timed region, the trainer's exchange steps are measured on the real code
+paths over the C2 model's parameter set (pipelinerl_amd/comm_probe.py) and reported under
+"exchange": the bucketed DP gradient all-reduce (GradBuckets, RCCL) and the trainer -> actors
+weight broadcast (WeightUpdateManager -> WorkerExtension, rank 0 -> ranks 1..N-1).
+
 Prints ONE JSON line (rank 0).  roofline.achieved = algorithmic bytes per launch
 (T*V*2 read + T*V*2 dlogits write + 37*T side data) / the average duration
 of the prl_grpo_forward launch measured with HIP events on its stream.
@@ -102,6 +107,7 @@ def main():
     ap.add_argument("--vocab", type=int, default=151936)
     ap.add_argument("--cpu-rows", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-comm-probe", action="store_true", help="N > 1: skip the all-reduce / broadcast probes")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -162,6 +168,18 @@ def main():
         dist.all_reduce(k_max, op=dist.ReduceOp.MAX)
     elapsed = float(t_max)
     kern_ms = float(k_max)
+    comm = None
+    if world > 1 and not args.no_comm_probe:
+        # the trainer's two exchange steps on the C2 model's parameter set, measured after the
+        # timed region (not part of `value`): DP gradient all-reduce, trainer -> actors broadcast
+        from pipelinerl_amd import comm_probe
+
+        del logits, fields
+        torch.cuda.empty_cache()
+        shapes = comm_probe.qwen2_param_shapes("1.5b")
+        comm = {"model": "Qwen2.5-1.5B parameter shapes, bf16",
+                "grad_allreduce": comm_probe.grad_allreduce_probe(shapes, dev, iters=5),
+                "weight_broadcast": comm_probe.broadcast_probe(shapes, dev, iters=3)}
 
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
@@ -196,6 +214,8 @@ def main():
                          "traffic_source": tsrc},
             "cpu_baseline": cpu,
         }
+        if comm is not None:
+            out["exchange"] = comm
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
