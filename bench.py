@@ -67,7 +67,7 @@ def make_workload(T: int, V: int, seq: int, prompt: int, seed: int, device):
     return logits.requires_grad_(True), {k: v.contiguous() for k, v in fields.items()}
 
 
-def cpu_baseline(rows: int, V: int, threads: int) -> dict:
+def cpu_baseline(rows: int, V: int, threads: int, min_seconds: float = 10.0, max_reps: int = 16) -> dict:
     """Oracle (numpy restatement of rl_step's loss head incl. gradient) on a bounded sample."""
     from oracle import grpo_oracle, synth
 
@@ -79,11 +79,15 @@ def cpu_baseline(rows: int, V: int, threads: int) -> dict:
     b["ref_logprobs"] = b["old_logprobs"].copy()
     cfg = dict(policy_loss="ppo", epsilon=4.0, kl_coef=0.0, final_kl_coef=0.0, batch_size=256,
                clamp_log_ratio_ref_new_value=5)
-    t0 = time.perf_counter()
-    grpo_oracle.rl_step_oracle(lg, b, cfg, 0, 10, dtype=np.float32, threads=threads, row_chunk=16)
+    # repeat the sample until ~min_seconds of CPU work (bounded: the bench stays within minutes)
+    reps, t0 = 0, time.perf_counter()
+    while reps < max_reps and (reps == 0 or time.perf_counter() - t0 < min_seconds):
+        grpo_oracle.rl_step_oracle(lg, b, cfg, 0, 10, dtype=np.float32, threads=threads, row_chunk=16)
+        reps += 1
     dt = time.perf_counter() - t0
-    return {"value": round(rows / dt, 1), "unit": "tokens/s", "cores": threads, "kind": "port",
-            "sample": f"{rows} packed rows x V={V}, fwd+grad, numpy float32 oracle, {threads} threads, {dt:.2f} s"}
+    return {"value": round(rows * reps / dt, 1), "unit": "tokens/s", "cores": threads, "kind": "port",
+            "sample": f"{reps} x {rows} packed rows x V={V}, fwd+grad, numpy float32 oracle, {threads} threads, "
+                      f"{dt:.2f} s"}
 
 
 def load_traffic(T: int, V: int) -> tuple[float | None, str | None]:
