@@ -98,28 +98,50 @@ def temporary_folder_and_move(output_dir: Path, group=None):
 
 
 def save_model_and_tokenizer(output_dir: Path, model, tokenizer, safe_serialization: bool = True, group=None):
+    from .sharding import full_state_dict, is_sharded
+
+    sd = full_state_dict(model) if is_sharded(model) else None  # collective: every rank
     with temporary_folder_and_move(output_dir, group) as tmp:
         if _rank() == 0:
             m = getattr(model, "module", model)
-            m.save_pretrained(tmp, safe_serialization=safe_serialization)
+            if sd is not None:
+                if getattr(getattr(m, "config", None), "tie_word_embeddings", False):
+                    sd.pop("lm_head.weight", None)  # tied copy (finetune_loop.py:228-231)
+                m.save_pretrained(tmp, state_dict=sd, safe_serialization=safe_serialization)
+            else:
+                m.save_pretrained(tmp, safe_serialization=safe_serialization)
             if hasattr(tokenizer, "save_pretrained"):
                 tokenizer.save_pretrained(tmp)
 
 
 def save_training_state(training_state_dir: Path, model, optimizer, lr_scheduler, extra: dict[str, Any],
                         group=None):
+    """training_state.pt (metrics, lr scheduler, optimizer); with FSDP the sharded optimizer
+    state goes to ``optim/`` (torch.distributed.checkpoint, every rank writes its shard)."""
+    from .sharding import is_sharded, save_optimizer
+
+    sharded = is_sharded(model)
     with temporary_folder_and_move(training_state_dir, group) as tmp:
+        if sharded:
+            save_optimizer(tmp / "optim", model, optimizer)
         if _rank() == 0:
             state = dict(extra)
-            state["optimizer_state"] = optimizer.state_dict()
+            if not sharded:
+                state["optimizer_state"] = optimizer.state_dict()
             state["lr_scheduler_state"] = lr_scheduler.state_dict()
             torch.save(state, tmp / "training_state.pt")
 
 
 def load_training_state(training_state_dir: Path, model, optimizer, lr_scheduler, metrics):
     """Restores optimizer / scheduler (in place) and returns metrics updated from the file."""
+    from .sharding import is_sharded, load_optimizer
+
     state = torch.load(Path(training_state_dir) / "training_state.pt", map_location="cpu", weights_only=True)
-    optimizer.load_state_dict(state.pop("optimizer_state"))
+    if is_sharded(model):
+        load_optimizer(Path(training_state_dir) / "optim", model, optimizer)
+        state.pop("optimizer_state", None)
+    else:
+        optimizer.load_state_dict(state.pop("optimizer_state"))
     lr_scheduler.load_state_dict(state.pop("lr_scheduler_state"))
     for k, v in state.items():
         if hasattr(metrics, k):

@@ -142,13 +142,16 @@ def _lm_head_of(model, has_value_head: bool):
     """The plain bias-free lm_head Linear, or None (with a one-time warning) when the model
     does something else between the decoder and the logits."""
     head = model.get_output_embeddings() if hasattr(model, "get_output_embeddings") else None
+    from ..sharding import is_sharded
+
     ok = (isinstance(head, torch.nn.Linear) and head.bias is None and not has_value_head
-          and getattr(getattr(model, "config", None), "final_logit_softcapping", None) is None)
+          and getattr(getattr(model, "config", None), "final_logit_softcapping", None) is None
+          and not is_sharded(model))  # FSDP: the root's hooks gather lm_head / embeddings
     if not ok:
         if not _warned.get("fused_lm_head"):
             _warned["fused_lm_head"] = True
-            logger.warning("fused_lm_head: model has no plain bias-free lm_head (or has a value head); "
-                           "using the full-logits loss head")
+            logger.warning("fused_lm_head: model has no plain bias-free lm_head (or has a value head, or "
+                           "is FSDP-sharded); using the full-logits loss head")
         return None
     return head
 

@@ -1,0 +1,121 @@
+"""Fully sharded data-parallel trainer (the reference's FSDP path for 32B, config C5).
+
+The reference gets FSDP from Accelerate's plugin (``use_fsdp``: conf/accelerate/fsdp_mp.yaml —
+FULL_SHARD, transformer-layer wrap, ``fsdp.{param,reduce,buffer}_dtype`` mixed precision,
+finetune_loop.py:369-391) and gathers a FULL_STATE_DICT on rank 0 before each weight broadcast
+(finetune_loop.py:222-247).  Here: FSDP2 ``fully_shard`` per decoder layer + the root (so the
+tied embedding / lm_head and the final norm live in the root group), RCCL reduce-scatter /
+all-gather on MI355X; the lockstep / sentinel protocol already guarantees every rank runs the
+same number of forward/backward passes, which FSDP's collectives require.
+
+  * gradient accumulation: ``set_requires_gradient_sync`` — the reduce-scatter runs on the
+    boundary micro-batch only (the reference's ``no_sync``), unless
+    ``fsdp_sync_every_micro_batch`` trades bandwidth for the unsharded gradient memory;
+  * ``grad_reduce: sum`` sets the divide factor to 1 (sum instead of mean), as GradBuckets does;
+  * weight snapshot for the actors: parameters are gathered bucket by bucket (every rank takes
+    part in each all-gather), rank 0 packs them into its bf16 staging buffer (weight_update.py);
+  * checkpoints: full HF weights on rank 0 (``current/``) and the sharded optimizer state with
+    torch.distributed.checkpoint (``training_state/optim/``).
+"""
+
+from __future__ import annotations
+
+import logging
+from typing import Iterator
+
+import torch
+import torch.distributed as dist
+
+logger = logging.getLogger(__name__)
+
+_DTYPES = {"bf16": torch.bfloat16, "fp32": torch.float32, "fp16": torch.float16}
+
+
+def fsdp_requested(cfg, args) -> bool:
+    return bool(cfg.get("use_fsdp", False)) or str(args.get("sharding", "none")) == "fsdp"
+
+
+def is_sharded(model) -> bool:
+    from torch.distributed.fsdp import FSDPModule
+
+    return isinstance(model, FSDPModule)
+
+
+def decoder_layers(model) -> list[torch.nn.Module]:
+    """The transformer blocks (TRANSFORMER_BASED_WRAP): modules named ``*DecoderLayer``."""
+    return [m for m in model.modules() if type(m).__name__.endswith("DecoderLayer")]
+
+
+def shard_model(model, fsdp_cfg=None, grad_reduce: str = "mean", reshard_after_forward: bool = True):
+    """Shard ``model`` in place over the default process group; returns it (an FSDPModule)."""
+    from torch.distributed.device_mesh import init_device_mesh
+    from torch.distributed.fsdp import MixedPrecisionPolicy, fully_shard
+
+    dev = next(model.parameters()).device
+    mesh = init_device_mesh(dev.type, (dist.get_world_size(),))
+    fsdp_cfg = fsdp_cfg or {}
+    store = next(model.parameters()).dtype
+    pd = _DTYPES.get(str(fsdp_cfg.get("param_dtype", "")), None)
+    rd = _DTYPES.get(str(fsdp_cfg.get("reduce_dtype", "")), None)
+    mp = MixedPrecisionPolicy(param_dtype=pd if pd not in (None, store) else None,
+                              reduce_dtype=rd if rd not in (None, store) else None)
+    layers = decoder_layers(model)
+    for layer in layers:
+        fully_shard(layer, mesh=mesh, mp_policy=mp, reshard_after_forward=reshard_after_forward)
+    fully_shard(model, mesh=mesh, mp_policy=mp, reshard_after_forward=reshard_after_forward)
+    for m in [*layers, model]:
+        if grad_reduce == "sum":
+            m.set_gradient_divide_factor(1.0)
+        if dist.get_backend() == "gloo":  # gloo has no PREMUL_SUM / AVG: plain SUM + a scale
+            m.set_force_sum_reduction_for_comms(True)
+    logger.info(f"FSDP: {len(layers)} decoder layers + root sharded over {dist.get_world_size()} ranks "
+                f"(param_dtype {mp.param_dtype}, reduce_dtype {mp.reduce_dtype})")
+    return model
+
+
+def set_gradient_sync(model, enabled: bool) -> None:
+    if is_sharded(model):
+        model.set_requires_gradient_sync(enabled)
+
+
+def gather_buckets(named: list[tuple[str, torch.Tensor]], bucket_bytes: int
+                   ) -> Iterator[list[tuple[int, torch.Tensor]]]:
+    """Yield [(index, full tensor)] buckets of the (possibly DTensor-sharded) parameters; every
+    rank must iterate it (each full_tensor() is an all-gather)."""
+    from torch.distributed.tensor import DTensor
+
+    cur: list[tuple[int, torch.Tensor]] = []
+    size = 0
+    for i, (_, p) in enumerate(named):
+        t = p.detach()
+        full = t.full_tensor() if isinstance(t, DTensor) else t
+        cur.append((i, full.contiguous()))
+        size += full.numel() * full.element_size()
+        if size >= bucket_bytes:
+            yield cur
+            cur, size = [], 0
+    if cur:
+        yield cur
+
+
+def full_state_dict(model) -> dict:
+    """Full (unsharded) CPU state dict on rank 0 (empty elsewhere); collective."""
+    from torch.distributed.checkpoint.state_dict import StateDictOptions, get_model_state_dict
+
+    return get_model_state_dict(model, options=StateDictOptions(full_state_dict=True, cpu_offload=True))
+
+
+def save_optimizer(path, model, optimizer) -> None:
+    import torch.distributed.checkpoint as dcp
+    from torch.distributed.checkpoint.state_dict import get_optimizer_state_dict
+
+    dcp.save({"optim": get_optimizer_state_dict(model, optimizer)}, checkpoint_id=str(path))
+
+
+def load_optimizer(path, model, optimizer) -> None:
+    import torch.distributed.checkpoint as dcp
+    from torch.distributed.checkpoint.state_dict import get_optimizer_state_dict, set_optimizer_state_dict
+
+    state = {"optim": get_optimizer_state_dict(model, optimizer)}
+    dcp.load(state, checkpoint_id=str(path))
+    set_optimizer_state_dict(model, optimizer, state["optim"])

@@ -16,7 +16,8 @@ rl_summary.json, the stats/throughput/rl metric keys), same protocol:
 MI355X-first differences: the loss head is the fused HIP kernel (rl_step); the per-pass
 count exchange runs on a CPU (gloo) control group, so the host never drains the GPU queue for
 it; gradients are reduced in 256 MiB flat buckets overlapped with the boundary backward
-(grad_sync.py); the weight broadcast is snapshotted by a HIP kernel and overlapped with the
+(grad_sync.py), or sharded with FSDP2 (``use_fsdp`` / ``finetune.sharding: fsdp``,
+finetune/sharding.py); the weight broadcast is snapshotted by a HIP kernel and overlapped with the
 next step on a side stream (weight_update.py); no per-pass empty_cache; no HF-internal CE pass.
 """
 
@@ -44,6 +45,7 @@ from .finetune.grad_sync import GradBuckets
 from .finetune.optim import get_optimizer
 from .finetune.rl import RLConfig, rl_step
 from .finetune.rl.utils import aggregate_rl_stats
+from .finetune.sharding import fsdp_requested, set_gradient_sync, shard_model
 from .finetune.types import PipelineBatchEncoding, TrainingMetrics
 from .streams import SingleStreamSpec, read_stream, set_streams_backend, write_to_streams
 from .weight_update import (TRAINER_TOPIC, ParameterInfo, SamplesProcessed, WeightUpdateManager,  # noqa: F401
@@ -189,13 +191,16 @@ def run_finetuning_loop(cfg, step_fn: Callable = rl_step, model=None, tokenizer=
         model = load_model(args, args.model_class, current_dir, ctx.device)
     if tokenizer is None:
         tokenizer = load_tokenizer(args.config_name, getattr(getattr(model, "config", None), "eos_token_id", None))
+    sharded = fsdp_requested(cfg, args) and ctx.initialized
+    if sharded:  # before the optimizer: it must see the sharded parameters
+        model = shard_model(model, cfg.get("fsdp"), grad_reduce=args.get("grad_reduce", "mean"))
     data_stream = SingleStreamSpec(exp_path=exp_root, topic=args.input, instance=0, partition=ctx.rank)
     optimizer = get_optimizer(args.optim, model, args.learning_rate, args.weight_decay)
     from transformers import get_scheduler
 
     lr_scheduler = get_scheduler(args.lr_scheduler_type, optimizer, args.num_warmup_steps, args.max_train_steps)
     grads = None
-    if ctx.initialized and ctx.world > 1:
+    if ctx.initialized and ctx.world > 1 and not sharded:
         grads = GradBuckets(list(model.parameters()), bucket_bytes=int(args.get("grad_bucket_mb", 256)) << 20,
                             reduce=args.get("grad_reduce", "mean"))
 
@@ -273,6 +278,7 @@ def rl_finetuning_worker(args, ctx: Dist, model, optimizer, lr_scheduler, grads:
     passes_took: list[float] = []
     mb_sizes: list[int] = []
     waiting = 0.0
+    sync_every = bool(args.get("fsdp_sync_every_micro_batch", False))
 
     def next_batch():
         timeout = 0.1
@@ -314,6 +320,7 @@ def rl_finetuning_worker(args, ctx: Dist, model, optimizer, lr_scheduler, grads:
 
         if do_step and grads is not None:
             grads.arm()
+        set_gradient_sync(model, do_step or sync_every)  # FSDP: reduce-scatter on the boundary only
         loss, stats = step_fn(model, batch, metrics.completed_steps, final_steps, rl_config)
         if sentinel:
             loss = loss * 0.0

@@ -199,19 +199,33 @@ class WeightUpdateManager:
     # -- protocol ------------------------------------------------------------------------
     def send_weight_update(self, version: int) -> None:
         self.wait()
-        if not self.is_main:
-            return
         named = self.named_parameters()
+        sharded = _is_sharded(named)
+        if not self.is_main and not sharded:
+            return
         infos = [ParameterInfo(name=n, shape=list(p.shape), dtype=str(torch.bfloat16)) for n, p in named]
+        layout = FlatLayout.from_infos(infos)
+        dev = named[0][1].device
+        if sharded:
+            # FSDP (finetune_loop.py:222-247 gathers a FULL_STATE_DICT): every rank takes part in
+            # the bucketed all-gathers, rank 0 packs each bucket into its staging buffer in
+            # stream order, so the snapshot precedes the next optimizer step without an event.
+            from .finetune.sharding import gather_buckets
+
+            flat = self._ensure_staging(layout.total, dev) if self.is_main else None
+            for bucket in gather_buckets(named, self.bucket_bytes):
+                if self.is_main:
+                    self.packer.flatten([t for _, t in bucket], [layout.offsets[i] for i, _ in bucket], flat)
+            if not self.is_main:
+                return
         request = WeightUpdateRequest(version=version, parameters_info=infos, transport=self.transport,
                                       bucket_bytes=self.bucket_bytes if self.transport == "bucketed" else 0)
-        layout = FlatLayout.from_infos(infos)
         t0 = time.time()
         futures = [self.pool.submit(self.post, url, request) for url in self.llm_urls]
         logger.info(f"Published weight update request for version {version}")
         params = [p.detach() for _, p in named]
-        dev = params[0].device
-        flat = self._ensure_staging(layout.total, dev)
+        if not sharded:
+            flat = self._ensure_staging(layout.total, dev)
         on_gpu = dev.type == "cuda"
         if on_gpu:
             if self._stream is None:
@@ -225,7 +239,8 @@ class WeightUpdateManager:
         with ctx:
             if on_gpu:
                 self._stream.wait_event(ready)  # snapshot after the optimizer step
-            self.packer.flatten(params, layout.offsets, flat)
+            if not sharded:
+                self.packer.flatten(params, layout.offsets, flat)
             if on_gpu:
                 self._snapshot_done = torch.cuda.Event()
                 self._snapshot_done.record(self._stream)
@@ -289,6 +304,12 @@ class WeightUpdateManager:
     def close(self) -> None:
         self.wait()
         self.pool.shutdown(wait=True)
+
+
+def _is_sharded(named) -> bool:
+    from torch.distributed.tensor import DTensor
+
+    return any(isinstance(p, DTensor) for _, p in named)
 
 
 class _nullcontext:

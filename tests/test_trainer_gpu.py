@@ -77,3 +77,43 @@ def test_varlen_attention_gpu(tmp_path):
     from test_attention_cpu import check
 
     check(tmp_path, "cuda")
+
+
+def _fsdp_rank(rank, port, exp):
+    sys.path[:0] = [str(ROOT), str(ROOT / "tests"), str(ROOT / "pipelinerl-swe_amd")]
+    os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from loop_helpers import loop_cfg
+    from pipelinerl_amd.finetune_loop import run_finetuning_loop
+    from pipelinerl_amd.streams import reset_streams_backend
+
+    reset_streams_backend()
+    exp = Path(exp)
+    cfg = loop_cfg(exp, exp / "tiny_qwen2", 1, 8, 2, load_as_bf16=True, dist_backend=None, sharding="fsdp",
+                   grad_reduce="mean")
+    m = run_finetuning_loop(cfg)
+    (exp / "fsdp_metrics.json").write_text(json.dumps({"steps": m.completed_steps, "samples": m.samples,
+                                                       "backend": dist.get_backend()}))
+    dist.destroy_process_group()
+
+
+def test_trainer_loop_one_gpu_fsdp(tmp_path):
+    """The FSDP2 path on the GPU (RCCL process group of one rank, HIP loss head): two steps,
+    full-weight checkpoint and sharded optimizer state."""
+    import torch.multiprocessing as mp
+    from loop_helpers import rollouts, tiny_model_dir, write_training_data
+    from pipelinerl_amd.streams import reset_streams_backend, set_streams_backend
+    from test_weight_update_cpu import free_port
+
+    reset_streams_backend()
+    set_streams_backend("files")
+    tiny_model_dir(tmp_path)
+    write_training_data(tmp_path, rollouts(4, 4), 1, 28, 8)
+    reset_streams_backend()
+    mp.spawn(_fsdp_rank, args=(free_port(), str(tmp_path)), nprocs=1, join=True)
+    m = json.loads((tmp_path / "fsdp_metrics.json").read_text())
+    assert m == {"steps": 2, "samples": 16, "backend": "nccl"}
+    lines = [json.loads(x) for x in (tmp_path / "finetune" / "logs" / "metrics.jsonl").read_text().splitlines()]
+    assert all(np.isfinite(line["rl/loss"]) for line in lines)
+    assert (tmp_path / "finetune" / "current" / "model.safetensors").exists()
+    assert (tmp_path / "finetune" / "training_state" / "optim").is_dir()
