@@ -2,7 +2,8 @@
 
     python -m pipelinerl_amd._build [--resource-usage]
 
-The library is the C-ABI declared in include/prl_hip.h.  It is built next to this file so
+The library is the C-ABI declared in include/prl_hip.h.  libprl_comm.so (include/prl_comm.h,
+csrc/comm.cpp) is the separate RCCL-linked communicator library.  It is built next to this file so
 it travels with the repository snapshot to the GPU box (a JIT cache would not).
 """
 
@@ -20,6 +21,7 @@ REPO = PKG.parents[1]
 INCLUDE = REPO / "include"
 CSRC = PKG / "csrc"
 LIB = PKG / "libprl_hip.so"
+COMM_LIB = PKG / "libprl_comm.so"
 ARCH = "gfx950"
 SOURCES = ["grpo_loss.hip", "flat_pack.hip"]
 
@@ -40,6 +42,23 @@ def _stale() -> bool:
 
 
 VARIANT_DIR = PKG / "variants"
+
+
+def build_comm(force: bool = False) -> Path:
+    """libprl_comm.so: host code over RCCL (no device code), rpath to the ROCm libraries."""
+    src, hdr = CSRC / "comm.cpp", INCLUDE / "prl_comm.h"
+    if not force and COMM_LIB.exists() and COMM_LIB.stat().st_mtime > max(src.stat().st_mtime,
+                                                                           hdr.stat().st_mtime):
+        return COMM_LIB
+    rocm = Path(hipcc()).resolve().parents[1]
+    tmp = COMM_LIB.with_suffix(".so.tmp")
+    cmd = [hipcc(), "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", f"-I{INCLUDE}", f"-I{rocm / 'include'}",
+           str(src), "-o", str(tmp), f"-L{rocm / 'lib'}", "-lrccl", f"-Wl,-rpath,{rocm / 'lib'}"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for comm.cpp:\n{r.stderr[-8000:]}")
+    os.replace(tmp, COMM_LIB)
+    return COMM_LIB
 
 
 def build(force: bool = False, resource_usage: bool = False, verbose: bool = False,
@@ -89,3 +108,4 @@ def build_variant(name: str, defines: dict[str, str]) -> Path:
 if __name__ == "__main__":
     out = build(force=True, resource_usage="--resource-usage" in sys.argv, verbose=True)
     print(out)
+    print(build_comm(force=True))

@@ -28,9 +28,8 @@ import types
 from typing import Any
 
 import torch
-import torch.distributed as dist
 
-from . import torch_utils
+from . import comm, torch_utils
 from .weight_update import FlatLayout, WeightUpdateRequest
 
 logger = logging.getLogger(__name__)
@@ -45,6 +44,12 @@ class WorkerExtension:
         logger.info(f"[INIT_ACTOR_UPDATE_GROUP]: actor {actor_idx}, ngpus {actor_ngpus}, rank {self.rank}, "
                     f"pg_rank {self.pg_rank}, init {weight_update_group_init_method}, "
                     f"world {weight_update_group_world_size}")
+        if self.actor_group_backend == "prl_comm":  # RCCL communicator of the prl_comm C ABI
+            from .comm import RcclComm
+
+            self.process_group = RcclComm.create(weight_update_group_init_method, self.pg_rank,
+                                                 weight_update_group_world_size, self.device)
+            return
         self.process_group = torch_utils.init_extra_process_group(
             group_name="actor", backend=self.actor_group_backend, init_method=weight_update_group_init_method,
             rank=self.pg_rank, world_size=weight_update_group_world_size)
@@ -63,7 +68,7 @@ class WorkerExtension:
         else:
             for info in request.parameters_info:
                 buf = torch.empty(tuple(info.shape), dtype=model_dtype, device=self.device)
-                dist.broadcast(buf, src=0, group=self.process_group)
+                comm.broadcast(buf, self.process_group, src=0)
                 self._load_one(info.name, buf)
         logger.info("Weight update received")
 
@@ -76,7 +81,7 @@ class WorkerExtension:
         flat = staging[:layout.total]
         elems = max(8, int(request.bucket_bytes) // 2)
         for a, b in layout.buckets(elems):
-            dist.broadcast(flat[a:b], src=0, group=self.process_group)
+            comm.broadcast(flat[a:b], self.process_group, src=0)
         for name, shape, n, off in zip(layout.names, layout.shapes, layout.numels, layout.offsets):
             self._load_one(name, flat[off:off + n].view(shape))
 

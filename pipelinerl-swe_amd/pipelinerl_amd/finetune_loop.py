@@ -208,10 +208,16 @@ def run_finetuning_loop(cfg, step_fn: Callable = rl_step, model=None, tokenizer=
     if ctx.is_main and args.send_weight_updates:
         from .torch_utils import init_extra_process_group
 
-        actor_group = init_extra_process_group(
-            group_name="actor", backend=args.get("actor_group_backend", "nccl"),
-            init_method=cfg.me.weight_update_group_init_method, rank=0,
-            world_size=cfg.me.weight_update_group_world_size)
+        backend = args.get("actor_group_backend", "nccl")
+        if backend == "prl_comm":  # RCCL communicator of the prl_comm C ABI (comm.py)
+            from .comm import RcclComm
+
+            actor_group = RcclComm.create(cfg.me.weight_update_group_init_method, 0,
+                                          cfg.me.weight_update_group_world_size, ctx.device)
+        else:
+            actor_group = init_extra_process_group(
+                group_name="actor", backend=backend, init_method=cfg.me.weight_update_group_init_method, rank=0,
+                world_size=cfg.me.weight_update_group_world_size)
     ctx.barrier()
 
     metrics = TrainingMetrics()
@@ -248,7 +254,10 @@ def run_finetuning_loop(cfg, step_fn: Callable = rl_step, model=None, tokenizer=
         if wum is not None:
             wum.close()
         if actor_group is not None:
-            dist.destroy_process_group(actor_group)
+            if hasattr(actor_group, "close"):
+                actor_group.close()
+            else:
+                dist.destroy_process_group(actor_group)
 
 
 def rl_finetuning_worker(args, ctx: Dist, model, optimizer, lr_scheduler, grads: GradBuckets | None,

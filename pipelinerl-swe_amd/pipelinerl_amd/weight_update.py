@@ -36,6 +36,8 @@ import torch
 import torch.distributed as dist
 from pydantic import BaseModel, Field
 
+from . import comm
+
 logger = logging.getLogger(__name__)
 
 TRAINER_TOPIC = "weight_update_request"
@@ -247,11 +249,11 @@ class WeightUpdateManager:
             if self.transport == "bucketed":
                 elems = max(ALIGN, self.bucket_bytes // 2)
                 for a, b in layout.buckets(elems):
-                    works.append(dist.broadcast(flat[a:b], src=0, group=self.group, async_op=True))
+                    works.append(comm.broadcast(flat[a:b], self.group, src=0, async_op=True))
             else:
                 for shape, n, off in zip(layout.shapes, layout.numels, layout.offsets):
-                    works.append(dist.broadcast(flat[off:off + n].view(shape), src=0, group=self.group,
-                                                async_op=True))
+                    works.append(comm.broadcast(flat[off:off + n].view(shape), self.group, src=0, async_op=True))
+            works = [w for w in works if w is not None]  # RcclComm calls are stream-ordered
             done = None
             if on_gpu:
                 for w in works:  # RCCL: makes the side stream (not the host) wait for the comm

@@ -49,3 +49,20 @@ def test_invalid_arguments_rejected_without_gpu():
     # null pointers / zero shapes are rejected before any device call
     assert lib.prl_grpo_forward(ctypes.byref(b), ctypes.byref(p), ctypes.byref(o), None, 0, None) == 1001
     assert lib.prl_flatten_bf16(None, None, None, None, -1, None, None) == 1001
+
+
+def test_comm_library_exports_header_symbols():
+    """libprl_comm.so (RCCL C ABI, include/prl_comm.h) loads without a GPU and exports every
+    declared function."""
+    from pipelinerl_amd import comm
+
+    lib = comm.load()
+    text = comm.HEADER_PATH.read_text()
+    declared = sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(prl_comm_\w+)\s*\(", text, flags=re.M)))
+    assert len(declared) >= 10
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert lib.prl_comm_abi_version() == 1
+    assert lib.prl_comm_error_string(3001).decode() == "invalid argument"
+    h = ctypes.c_void_p()
+    assert lib.prl_comm_init(None, 0, 1, 0, ctypes.byref(h)) == 3001  # argument checks before any HIP call
