@@ -1,0 +1,66 @@
+"""Throughput of the trainer-input preprocessing (populate_rl_data + collate_packed) on a
+C3-shaped rollout set: 64 groups x 8 rollouts, prompt U{64..512}, completion U{256..8192},
+packed into 12 000-token micro-batches.  --reference also times the reference's own
+populate_rl_data / collate_packed (pandas) on the same rollouts (build container only).
+Prints one JSON line."""
+import json
+import sys, time, types, numpy as np
+from pathlib import Path
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT / "pipelinerl-swe_amd")]
+from pipelinerl_amd.finetune.rl import RLConfig, populate_rl_data, prepare_rl_fields
+from pipelinerl_amd.finetune.data import collate_packed
+rng = np.random.default_rng(0)
+EOS=151643
+data=[]
+t0=time.time()
+for g in range(64):
+    for a in range(8):
+        p, c = int(rng.integers(64, 513)), int(rng.integers(256, 8193))
+        ids = rng.integers(0, 151643, p + c).tolist()
+        if rng.random() < 0.75: ids[-1] = EOS
+        labels = [-100] * p + ids[p:]
+        lps = (-rng.random(c) * 4).tolist()
+        enc = prepare_rl_fields({"input_ids": ids, "labels": labels, "attention_mask": [1] * len(ids)}, float(rng.integers(0, 2)), lps, lps)
+        enc.update(group_id=f"g{g}", rollout_index=a, step_index=0, model_version=0)
+        data.append(enc)
+t1=time.time()
+out = populate_rl_data(data, EOS, RLConfig())
+t2=time.time()
+ntok=sum(len(d["input_ids"]) for d in out)
+# pack ~12000-token micro-batches
+i=0; nb=0
+t3=time.time()
+while i < len(out):
+    cur=[]; tot=0
+    while i < len(out) and tot + len(out[i]["input_ids"]) <= 12000:
+        cur.append(out[i]); tot += len(out[i]["input_ids"]); i += 1
+    if not cur: cur=[out[i]]; i+=1
+    collate_packed(cur, types.SimpleNamespace(eos_token_id=EOS), 1); nb+=1
+t4=time.time()
+res = {"rollouts": len(out), "tokens": ntok, "micro_batches": nb,
+       "build": {"populate_s": round(t2 - t1, 3), "populate_Mtok_s": round(ntok / (t2 - t1) / 1e6, 2),
+                 "collate_s": round(t4 - t3, 3), "collate_Mtok_s": round(ntok / (t4 - t3) / 1e6, 2)}}
+if "--reference" in sys.argv:
+    import copy
+    import os
+    sys.modules.setdefault("omegaconf", types.SimpleNamespace(DictConfig=dict))
+    sys.path.insert(0, "/root/reference")
+    os.environ["PYTHONDONTWRITEBYTECODE"] = "1"
+    sys.dont_write_bytecode = True
+    from pipelinerl.finetune.rl import RLConfig as RefCfg, populate_rl_data as ref_populate
+    from pipelinerl.finetune.data import collate_packed as ref_collate
+    t5 = time.time()
+    rout = ref_populate(copy.deepcopy(data), EOS, RefCfg())
+    t6 = time.time()
+    i = 0
+    while i < len(rout):
+        cur=[]; tot=0
+        while i < len(rout) and tot + len(rout[i]["input_ids"]) <= 12000:
+            cur.append(rout[i]); tot += len(rout[i]["input_ids"]); i += 1
+        if not cur: cur=[rout[i]]; i+=1
+        ref_collate(cur, types.SimpleNamespace(eos_token_id=EOS), 1)
+    t7 = time.time()
+    res["reference"] = {"populate_s": round(t6 - t5, 3), "populate_Mtok_s": round(ntok / (t6 - t5) / 1e6, 2),
+                        "collate_s": round(t7 - t6, 3), "collate_Mtok_s": round(ntok / (t7 - t6) / 1e6, 2)}
+print(json.dumps(res))
