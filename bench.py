@@ -16,6 +16,11 @@ paths over the C2 model's parameter set (pipelinerl_amd/comm_probe.py) and repor
 "exchange": the bucketed DP gradient all-reduce (GradBuckets, RCCL) and the trainer -> actors
 weight broadcast (WeightUpdateManager -> WorkerExtension, rank 0 -> ranks 1..N-1).
 
+After that, at every N, the whole optimizer step the loss head sits in is measured and reported
+under "trainer_step" (pipelinerl_amd/trainer_probe.py): Qwen2.5-1.5B shapes (random init, bf16),
+4 packed micro-batches of 16 384 tokens per rank (varlen attention, fused loss head, backward),
+the bucketed RCCL gradient all-reduce overlapped with the last backward, clip, fused AdamW.
+
 Prints ONE JSON line (rank 0).  roofline.achieved = algorithmic bytes per launch
 (T*V*2 read + T*V*2 dlogits write + 37*T side data) / the average duration
 of the prl_grpo_forward launch measured with HIP events on its stream.
@@ -112,6 +117,7 @@ def main():
     ap.add_argument("--cpu-rows", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-comm-probe", action="store_true", help="N > 1: skip the all-reduce / broadcast probes")
+    ap.add_argument("--no-trainer-step", action="store_true", help="skip the full trainer-step probe")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -178,12 +184,20 @@ def main():
         # timed region (not part of `value`): DP gradient all-reduce, trainer -> actors broadcast
         from pipelinerl_amd import comm_probe
 
-        del logits, fields
+        logits = fields = None
         torch.cuda.empty_cache()
         shapes = comm_probe.qwen2_param_shapes("1.5b")
         comm = {"model": "Qwen2.5-1.5B parameter shapes, bf16",
                 "grad_allreduce": comm_probe.grad_allreduce_probe(shapes, dev, iters=5),
                 "weight_broadcast": comm_probe.broadcast_probe(shapes, dev, iters=3)}
+    trainer = None
+    if not args.no_trainer_step:
+        # the whole optimizer step the loss head sits in (reported beside `value`, not in it)
+        from pipelinerl_amd.trainer_probe import trainer_step_probe
+
+        logits = fields = None
+        torch.cuda.empty_cache()
+        trainer = trainer_step_probe("1.5b", tokens=16384, micro_batches=4, steps=3, warmup=1, device=dev)
 
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
@@ -220,6 +234,8 @@ def main():
         }
         if comm is not None:
             out["exchange"] = comm
+        if trainer is not None:
+            out["trainer_step"] = trainer
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

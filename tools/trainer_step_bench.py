@@ -23,37 +23,7 @@ sys.path[:0] = [str(ROOT), str(ROOT / "pipelinerl-swe_amd"), str(ROOT / "tools")
 
 import torch  # noqa: E402
 
-QWEN = {  # published Qwen2.5 shapes (config.json of each checkpoint)
-    "0.5b": dict(hidden_size=896, intermediate_size=4864, num_hidden_layers=24, num_attention_heads=14,
-                 num_key_value_heads=2, vocab_size=151936, tie_word_embeddings=True),
-    "1.5b": dict(hidden_size=1536, intermediate_size=8960, num_hidden_layers=28, num_attention_heads=12,
-                 num_key_value_heads=2, vocab_size=151936, tie_word_embeddings=True),
-    "7b": dict(hidden_size=3584, intermediate_size=18944, num_hidden_layers=28, num_attention_heads=28,
-               num_key_value_heads=4, vocab_size=152064, tie_word_embeddings=False),
-}
-
-
-def packed_batch(T, seq, prompt, V, device, seed=0):
-    from pipelinerl_amd.finetune.types import PipelineBatchEncoding
-
-    g = torch.Generator().manual_seed(seed)
-    nseq = T // seq
-    pos = torch.arange(T) % seq
-    ids = torch.randint(0, min(V, 151643), (1, T), generator=g)
-    labels = torch.where(pos[None] >= prompt, ids, torch.full_like(ids, -100))
-    rewards = torch.repeat_interleave(torch.randint(0, 2, (nseq,), generator=g).float(), seq)[None]
-    lab = (labels != -100).float()
-    old = (torch.randn((1, T), generator=g) - 12.0) * lab
-    b = PipelineBatchEncoding(
-        input_ids=ids, labels=labels, attention_mask=torch.ones_like(ids), position_ids=pos[None],
-        rewards=rewards, advantages=rewards - rewards.mean(), ref_logprobs=old.clone(), old_logprobs=old,
-        group_tokens=torch.full((1, T), float(seq)), num_labels=torch.full((1, T), float(seq - prompt)),
-        overflow=torch.zeros((1, T)), seq_boundaries=torch.arange(0, T + 1, seq, dtype=torch.int32),
-        model_version=0, is_packed=True)
-    sb = b.seq_boundaries
-    b.to_device(device)
-    b.seq_boundaries = sb  # host metadata, as the trainer's loader keeps it
-    return b
+from pipelinerl_amd.trainer_probe import QWEN, packed_batch  # noqa: E402
 
 
 def timed(fn, steps, warmup):
