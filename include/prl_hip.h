@@ -205,6 +205,31 @@ int prl_grad_sqnorm(const void* const* srcs, const int32_t* dtypes, const int64_
                     int32_t n, double* out, void* workspace, size_t workspace_bytes,
                     void* stream);
 
+/* ---- Trainer-step model ops (bf16; csrc/model_ops.hip).  One HBM pass each; the forward
+ * reproduces the eager HF chains' bf16 roundings (transformers Qwen2RMSNorm.forward,
+ * Qwen2MLP.forward act_fn(gate) * up with SiLU, apply_rotary_pos_emb).  Row-major contiguous
+ * tensors, 16-B aligned (8-B for RoPE), H and D multiples of 8; PRL_E_UNSUPPORTED otherwise. */
+
+/* y = bf16(w * bf16(x * rsqrt(mean(x^2) + eps))) per row of H; rstd[rows] saved (fp32). */
+int prl_rmsnorm_forward(const void* x, const void* w, void* y, float* rstd, int64_t rows, int64_t H,
+                        float eps, void* stream);
+int prl_rmsnorm_workspace_bytes(int64_t H, size_t* bytes);
+/* dx and dw (bf16, dw reduced over all rows through the fp32 workspace); H <= 5120. */
+int prl_rmsnorm_backward(const void* dy, const void* x, const void* w, const float* rstd, void* dx,
+                         void* dw, void* workspace, size_t workspace_bytes, int64_t rows, int64_t H,
+                         void* stream);
+/* out = bf16(bf16(silu(gate)) * up) over n elements; backward gives dgate, dup. */
+int prl_swiglu_forward(const void* gate, const void* up, void* out, int64_t n, void* stream);
+int prl_swiglu_backward(const void* dout, const void* gate, const void* up, void* dgate, void* dup,
+                        int64_t n, void* stream);
+/* q [tokens, hq, d], k [tokens, hkv, d] token-major; cos / sin [tokens, d] (HF layout:
+ * halves repeated).  Out-of-place; backward applies the transposed rotation. */
+int prl_rope_forward(const void* q, const void* k, const void* cos, const void* sin, void* q_out,
+                     void* k_out, int64_t tokens, int32_t hq, int32_t hkv, int32_t d, void* stream);
+int prl_rope_backward(const void* dq_out, const void* dk_out, const void* cos, const void* sin,
+                      void* dq, void* dk, int64_t tokens, int32_t hq, int32_t hkv, int32_t d,
+                      void* stream);
+
 #ifdef __cplusplus
 }
 #endif

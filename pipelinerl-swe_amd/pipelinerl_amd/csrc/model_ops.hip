@@ -1,0 +1,399 @@
+// Fused element-wise ops of the trainer's model step (Qwen2 / Llama-style decoder), bf16.
+//
+// In the reference's trainer these run as HF eager op chains (transformers Qwen2RMSNorm,
+// Qwen2MLP act_fn(gate) * up, apply_rotary_pos_emb): ~25 % of a 1.5B trainer step on MI355X
+// is those chains (profiles/r01_trainer_step_kernel_stats.csv).  Each op here is one HBM pass
+// forward and one backward, and the forward reproduces the eager chain's bf16 roundings
+// exactly (same intermediate casts), so patched and unpatched models agree bit for bit in
+// the forward pass.
+//   rmsnorm   y = bf16(w * bf16(x * rsqrt(mean(x^2) + eps)))         (fp32 statistics)
+//   swiglu    h = bf16(bf16(silu(g)) * u)
+//   rope      q' = bf16(bf16(q * cos) + bf16(rotate_half(q) * sin))  (q and k in one launch)
+// HBM-bound: 16-B vector loads/stores, one wave per row for the norms.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <utility>
+
+#include "prl_hip.h"
+
+namespace prl_ops {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float lo(uint32_t v) { return __builtin_bit_cast(float, v << 16); }
+__device__ __forceinline__ float hi(uint32_t v) { return __builtin_bit_cast(float, v & 0xFFFF0000u); }
+__device__ __forceinline__ uint32_t rne(float f) {  // float -> bf16 bits, round to nearest even
+  const uint32_t u = __builtin_bit_cast(uint32_t, f);
+  if ((u & 0x7FFFFFFFu) > 0x7F800000u) return (u >> 16) | 0x40u;  // NaN stays NaN
+  return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+}
+__device__ __forceinline__ float r16(float f) { return __builtin_bit_cast(float, rne(f) << 16); }  // bf16 round
+__device__ __forceinline__ uint32_t pack(float a, float b) { return rne(a) | (rne(b) << 16); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// ---------------------------------------------------------------------------------------
+// RMSNorm.  One wave per row; the row (H <= 64 * 8 * NV bf16) stays in registers.
+template <int NV>
+__global__ __launch_bounds__(256) void rmsnorm_fwd(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
+                                                   uint16_t* __restrict__ y, float* __restrict__ rstd,
+                                                   int64_t rows, int H, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
+  const int nv8 = H >> 3;
+  u32x4 wv[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int c = k * 64 + lane;
+    wv[k] = c < nv8 ? reinterpret_cast<const u32x4*>(w)[c] : u32x4{0, 0, 0, 0};
+  }
+  for (int64_t r = wave; r < rows; r += nwaves) {
+    const u32x4* xr = reinterpret_cast<const u32x4*>(x + r * H);
+    u32x4 xv[NV];
+    float ss = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = k * 64 + lane;
+      xv[k] = c < nv8 ? __builtin_nontemporal_load(xr + c) : u32x4{0, 0, 0, 0};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float a = lo(xv[k][j]), b = hi(xv[k][j]);
+        ss = __builtin_fmaf(a, a, __builtin_fmaf(b, b, ss));
+      }
+    }
+    ss = wave_sum(ss);
+    const float rs = 1.0f / __builtin_sqrtf(ss / (float)H + eps);
+    if (lane == 0) rstd[r] = rs;
+    u32x4* yr = reinterpret_cast<u32x4*>(y + r * H);
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = k * 64 + lane;
+      if (c < nv8) {
+        u32x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float t0 = r16(lo(xv[k][j]) * rs), t1 = r16(hi(xv[k][j]) * rs);
+          o[j] = pack(lo(wv[k][j]) * t0, hi(wv[k][j]) * t1);
+        }
+        __builtin_nontemporal_store(o, yr + c);
+      }
+    }
+  }
+}
+
+// dx_i = r g_i - (r^3 / H) x_i sum_j g_j x_j with g = bf16(dy * w);  dw partial per block:
+// sum over the block's rows of bf16(dy * bf16(x r)) (the eager chain's weight-grad product).
+template <int NV>
+__global__ __launch_bounds__(256) void rmsnorm_bwd(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
+                                                   const uint16_t* __restrict__ w, const float* __restrict__ rstd,
+                                                   uint16_t* __restrict__ dx, float* __restrict__ partial,
+                                                   int64_t rows, int H) {
+  __shared__ float red[4][64 * 8 * NV];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t wave = (int64_t)blockIdx.x * 4 + wid;
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
+  const int nv8 = H >> 3;
+  const float invH = 1.0f / (float)H;
+  u32x4 wv[NV];
+  float acc[NV][8];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int c = k * 64 + lane;
+    wv[k] = c < nv8 ? reinterpret_cast<const u32x4*>(w)[c] : u32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[k][j] = 0.f;
+  }
+  for (int64_t r = wave; r < rows; r += nwaves) {
+    const u32x4* xr = reinterpret_cast<const u32x4*>(x + r * H);
+    const u32x4* gr = reinterpret_cast<const u32x4*>(dy + r * H);
+    const float rs = rstd[r];
+    u32x4 xv[NV], gv[NV];
+    float dot = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = k * 64 + lane;
+      xv[k] = c < nv8 ? __builtin_nontemporal_load(xr + c) : u32x4{0, 0, 0, 0};
+      gv[k] = c < nv8 ? __builtin_nontemporal_load(gr + c) : u32x4{0, 0, 0, 0};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float g0 = r16(lo(gv[k][j]) * lo(wv[k][j])), g1 = r16(hi(gv[k][j]) * hi(wv[k][j]));
+        dot = __builtin_fmaf(g0, lo(xv[k][j]), __builtin_fmaf(g1, hi(xv[k][j]), dot));
+        const float t0 = r16(lo(xv[k][j]) * rs), t1 = r16(hi(xv[k][j]) * rs);
+        acc[k][2 * j] += r16(lo(gv[k][j]) * t0);
+        acc[k][2 * j + 1] += r16(hi(gv[k][j]) * t1);
+      }
+    }
+    dot = wave_sum(dot);
+    const float cfac = rs * rs * rs * invH * dot;
+    u32x4* dr = reinterpret_cast<u32x4*>(dx + r * H);
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = k * 64 + lane;
+      if (c < nv8) {
+        u32x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float g0 = r16(lo(gv[k][j]) * lo(wv[k][j])), g1 = r16(hi(gv[k][j]) * hi(wv[k][j]));
+          o[j] = pack(rs * g0 - cfac * lo(xv[k][j]), rs * g1 - cfac * hi(xv[k][j]));
+        }
+        __builtin_nontemporal_store(o, dr + c);
+      }
+    }
+  }
+  // block partial of dw: fold the 4 waves in LDS, one row of H floats per block
+#pragma unroll
+  for (int k = 0; k < NV; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[wid][(k * 64 + lane) * 8 + j] = acc[k][j];
+  __syncthreads();
+  for (int i = threadIdx.x; i < H; i += 256)
+    partial[(int64_t)blockIdx.x * H + i] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+}
+
+__global__ __launch_bounds__(256) void rmsnorm_dw_finalize(const float* __restrict__ partial, int nblocks, int H,
+                                                           uint16_t* __restrict__ dw) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= H) return;
+  float s = 0.f;
+  for (int b = 0; b < nblocks; ++b) s += partial[(int64_t)b * H + i];
+  dw[i] = (uint16_t)rne(s);
+}
+
+// ---------------------------------------------------------------------------------------
+// SwiGLU: h = bf16(bf16(silu(g)) * u)
+__device__ __forceinline__ float silu(float g) { return g / (1.0f + expf(-g)); }
+
+__global__ __launch_bounds__(256) void swiglu_fwd(const u32x4* __restrict__ g, const u32x4* __restrict__ u,
+                                                  u32x4* __restrict__ h, int64_t n8) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += stride) {
+    const u32x4 gv = __builtin_nontemporal_load(g + i), uv = __builtin_nontemporal_load(u + i);
+    u32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      o[j] = pack(r16(silu(lo(gv[j]))) * lo(uv[j]), r16(silu(hi(gv[j]))) * hi(uv[j]));
+    __builtin_nontemporal_store(o, h + i);
+  }
+}
+
+// du = bf16(dh * s), s = bf16(silu(g));  dg = bf16(bf16(dh * u) * sig (1 + g (1 - sig)))
+__global__ __launch_bounds__(256) void swiglu_bwd(const u32x4* __restrict__ dh, const u32x4* __restrict__ g,
+                                                  const u32x4* __restrict__ u, u32x4* __restrict__ dg,
+                                                  u32x4* __restrict__ du, int64_t n8) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += stride) {
+    const u32x4 dv = __builtin_nontemporal_load(dh + i), gv = __builtin_nontemporal_load(g + i),
+                uv = __builtin_nontemporal_load(u + i);
+    u32x4 og, ou;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float dgr[2], dur[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const float gg = e ? hi(gv[j]) : lo(gv[j]);
+        const float uu = e ? hi(uv[j]) : lo(uv[j]);
+        const float dd = e ? hi(dv[j]) : lo(dv[j]);
+        const float sig = 1.0f / (1.0f + expf(-gg));
+        dur[e] = dd * r16(silu(gg));  // the saved bf16 activation, as the eager chain keeps it
+        const float ds = r16(dd * uu);
+        dgr[e] = ds * (sig * (1.0f + gg * (1.0f - sig)));
+      }
+      og[j] = pack(dgr[0], dgr[1]);
+      ou[j] = pack(dur[0], dur[1]);
+    }
+    __builtin_nontemporal_store(og, dg + i);
+    __builtin_nontemporal_store(ou, du + i);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// RoPE on q [T, Hq, D] and k [T, Hkv, D] (token-major, contiguous), cos / sin [T, D].
+// One thread per (token, head, 4 rotation pairs).  dir = +1 forward, -1 backward
+// (backward: dx = dy cos + rotate_half^T(dy sin), with rotate_half^T(z) = [z2, -z1]).
+template <int DIR>
+__global__ __launch_bounds__(256) void rope_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
+                                                   const uint16_t* __restrict__ cs, const uint16_t* __restrict__ sn,
+                                                   uint16_t* __restrict__ qo, uint16_t* __restrict__ ko,
+                                                   int64_t tokens, int hq, int hkv, int D) {
+  const int half = D >> 1, chunks = half >> 2;  // 4 pairs per thread
+  const int per_tok = (hq + hkv) * chunks;
+  const int64_t total = tokens * per_tok;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += stride) {
+    const int64_t t = idx / per_tok;
+    const int rem = (int)(idx - t * per_tok);
+    const int h = rem / chunks, c = rem - h * chunks;
+    const bool isq = h < hq;
+    const uint16_t* src = isq ? q + (t * hq + h) * D : k + (t * hkv + (h - hq)) * D;
+    uint16_t* dst = isq ? qo + (t * hq + h) * D : ko + (t * hkv + (h - hq)) * D;
+    const int i = c * 4;
+    const u32x2 x1 = *reinterpret_cast<const u32x2*>(src + i), x2 = *reinterpret_cast<const u32x2*>(src + half + i);
+    const u32x2 c1 = *reinterpret_cast<const u32x2*>(cs + t * D + i),
+                c2 = *reinterpret_cast<const u32x2*>(cs + t * D + half + i);
+    const u32x2 s1 = *reinterpret_cast<const u32x2*>(sn + t * D + i),
+                s2 = *reinterpret_cast<const u32x2*>(sn + t * D + half + i);
+    u32x2 o1, o2;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      float a[2], b[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const float xa = e ? hi(x1[j]) : lo(x1[j]), xb = e ? hi(x2[j]) : lo(x2[j]);
+        const float ca = e ? hi(c1[j]) : lo(c1[j]), cb = e ? hi(c2[j]) : lo(c2[j]);
+        const float sa = e ? hi(s1[j]) : lo(s1[j]), sb = e ? hi(s2[j]) : lo(s2[j]);
+        if (DIR > 0) {  // [x1 c1 - x2 s1, x2 c2 + x1 s2]
+          a[e] = r16(xa * ca) + r16(-xb * sa);
+          b[e] = r16(xb * cb) + r16(xa * sb);
+        } else {        // [y1 c1 + y2 s2, y2 c2 - y1 s1]
+          a[e] = r16(xa * ca) + r16(xb * sb);
+          b[e] = r16(xb * cb) + (-r16(xa * sa));
+        }
+      }
+      o1[j] = pack(a[0], a[1]);
+      o2[j] = pack(b[0], b[1]);
+    }
+    *reinterpret_cast<u32x2*>(dst + i) = o1;
+    *reinterpret_cast<u32x2*>(dst + half + i) = o2;
+  }
+}
+
+constexpr int kMaxNV = 16;     // forward: H <= 8192
+constexpr int kMaxNVBwd = 10;  // backward keeps 8 x NV fp32 dw accumulators per lane: H <= 5120
+
+template <int NV>
+hipError_t launch_norm_fwd(const void* x, const void* w, void* y, float* rstd, int64_t rows, int H, float eps,
+                           int grid, hipStream_t s) {
+  hipLaunchKernelGGL(rmsnorm_fwd<NV>, dim3(grid), dim3(256), 0, s, (const uint16_t*)x, (const uint16_t*)w,
+                     (uint16_t*)y, rstd, rows, H, eps);
+  return hipGetLastError();
+}
+template <int NV>
+hipError_t launch_norm_bwd(const void* dy, const void* x, const void* w, const float* rstd, void* dx, float* partial,
+                           int64_t rows, int H, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(rmsnorm_bwd<NV>, dim3(grid), dim3(256), 0, s, (const uint16_t*)dy, (const uint16_t*)x,
+                     (const uint16_t*)w, rstd, (uint16_t*)dx, partial, rows, H);
+  return hipGetLastError();
+}
+template <int... N>
+hipError_t norm_fwd_table(int nv, const void* x, const void* w, void* y, float* rstd, int64_t rows, int H, float eps,
+                          int grid, hipStream_t s, std::integer_sequence<int, N...>) {
+  hipError_t e = hipErrorInvalidValue;
+  ((nv == N + 1 ? (e = launch_norm_fwd<N + 1>(x, w, y, rstd, rows, H, eps, grid, s), true) : false) || ...);
+  return e;
+}
+template <int... N>
+hipError_t norm_bwd_table(int nv, const void* dy, const void* x, const void* w, const float* rstd, void* dx,
+                          float* partial, int64_t rows, int H, int grid, hipStream_t s,
+                          std::integer_sequence<int, N...>) {
+  hipError_t e = hipErrorInvalidValue;
+  ((nv == N + 1 ? (e = launch_norm_bwd<N + 1>(dy, x, w, rstd, dx, partial, rows, H, grid, s), true) : false) || ...);
+  return e;
+}
+
+bool a16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+bool a8(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7u) == 0; }
+int ew_grid(int64_t n8) {
+  const int64_t g = (n8 + 255) / 256;
+  return (int)(g < 4096 ? (g > 0 ? g : 1) : 4096);
+}
+constexpr int kNormBlocks = 512;
+
+}  // namespace prl_ops
+
+using namespace prl_ops;
+
+extern "C" {
+
+int prl_rmsnorm_workspace_bytes(int64_t H, size_t* bytes) {
+  if (!bytes || H <= 0) return PRL_E_INVALID;
+  *bytes = sizeof(float) * (size_t)kNormBlocks * (size_t)H;
+  return PRL_OK;
+}
+
+int prl_rmsnorm_forward(const void* x, const void* w, void* y, float* rstd, int64_t rows, int64_t H, float eps,
+                        void* stream) {
+  if (!x || !w || !y || !rstd || rows < 0 || H <= 0) return PRL_E_INVALID;
+  if (H % 8 || H > 64 * 8 * kMaxNV || !a16(x) || !a16(w) || !a16(y)) return PRL_E_UNSUPPORTED;
+  if (rows == 0) return PRL_OK;
+  const int nv = (int)((H / 8 + 63) / 64);
+  const int64_t g = (rows + 3) / 4;
+  const int grid = (int)(g < 2048 ? g : 2048);
+  return (int)norm_fwd_table(nv, x, w, y, rstd, rows, (int)H, eps, grid, static_cast<hipStream_t>(stream),
+                             std::make_integer_sequence<int, kMaxNV>{});
+}
+
+int prl_rmsnorm_backward(const void* dy, const void* x, const void* w, const float* rstd, void* dx, void* dw,
+                         void* workspace, size_t workspace_bytes, int64_t rows, int64_t H, void* stream) {
+  if (!dy || !x || !w || !rstd || !dx || !dw || !workspace || rows < 0 || H <= 0) return PRL_E_INVALID;
+  if (H % 8 || H > 64 * 8 * kMaxNVBwd || !a16(x) || !a16(w) || !a16(dy) || !a16(dx)) return PRL_E_UNSUPPORTED;
+  if (workspace_bytes < sizeof(float) * (size_t)kNormBlocks * (size_t)H) return PRL_E_WORKSPACE;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int nv = (int)((H / 8 + 63) / 64);
+  const int64_t g = (rows + 3) / 4;
+  const int grid = (int)(g < kNormBlocks ? (g > 0 ? g : 1) : kNormBlocks);
+  float* partial = static_cast<float*>(workspace);
+  hipError_t e = norm_bwd_table(nv, dy, x, w, rstd, dx, partial, rows, (int)H, grid, s,
+                                std::make_integer_sequence<int, kMaxNVBwd>{});
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(rmsnorm_dw_finalize, dim3((unsigned)((H + 255) / 256)), dim3(256), 0, s, partial, grid,
+                     (int)H, (uint16_t*)dw);
+  return (int)hipGetLastError();
+}
+
+int prl_swiglu_forward(const void* gate, const void* up, void* out, int64_t n, void* stream) {
+  if (!gate || !up || !out || n < 0) return PRL_E_INVALID;
+  if (n % 8 || !a16(gate) || !a16(up) || !a16(out)) return PRL_E_UNSUPPORTED;
+  if (n == 0) return PRL_OK;
+  const int64_t n8 = n / 8;
+  hipLaunchKernelGGL(swiglu_fwd, dim3(ew_grid(n8)), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     (const u32x4*)gate, (const u32x4*)up, (u32x4*)out, n8);
+  return (int)hipGetLastError();
+}
+
+int prl_swiglu_backward(const void* dout, const void* gate, const void* up, void* dgate, void* dup, int64_t n,
+                        void* stream) {
+  if (!dout || !gate || !up || !dgate || !dup || n < 0) return PRL_E_INVALID;
+  if (n % 8 || !a16(dout) || !a16(gate) || !a16(up) || !a16(dgate) || !a16(dup)) return PRL_E_UNSUPPORTED;
+  if (n == 0) return PRL_OK;
+  const int64_t n8 = n / 8;
+  hipLaunchKernelGGL(swiglu_bwd, dim3(ew_grid(n8)), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     (const u32x4*)dout, (const u32x4*)gate, (const u32x4*)up, (u32x4*)dgate, (u32x4*)dup, n8);
+  return (int)hipGetLastError();
+}
+
+static int rope_launch(int dir, const void* q, const void* k, const void* cs, const void* sn, void* qo, void* ko,
+                       int64_t tokens, int32_t hq, int32_t hkv, int32_t d, void* stream) {
+  if (!q || !k || !cs || !sn || !qo || !ko || tokens < 0 || hq <= 0 || hkv < 0 || d <= 0) return PRL_E_INVALID;
+  if (d % 8 || !a8(q) || !a8(k) || !a8(cs) || !a8(sn) || !a8(qo) || !a8(ko)) return PRL_E_UNSUPPORTED;
+  if (tokens == 0) return PRL_OK;
+  const int64_t total = tokens * (int64_t)(hq + hkv) * (d / 8);
+  const int64_t g = (total + 255) / 256;
+  const int grid = (int)(g < 8192 ? g : 8192);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (dir > 0)
+    hipLaunchKernelGGL(rope_kernel<1>, dim3(grid), dim3(256), 0, s, (const uint16_t*)q, (const uint16_t*)k,
+                       (const uint16_t*)cs, (const uint16_t*)sn, (uint16_t*)qo, (uint16_t*)ko, tokens, hq, hkv, d);
+  else
+    hipLaunchKernelGGL(rope_kernel<-1>, dim3(grid), dim3(256), 0, s, (const uint16_t*)q, (const uint16_t*)k,
+                       (const uint16_t*)cs, (const uint16_t*)sn, (uint16_t*)qo, (uint16_t*)ko, tokens, hq, hkv, d);
+  return (int)hipGetLastError();
+}
+
+int prl_rope_forward(const void* q, const void* k, const void* cos, const void* sin, void* q_out, void* k_out,
+                     int64_t tokens, int32_t hq, int32_t hkv, int32_t d, void* stream) {
+  return rope_launch(1, q, k, cos, sin, q_out, k_out, tokens, hq, hkv, d, stream);
+}
+
+int prl_rope_backward(const void* dq_out, const void* dk_out, const void* cos, const void* sin, void* dq, void* dk,
+                      int64_t tokens, int32_t hq, int32_t hkv, int32_t d, void* stream) {
+  return rope_launch(-1, dq_out, dk_out, cos, sin, dq, dk, tokens, hq, hkv, d, stream);
+}
+
+}  // extern "C"

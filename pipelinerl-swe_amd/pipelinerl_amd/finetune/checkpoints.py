@@ -70,6 +70,10 @@ def load_model(args, model_class: str, current_dir: Path, device: torch.device):
         model = AutoModelForCausalLM.from_config(AutoConfig.from_pretrained(src), **kw)
     else:
         model = AutoModelForCausalLM.from_pretrained(src, **kw)
+    if device.type == "cuda" and args.get("fused_model_ops", True):  # HIP RMSNorm / SwiGLU / RoPE
+        from .model_ops import patch_model
+
+        patch_model(model)
     if args.get("gradient_checkpointing", False):
         model.gradient_checkpointing_enable(
             gradient_checkpointing_kwargs={"use_reentrant": bool(args.get("reentrant_checkpointing", False))})

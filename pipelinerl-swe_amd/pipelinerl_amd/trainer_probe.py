@@ -26,7 +26,7 @@ QWEN = {  # published Qwen2.5 shapes (config.json of each checkpoint)
 }
 
 
-def qwen2_model(name: str, device: torch.device, grad_ckpt: bool = False):
+def qwen2_model(name: str, device: torch.device, grad_ckpt: bool = False, fused_ops: bool = True):
     from transformers import AutoModelForCausalLM, Qwen2Config
 
     from .finetune.attention import register
@@ -35,6 +35,10 @@ def qwen2_model(name: str, device: torch.device, grad_ckpt: bool = False):
     torch.manual_seed(0)
     with torch.device(device):  # initialise on the GPU (a CPU init of 1.5B+ params takes minutes)
         model = AutoModelForCausalLM.from_config(cfg, dtype=torch.bfloat16, attn_implementation=register())
+    if fused_ops:
+        from .finetune.model_ops import patch_model
+
+        patch_model(model)
     if grad_ckpt:
         model.gradient_checkpointing_enable(gradient_checkpointing_kwargs={"use_reentrant": False})
     model.train()
@@ -75,7 +79,7 @@ def rl_config(samples_per_step: int, fused_head: bool = False):
 
 def trainer_step_probe(name: str = "1.5b", tokens: int = 16384, seq: int = 2048, prompt: int = 256,
                        micro_batches: int = 4, steps: int = 3, warmup: int = 1, device=None,
-                       fused_head: bool = False, grad_ckpt: bool = False) -> dict:
+                       fused_head: bool = False, grad_ckpt: bool = False, fused_ops: bool = True) -> dict:
     from .finetune.grad_sync import GradBuckets
     from .finetune.optim import get_optimizer
     from .finetune.rl import rl_step
@@ -84,7 +88,7 @@ def trainer_step_probe(name: str = "1.5b", tokens: int = 16384, seq: int = 2048,
     world = dist.get_world_size() if dist.is_initialized() else 1
     rank = dist.get_rank() if dist.is_initialized() else 0
     torch.cuda.reset_peak_memory_stats(device)
-    model = qwen2_model(name, device, grad_ckpt)
+    model = qwen2_model(name, device, grad_ckpt, fused_ops)
     opt = get_optimizer("adamw_torch", model, 1e-6, 0.01)
     grads = GradBuckets(list(model.parameters())) if world > 1 else None
     batches = [packed_batch(tokens, seq, prompt, QWEN[name]["vocab_size"], device, seed=rank * 97 + i)
@@ -129,6 +133,7 @@ def trainer_step_probe(name: str = "1.5b", tokens: int = 16384, seq: int = 2048,
     total = tokens * micro_batches * world
     return {"model": f"Qwen2.5-{name} shapes (random init, bf16)", "tokens_per_micro_batch": tokens,
             "micro_batches_per_step": micro_batches, "seq_len": seq, "prompt_len": prompt,
-            "loss_head": "fused_lm_head" if fused_head else "fused", "ms_per_optimizer_step": round(sec * 1e3, 2),
+            "loss_head": "fused_lm_head" if fused_head else "fused", "fused_model_ops": fused_ops,
+            "ms_per_optimizer_step": round(sec * 1e3, 2),
             "tokens_per_s": round(total / sec, 1), "tokens_per_s_per_gpu": round(total / sec / world, 1),
             "peak_mem_gb": round(peak, 2), "steps": steps, "warmup": warmup}

@@ -1,0 +1,164 @@
+"""Fused model ops (csrc/model_ops.hip) against the eager HF chains they replace, on the GPU.
+Forward: bit-identical to the eager bf16 chain.  Backward: against torch autograd through the
+same chain and against an fp32 reference of the op."""
+
+import copy
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _eager_rmsnorm(x, w, eps):  # transformers Qwen2RMSNorm.forward
+    h = x.to(torch.float32)
+    var = h.pow(2).mean(-1, keepdim=True)
+    h = h * torch.rsqrt(var + eps)
+    return w * h.to(x.dtype)
+
+
+def _close(a, b, rtol, atol=0.0):
+    err = (a.float() - b.float()).abs()
+    lim = atol + rtol * b.float().abs()
+    return bool((err <= lim).all()), float(err.max())
+
+
+@pytest.mark.parametrize("H", [896, 1536, 3584, 5120])
+def test_rmsnorm(H):
+    from pipelinerl_amd.finetune.model_ops import RMSNormFn
+
+    g = torch.Generator(device=DEV).manual_seed(H)
+    x = (torch.randn((3, 701, H), generator=g, device=DEV) * 2).to(torch.bfloat16)
+    w = (1 + 0.1 * torch.randn(H, generator=g, device=DEV)).to(torch.bfloat16)
+    dy = torch.randn((3, 701, H), generator=g, device=DEV).to(torch.bfloat16)
+    xa, wa = x.clone().requires_grad_(), w.clone().requires_grad_()
+    ya = _eager_rmsnorm(xa, wa, 1e-6)
+    ya.backward(dy)
+    xb, wb = x.clone().requires_grad_(), w.clone().requires_grad_()
+    yb = RMSNormFn.apply(xb, wb, 1e-6)
+    yb.backward(dy)
+    # forward: same roundings; rstd from a different fp32 summation order may flip a last bit
+    diff = (ya.float() != yb.float()).float().mean().item()
+    assert diff < 1e-3, diff
+    assert _close(yb, ya, 1.6e-2)[0]  # <= 2 bf16 ulps where a last bit of rstd flips
+    ok, err = _close(xb.grad, xa.grad, 2e-2, 1e-3)
+    assert ok, err
+    # fp32 reference of the op for the weight gradient (both bf16 paths reduce 2103 rows)
+    xf, wf = x.float().requires_grad_(), w.float().requires_grad_()
+    (_eager_rmsnorm(xf, wf, 1e-6) * dy.float()).sum().backward()
+    ok, err = _close(wb.grad, wf.grad, 2e-2, 1e-2 * float(wf.grad.abs().max()))
+    assert ok, err
+
+
+def test_swiglu():
+    from pipelinerl_amd.finetune.model_ops import SwiGLUFn
+
+    g0 = torch.Generator(device=DEV).manual_seed(1)
+    gate = (torch.randn((5, 333, 1024), generator=g0, device=DEV) * 3).to(torch.bfloat16)
+    up = torch.randn((5, 333, 1024), generator=g0, device=DEV).to(torch.bfloat16)
+    dh = torch.randn((5, 333, 1024), generator=g0, device=DEV).to(torch.bfloat16)
+    ga, ua = gate.clone().requires_grad_(), up.clone().requires_grad_()
+    ha = torch.nn.functional.silu(ga) * ua
+    ha.backward(dh)
+    gb, ub = gate.clone().requires_grad_(), up.clone().requires_grad_()
+    hb = SwiGLUFn.apply(gb, ub)
+    hb.backward(dh)
+    assert torch.equal(ha, hb)
+    assert torch.equal(ua.grad, ub.grad)
+    ok, err = _close(gb.grad, ga.grad, 8e-3, 1e-6)
+    assert ok, err
+
+
+def test_rope_matches_hf():
+    from transformers.models.qwen2 import modeling_qwen2 as mq
+
+    from pipelinerl_amd.finetune.model_ops import RopeFn
+
+    B, T, hq, hkv, D = 2, 97, 12, 2, 128
+    g = torch.Generator(device=DEV).manual_seed(3)
+    qp = torch.randn((B, T, hq * D), generator=g, device=DEV).to(torch.bfloat16)
+    kp = torch.randn((B, T, hkv * D), generator=g, device=DEV).to(torch.bfloat16)
+    pos = torch.arange(T, device=DEV)[None].expand(B, T) + torch.tensor([[0], [5]], device=DEV)
+    inv = 1.0 / (1e6 ** (torch.arange(0, D, 2, device=DEV).float() / D))
+    fr = pos[..., None].float() * inv
+    emb = torch.cat([fr, fr], -1)
+    cos, sin = emb.cos().to(torch.bfloat16), emb.sin().to(torch.bfloat16)
+    dq = torch.randn((B, hq, T, D), generator=g, device=DEV).to(torch.bfloat16)
+    dk = torch.randn((B, hkv, T, D), generator=g, device=DEV).to(torch.bfloat16)
+
+    def views(a, b):
+        a = a.clone().requires_grad_()
+        b = b.clone().requires_grad_()
+        return a, b, a.view(B, T, hq, D).transpose(1, 2), b.view(B, T, hkv, D).transpose(1, 2)
+
+    qa0, ka0, qa, ka = views(qp, kp)
+    oqa, oka = mq.apply_rotary_pos_emb(qa, ka, cos, sin)
+    torch.autograd.backward([oqa, oka], [dq, dk])
+    qb0, kb0, qb, kb = views(qp, kp)
+    oqb, okb = RopeFn.apply(qb, kb, cos, sin)
+    torch.autograd.backward([oqb, okb], [dq, dk])
+    assert torch.equal(oqa, oqb) and torch.equal(oka, okb)
+    assert oqb.transpose(1, 2).is_contiguous()
+    assert torch.equal(qa0.grad, qb0.grad) and torch.equal(ka0.grad, kb0.grad)
+
+
+def test_patched_qwen2_matches_eager(tmp_path):
+    from loop_helpers import tiny_model_dir
+    from transformers import AutoConfig, AutoModelForCausalLM
+
+    from pipelinerl_amd.finetune.attention import packed_kwargs, register
+    from pipelinerl_amd.finetune.model_ops import patch_model
+
+    cfg = AutoConfig.from_pretrained(tiny_model_dir(tmp_path, vocab=512))
+    cfg.hidden_size, cfg.intermediate_size, cfg.num_attention_heads, cfg.num_key_value_heads = 256, 512, 4, 2
+    torch.manual_seed(0)
+    eager = AutoModelForCausalLM.from_config(cfg, dtype=torch.bfloat16, attn_implementation=register()).to(DEV)
+    fused = copy.deepcopy(eager)
+    T = 96
+    ids = torch.randint(0, 512, (1, T), device=DEV)
+    pos = torch.cat([torch.arange(40), torch.arange(56)])[None].to(DEV)
+    batch = type("B", (), {"seq_boundaries": torch.tensor([0, 40, 96]), "position_ids": pos})()
+    kw = packed_kwargs(batch, DEV)
+    outs = []
+    try:
+        for m in (eager, fused):
+            if m is fused:  # patch after the eager pass: the RoPE patch is module-wide
+                counts = patch_model(fused)
+                assert counts["rmsnorm"] == 2 * cfg.num_hidden_layers + 1
+                assert counts["swiglu_mlp"] == cfg.num_hidden_layers and counts["rope_modules"] == 1
+            lg = m(input_ids=ids, position_ids=pos, **kw).logits
+            lg.float().pow(2).mean().backward()
+            outs.append(lg.detach())
+    finally:
+        from transformers.models.qwen2 import modeling_qwen2 as mq
+
+        f = mq.apply_rotary_pos_emb
+        if getattr(f, "_prl_fused", False):  # leave the module as other tests expect it
+            mq.apply_rotary_pos_emb = f._prl_orig
+    assert (outs[0].float() - outs[1].float()).abs().max() <= 5e-2 * outs[0].float().abs().max()
+    for (n, p), (_, q) in zip(eager.named_parameters(), fused.named_parameters()):
+        err = float((p.grad.float() - q.grad.float()).abs().max())
+        assert err <= 5e-2 * float(p.grad.float().abs().max()) + 1e-6, (n, err)
+
+
+def test_varlen_gqa_native_matches_repeated():
+    """torch's varlen flash attention takes GQA (Hkv < Hq) directly: forward and gradients equal
+    the repeated-k/v form the attention path used before (finetune/attention.py)."""
+    from torch.nn.attention.varlen import varlen_attn
+
+    T, hq, hkv, D = 256, 12, 2, 128
+    g = torch.Generator(device=DEV).manual_seed(0)
+    q, k, v = (torch.randn((T, h, D), generator=g, device=DEV).to(torch.bfloat16) for h in (hq, hkv, hkv))
+    do = torch.randn((T, hq, D), generator=g, device=DEV).to(torch.bfloat16)
+    cu = torch.tensor([0, 100, 256], dtype=torch.int32, device=DEV)
+    grads = []
+    for rep in (False, True):
+        qq, kk, vv = (t.clone().requires_grad_() for t in (q, k, v))
+        kx, vx = (kk.repeat_interleave(hq // hkv, 1), vv.repeat_interleave(hq // hkv, 1)) if rep else (kk, vv)
+        out = varlen_attn(qq, kx, vx, cu, cu, 156, 156, is_causal=True)
+        out.backward(do)
+        grads.append((out.detach(), qq.grad, kk.grad, vv.grad))
+    assert torch.equal(grads[0][0], grads[1][0]) and torch.equal(grads[0][1], grads[1][1])
+    for a, b in zip(grads[0][2:], grads[1][2:]):  # dk / dv: group sums in a different order
+        assert float((a.float() - b.float()).abs().max()) <= 2e-2 * float(b.float().abs().max())

@@ -78,18 +78,14 @@ def mode_loss(a):
 
 def mode_trainer(a):
     from aten_rl_step import aten_loss_head
-    from pipelinerl_amd.finetune.attention import packed_kwargs, register
+    from pipelinerl_amd.finetune.attention import packed_kwargs
     from pipelinerl_amd.finetune.optim import get_optimizer
     from pipelinerl_amd.finetune.rl import rl_step
-    from transformers import AutoModelForCausalLM, Qwen2Config
+
+    from pipelinerl_amd.trainer_probe import qwen2_model
 
     shapes = QWEN[a.model]
-    cfg_m = Qwen2Config(max_position_embeddings=32768, rope_theta=1e6, rms_norm_eps=1e-6, **shapes)
-    torch.manual_seed(0)
-    model = AutoModelForCausalLM.from_config(cfg_m, dtype=torch.bfloat16, attn_implementation=register()).cuda()
-    if a.grad_ckpt:
-        model.gradient_checkpointing_enable(gradient_checkpointing_kwargs={"use_reentrant": False})
-    model.train()
+    model = qwen2_model(a.model, torch.device("cuda"), a.grad_ckpt, fused_ops=not a.eager_ops)
     opt = get_optimizer("adamw_torch", model, 1e-6, 0.01)
     batch = packed_batch(a.tokens, a.seq, a.prompt, shapes["vocab_size"], "cuda")
     out = {}
@@ -118,7 +114,8 @@ def mode_trainer(a):
         opt.zero_grad(set_to_none=True)
         torch.cuda.empty_cache()
     print(json.dumps({"mode": "trainer", "model": f"Qwen2.5-{a.model} shapes (random init)", "T": a.tokens,
-                      "seq": a.seq, "grad_ckpt": a.grad_ckpt, "results": out}), flush=True)
+                      "seq": a.seq, "grad_ckpt": a.grad_ckpt, "fused_model_ops": not a.eager_ops,
+                      "results": out}), flush=True)
 
 
 if __name__ == "__main__":
@@ -133,6 +130,7 @@ if __name__ == "__main__":
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--loss", default="fused,aten")
     ap.add_argument("--grad-ckpt", action="store_true")
+    ap.add_argument("--eager-ops", action="store_true", help="HF eager RMSNorm / SwiGLU / RoPE (no model_ops patch)")
     ap.add_argument("--chunk", type=int, default=16384, help="lm_head_chunk_rows for --loss fused_head")
     a = ap.parse_args()
     mode_loss(a) if a.mode == "loss" else mode_trainer(a)
