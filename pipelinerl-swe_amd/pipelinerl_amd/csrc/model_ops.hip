@@ -157,12 +157,33 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd(const uint16_t* __restrict__ 
     partial[(int64_t)blockIdx.x * H + i] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
 }
 
-__global__ __launch_bounds__(256) void rmsnorm_dw_finalize(const float* __restrict__ partial, int nblocks, int H,
-                                                           uint16_t* __restrict__ dw) {
+// dw = sum over the bwd kernel's block partials, deterministic, two levels:
+// stage 1: block (column tile of 64, slice s) -> 4 waves x (rows of the slice) -> LDS fold;
+// stage 2: one thread per column folds the slices in order.
+constexpr int kDwSlices = 32;
+__global__ __launch_bounds__(256) void rmsnorm_dw_stage1(const float* __restrict__ partial, int nblocks, int H,
+                                                         float* __restrict__ mid) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + lane;
+  const int per = (nblocks + kDwSlices - 1) / kDwSlices;
+  const int b0 = blockIdx.y * per, b1 = b0 + per < nblocks ? b0 + per : nblocks;
+  float s = 0.f;
+  if (col < H) {
+#pragma unroll 8
+    for (int b = b0 + wid; b < b1; b += 4) s += partial[(int64_t)b * H + col];
+  }
+  red[wid][lane] = s;
+  __syncthreads();
+  if (wid == 0 && col < H) mid[(int64_t)blockIdx.y * H + col] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+}
+
+__global__ __launch_bounds__(256) void rmsnorm_dw_stage2(const float* __restrict__ mid, int H, uint16_t* __restrict__ dw) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= H) return;
   float s = 0.f;
-  for (int b = 0; b < nblocks; ++b) s += partial[(int64_t)b * H + i];
+#pragma unroll
+  for (int k = 0; k < kDwSlices; ++k) s += mid[(int64_t)k * H + i];
   dw[i] = (uint16_t)rne(s);
 }
 
@@ -303,7 +324,7 @@ int ew_grid(int64_t n8) {
   const int64_t g = (n8 + 255) / 256;
   return (int)(g < 4096 ? (g > 0 ? g : 1) : 4096);
 }
-constexpr int kNormBlocks = 512;
+constexpr int kNormBlocks = 2048;  // rmsnorm backward blocks (4 waves each): enough waves in flight
 
 }  // namespace prl_ops
 
@@ -313,7 +334,7 @@ extern "C" {
 
 int prl_rmsnorm_workspace_bytes(int64_t H, size_t* bytes) {
   if (!bytes || H <= 0) return PRL_E_INVALID;
-  *bytes = sizeof(float) * (size_t)kNormBlocks * (size_t)H;
+  *bytes = sizeof(float) * (size_t)(kNormBlocks + kDwSlices) * (size_t)H;
   return PRL_OK;
 }
 
@@ -333,7 +354,7 @@ int prl_rmsnorm_backward(const void* dy, const void* x, const void* w, const flo
                          void* workspace, size_t workspace_bytes, int64_t rows, int64_t H, void* stream) {
   if (!dy || !x || !w || !rstd || !dx || !dw || !workspace || rows < 0 || H <= 0) return PRL_E_INVALID;
   if (H % 8 || H > 64 * 8 * kMaxNVBwd || !a16(x) || !a16(w) || !a16(dy) || !a16(dx)) return PRL_E_UNSUPPORTED;
-  if (workspace_bytes < sizeof(float) * (size_t)kNormBlocks * (size_t)H) return PRL_E_WORKSPACE;
+  if (workspace_bytes < sizeof(float) * (size_t)(kNormBlocks + kDwSlices) * (size_t)H) return PRL_E_WORKSPACE;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int nv = (int)((H / 8 + 63) / 64);
   const int64_t g = (rows + 3) / 4;
@@ -342,8 +363,11 @@ int prl_rmsnorm_backward(const void* dy, const void* x, const void* w, const flo
   hipError_t e = norm_bwd_table(nv, dy, x, w, rstd, dx, partial, rows, (int)H, grid, s,
                                 std::make_integer_sequence<int, kMaxNVBwd>{});
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(rmsnorm_dw_finalize, dim3((unsigned)((H + 255) / 256)), dim3(256), 0, s, partial, grid,
-                     (int)H, (uint16_t*)dw);
+  float* mid = partial + (size_t)kNormBlocks * (size_t)H;
+  hipLaunchKernelGGL(rmsnorm_dw_stage1, dim3((unsigned)((H + 63) / 64), kDwSlices), dim3(256), 0, s, partial, grid,
+                     (int)H, mid);
+  hipLaunchKernelGGL(rmsnorm_dw_stage2, dim3((unsigned)((H + 255) / 256)), dim3(256), 0, s, mid, (int)H,
+                     (uint16_t*)dw);
   return (int)hipGetLastError();
 }
 
