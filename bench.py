@@ -18,8 +18,9 @@ weight broadcast (WeightUpdateManager -> WorkerExtension, rank 0 -> ranks 1..N-1
 
 After that, at every N, the whole optimizer step the loss head sits in is measured and reported
 under "trainer_step" (pipelinerl_amd/trainer_probe.py): Qwen2.5-1.5B shapes (random init, bf16),
-4 packed micro-batches of 16 384 tokens per rank (varlen attention, fused loss head, backward),
-the bucketed RCCL gradient all-reduce overlapped with the last backward, clip, fused AdamW.
+2 packed micro-batches of 65 536 tokens per rank (C2's micro-batch; varlen attention, fused
+RMSNorm / SwiGLU / RoPE, label-row lm_head + fused loss head, backward), the bucketed RCCL
+gradient all-reduce overlapped with the last backward, clip, fused AdamW.
 
 Prints ONE JSON line (rank 0).  roofline.achieved = algorithmic bytes per launch
 (T*V*2 read + T*V*2 dlogits write + 37*T side data) / the average duration
@@ -197,7 +198,8 @@ def main():
 
         logits = fields = None
         torch.cuda.empty_cache()
-        trainer = trainer_step_probe("1.5b", tokens=16384, micro_batches=4, steps=3, warmup=1, device=dev)
+        trainer = trainer_step_probe("1.5b", tokens=T, micro_batches=2, steps=2, warmup=1, device=dev,
+                                     fused_head=True)
 
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
