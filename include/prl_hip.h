@@ -230,6 +230,23 @@ int prl_rope_backward(const void* dq_out, const void* dk_out, const void* cos, c
                       void* dq, void* dk, int64_t tokens, int32_t hq, int32_t hkv, int32_t d,
                       void* stream);
 
+/* ---- Flash-attention backward for packed causal attention (csrc/attn_bwd.hip), bf16,
+ * head_dim 128, heads of q / k / v equal (GQA callers repeat k / v).  Tensors [tokens, heads,
+ * 128] token-major.  lse: the forward's log-sum-exp in torch's varlen layout
+ * [nseq][heads][lse_len] (sequence b's row starts at token cu_seqlens[b]; lse_len >= its length).
+ * Replaces the backward of torch's varlen flash attention used by the trainer's packed
+ * attention (finetune/attention.py; the reference's flash-attn varlen, finetune_loop.py:381). */
+/* lse2 = lse * log2(e), delta = rowsum(out * dout), both fp32 [heads][tokens]. */
+int prl_attn_bwd_preprocess(const void* out, const void* dout, const float* lse,
+                            const int32_t* cu_seqlens, int32_t nseq, int64_t lse_len, float* lse2,
+                            float* delta, int64_t tokens, int32_t heads, int32_t head_dim, void* stream);
+/* kv_items / q_items: device int32 triplets (seq_start, seq_end, block_start) covering every
+ * sequence in 128-key / 128-query blocks.  Writes dq, dk, dv (bf16). */
+int prl_attn_bwd(const void* q, const void* k, const void* v, const void* dout, const float* lse2,
+                 const float* delta, const int32_t* kv_items, int32_t n_kv_items, const int32_t* q_items,
+                 int32_t n_q_items, void* dq, void* dk, void* dv, int64_t tokens, int32_t heads,
+                 int32_t head_dim, float scale, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -23,7 +23,7 @@ CSRC = PKG / "csrc"
 LIB = PKG / "libprl_hip.so"
 COMM_LIB = PKG / "libprl_comm.so"
 ARCH = "gfx950"
-SOURCES = ["grpo_loss.hip", "flat_pack.hip", "model_ops.hip"]
+SOURCES = ["grpo_loss.hip", "flat_pack.hip", "model_ops.hip", "attn_bwd.hip"]
 
 
 def hipcc() -> str:

@@ -1,0 +1,290 @@
+// Flash-attention backward for the trainer's packed (varlen) causal attention, gfx950, bf16,
+// head dim 128.  Replaces the backward of torch's varlen flash attention (AOTriton on ROCm,
+// ~150 TF at 8 x 2048 on MI355X) behind finetune/attention.py.
+//
+// Given Q, K, V, dO [T, H, 128] (token-major, packed sequences [cu[i], cu[i+1])), the forward's
+// log-sum-exp L (natural log of sum_j exp(s * S_ij)) and delta_i = sum_d dO_id O_id:
+//   P  = exp(s S - L),  dS = P (dP - delta),  S = Q K^T, dP = dO V^T
+//   dV = P^T dO,  dK = s dS^T Q,  dQ = s dS K
+// Two kernels, no atomics, no score matrix in HBM:
+//   attn_bwd_dkdv  one workgroup = 128 keys of one (sequence, head); each wave owns 32 keys and
+//                  keeps dK^T, dV^T (128 x 32 fp32 each) in accumulators while the workgroup
+//                  sweeps the causal query tiles (32 rows, staged in LDS row-major + transposed)
+//   attn_bwd_dq    one workgroup = 128 queries; each wave owns 32 queries (dQ^T in accumulators)
+//                  and sweeps the causal key tiles
+// MFMA: v_mfma_f32_32x32x16_bf16.  Lane layouts (probed, tools/mfma_layout_probe.hip):
+//   A[m][k]: lane l holds A[l%32][8(l/32)+i];  B[k][n]: lane l holds B[8(l/32)+i][l%32];
+//   C[m][n]: lane l, reg r holds C[8(r/4)+4(l/32)+(r%4)][l%32].
+// S and dP are computed with the KEY (dK/dV kernel) or the QUERY (dQ kernel) on the lane, so
+// their accumulators are the B operands of the next product as they stand: the reduction index
+// of that product is taken in the permuted order sigma(8h+i) = 8(i/4) + 4h + (i%4) (+16 for the
+// second half), and the A operand is read from the transposed LDS image in the same order.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "prl_hip.h"
+
+namespace prl_attn {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int D = 128;
+constexpr int TILE = 32;
+
+__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ bf16x8 ld8(const __bf16* p) { return __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(p)); }
+__device__ __forceinline__ bf16x8 zero8() { return __builtin_bit_cast(bf16x8, u32x4{0, 0, 0, 0}); }
+// two 4-element runs -> one A fragment (sigma order)
+__device__ __forceinline__ bf16x8 ld4x2(const __bf16* p0, const __bf16* p1) {
+  const u32x2 a = *reinterpret_cast<const u32x2*>(p0), b = *reinterpret_cast<const u32x2*>(p1);
+  return __builtin_bit_cast(bf16x8, u32x4{a[0], a[1], b[0], b[1]});
+}
+__device__ __forceinline__ void st4(__bf16* p, float a, float b, float c, float d) {
+  bf16x4 v = {(__bf16)a, (__bf16)b, (__bf16)c, (__bf16)d};
+  *reinterpret_cast<u32x2*>(p) = __builtin_bit_cast(u32x2, v);
+}
+
+// Stage a 32-row tile of X[T, H, D] (rows r0.., head h) into LDS: row-major [32][128] and
+// transposed [128][32]; rows >= r1 are zero.  256 threads, 2 chunks of 8 elements each.
+template <bool TRANS>
+__device__ __forceinline__ void stage_tile(const __bf16* __restrict__ X, int64_t rs, int h, int r0, int r1,
+                                           __bf16* __restrict__ rowm, __bf16* __restrict__ trans, int tid) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int c = tid + 256 * j;
+    const int r = c >> 4, d8 = (c & 15) * 8;
+    const int t = r0 + r;
+    const bf16x8 x = t < r1 ? ld8(X + (int64_t)t * rs + h * D + d8) : zero8();
+    *reinterpret_cast<u32x4*>(rowm + r * D + d8) = __builtin_bit_cast(u32x4, x);
+    if (TRANS) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) trans[(d8 + i) * TILE + r] = x[i];
+    }
+  }
+}
+
+// items: int32 triplets (seq_start, seq_end, block_start), block = 128 keys (dkdv) / queries (dq)
+__global__ __launch_bounds__(256) void attn_bwd_dkdv(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
+                                                     const __bf16* __restrict__ v, const __bf16* __restrict__ dout,
+                                                     const float* __restrict__ lse2, const float* __restrict__ delta,
+                                                     const int32_t* __restrict__ items, __bf16* __restrict__ dk,
+                                                     __bf16* __restrict__ dv, int64_t T, int H, float c2, float scale) {
+  __shared__ __attribute__((aligned(16))) __bf16 sQ[TILE * D], sdO[TILE * D], sQt[D * TILE], sdOt[D * TILE];
+  __shared__ float sL[TILE], sDl[TILE];
+  const int it = blockIdx.x, h = blockIdx.y, tid = threadIdx.x;
+  const int s1 = items[3 * it + 1], kb = items[3 * it + 2];
+  const int lane = tid & 63, w = tid >> 6, hi = lane >> 5, l32 = lane & 31;
+  const int64_t rs = (int64_t)H * D;
+  const int kw = kb + 32 * w;
+  const int key = kw + l32;
+  const bool kval = key < s1;
+  bf16x8 kf[8], vf[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    kf[c] = kval ? ld8(k + (int64_t)key * rs + h * D + 16 * c + 8 * hi) : zero8();
+    vf[c] = kval ? ld8(v + (int64_t)key * rs + h * D + 16 * c + 8 * hi) : zero8();
+  }
+  f32x16 dKt[4], dVt[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    dKt[i] = f32x16{};
+    dVt[i] = f32x16{};
+  }
+  for (int q0 = kb; q0 < s1; q0 += TILE) {
+    __syncthreads();
+    stage_tile<true>(q, rs, h, q0, s1, sQ, sQt, tid);
+    stage_tile<true>(dout, rs, h, q0, s1, sdO, sdOt, tid);
+    if (tid < TILE) {
+      const int t = q0 + tid;
+      sL[tid] = t < s1 ? lse2[(int64_t)h * T + t] : 0.f;
+      sDl[tid] = t < s1 ? delta[(int64_t)h * T + t] : 0.f;
+    }
+    __syncthreads();
+    if (kw >= s1 || kw > q0 + TILE - 1) continue;  // every key of this wave is after every query
+    f32x16 S = f32x16{}, dP = f32x16{};
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      S = mfma(ld8(sQ + l32 * D + 16 * c + 8 * hi), kf[c], S);
+      dP = mfma(ld8(sdO + l32 * D + 16 * c + 8 * hi), vf[c], dP);
+    }
+    bf16x8 pb[2], sb[2];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int qi = 8 * (r >> 2) + 4 * hi + (r & 3);
+      const int t = q0 + qi;
+      const bool ok = kval && key <= t && t < s1;
+      const float p = ok ? exp2f(S[r] * c2 - sL[qi]) : 0.f;
+      pb[r >> 3][r & 7] = (__bf16)p;
+      sb[r >> 3][r & 7] = (__bf16)(p * (dP[r] - sDl[qi]));
+    }
+#pragma unroll
+    for (int dc = 0; dc < 4; ++dc) {
+      const int d = 32 * dc + l32;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int o0 = d * TILE + 16 * ks + 4 * hi, o1 = o0 + 8;
+        dVt[dc] = mfma(ld4x2(sdOt + o0, sdOt + o1), pb[ks], dVt[dc]);
+        dKt[dc] = mfma(ld4x2(sQt + o0, sQt + o1), sb[ks], dKt[dc]);
+      }
+    }
+  }
+  if (!kval) return;
+  __bf16* dkr = dk + (int64_t)key * rs + h * D;
+  __bf16* dvr = dv + (int64_t)key * rs + h * D;
+#pragma unroll
+  for (int dc = 0; dc < 4; ++dc)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d0 = 32 * dc + 8 * g + 4 * hi;
+      st4(dkr + d0, scale * dKt[dc][4 * g], scale * dKt[dc][4 * g + 1], scale * dKt[dc][4 * g + 2],
+          scale * dKt[dc][4 * g + 3]);
+      st4(dvr + d0, dVt[dc][4 * g], dVt[dc][4 * g + 1], dVt[dc][4 * g + 2], dVt[dc][4 * g + 3]);
+    }
+}
+
+__global__ __launch_bounds__(256) void attn_bwd_dq(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
+                                                   const __bf16* __restrict__ v, const __bf16* __restrict__ dout,
+                                                   const float* __restrict__ lse2, const float* __restrict__ delta,
+                                                   const int32_t* __restrict__ items, __bf16* __restrict__ dq,
+                                                   int64_t T, int H, float c2, float scale) {
+  __shared__ __attribute__((aligned(16))) __bf16 sK[TILE * D], sV[TILE * D], sKt[D * TILE];
+  const int it = blockIdx.x, h = blockIdx.y, tid = threadIdx.x;
+  const int s0 = items[3 * it], s1 = items[3 * it + 1], qb = items[3 * it + 2];
+  const int lane = tid & 63, w = tid >> 6, hi = lane >> 5, l32 = lane & 31;
+  const int64_t rs = (int64_t)H * D;
+  const int qw = qb + 32 * w;
+  const int qq = qw + l32;
+  const bool qval = qq < s1;
+  bf16x8 qf[8], of[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    qf[c] = qval ? ld8(q + (int64_t)qq * rs + h * D + 16 * c + 8 * hi) : zero8();
+    of[c] = qval ? ld8(dout + (int64_t)qq * rs + h * D + 16 * c + 8 * hi) : zero8();
+  }
+  const float lq = qval ? lse2[(int64_t)h * T + qq] : 0.f;
+  const float dq_delta = qval ? delta[(int64_t)h * T + qq] : 0.f;
+  f32x16 dQt[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) dQt[i] = f32x16{};
+  const int kend = (qb + 128 < s1 ? qb + 128 : s1);  // causal: keys <= the block's last query
+  for (int k0 = s0; k0 < kend; k0 += TILE) {
+    __syncthreads();
+    stage_tile<true>(k, rs, h, k0, s1, sK, sKt, tid);
+    stage_tile<false>(v, rs, h, k0, s1, sV, nullptr, tid);
+    __syncthreads();
+    if (qw >= s1 || k0 > qw + TILE - 1) continue;  // every key of the tile is after every query of this wave
+    f32x16 St = f32x16{}, dPt = f32x16{};
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      St = mfma(ld8(sK + l32 * D + 16 * c + 8 * hi), qf[c], St);
+      dPt = mfma(ld8(sV + l32 * D + 16 * c + 8 * hi), of[c], dPt);
+    }
+    bf16x8 sb[2];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int kj = k0 + 8 * (r >> 2) + 4 * hi + (r & 3);
+      const bool ok = qval && kj <= qq && kj < s1;
+      const float p = ok ? exp2f(St[r] * c2 - lq) : 0.f;
+      sb[r >> 3][r & 7] = (__bf16)(p * (dPt[r] - dq_delta));
+    }
+#pragma unroll
+    for (int dc = 0; dc < 4; ++dc) {
+      const int d = 32 * dc + l32;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int o0 = d * TILE + 16 * ks + 4 * hi, o1 = o0 + 8;
+        dQt[dc] = mfma(ld4x2(sKt + o0, sKt + o1), sb[ks], dQt[dc]);
+      }
+    }
+  }
+  if (!qval) return;
+  __bf16* dqr = dq + (int64_t)qq * rs + h * D;
+#pragma unroll
+  for (int dc = 0; dc < 4; ++dc)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d0 = 32 * dc + 8 * g + 4 * hi;
+      st4(dqr + d0, scale * dQt[dc][4 * g], scale * dQt[dc][4 * g + 1], scale * dQt[dc][4 * g + 2],
+          scale * dQt[dc][4 * g + 3]);
+    }
+}
+
+// delta[h][t] = sum_d O dO (fp32);  lse2[h][t] = L * log2(e), with L in torch's varlen layout
+// [nseq][H][lse_len] (row of sequence b starting at token cu[b]).  One wave per (t, h).
+__global__ __launch_bounds__(256) void attn_bwd_pre(const __bf16* __restrict__ out, const __bf16* __restrict__ dout,
+                                                    const float* __restrict__ lse, const int32_t* __restrict__ cu,
+                                                    int nseq, int64_t lse_len, float* __restrict__ lse2,
+                                                    float* __restrict__ delta, int64_t T, int H) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= T * H) return;
+  const int64_t t = row / H;
+  const int h = (int)(row - t * H);
+  const __bf16* o = out + row * D;
+  const __bf16* g = dout + row * D;
+  float s = (float)o[2 * lane] * (float)g[2 * lane] + (float)o[2 * lane + 1] * (float)g[2 * lane + 1];
+#pragma unroll
+  for (int m = 32; m > 0; m >>= 1) s += __shfl_xor(s, m, 64);
+  if (lane == 0) {
+    int lo = 0, hi = nseq - 1;  // last b with cu[b] <= t
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (cu[mid] <= t) lo = mid; else hi = mid - 1;
+    }
+    const int64_t off = t - cu[lo];
+    delta[(int64_t)h * T + t] = s;
+    lse2[(int64_t)h * T + t] = off < lse_len ? lse[((int64_t)lo * H + h) * lse_len + off] * 1.4426950408889634f : 0.f;
+  }
+}
+
+}  // namespace prl_attn
+
+using namespace prl_attn;
+
+extern "C" {
+
+int prl_attn_bwd_preprocess(const void* out, const void* dout, const float* lse, const int32_t* cu_seqlens,
+                            int32_t nseq, int64_t lse_len, float* lse2, float* delta, int64_t tokens, int32_t heads,
+                            int32_t head_dim, void* stream) {
+  if (!out || !dout || !lse || !cu_seqlens || !lse2 || !delta || tokens < 0 || heads <= 0 || nseq <= 0 ||
+      lse_len <= 0)
+    return PRL_E_INVALID;
+  if (head_dim != D) return PRL_E_UNSUPPORTED;
+  if (tokens == 0) return PRL_OK;
+  const int64_t rows = tokens * heads;
+  hipLaunchKernelGGL(attn_bwd_pre, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     (const __bf16*)out, (const __bf16*)dout, lse, cu_seqlens, (int)nseq, lse_len, lse2, delta, tokens,
+                     (int)heads);
+  return (int)hipGetLastError();
+}
+
+int prl_attn_bwd(const void* q, const void* k, const void* v, const void* dout, const float* lse2, const float* delta,
+                 const int32_t* kv_items, int32_t n_kv_items, const int32_t* q_items, int32_t n_q_items, void* dq,
+                 void* dk, void* dv, int64_t tokens, int32_t heads, int32_t head_dim, float scale, void* stream) {
+  if (!q || !k || !v || !dout || !lse2 || !delta || !dq || !dk || !dv || tokens < 0 || heads <= 0 ||
+      n_kv_items < 0 || n_q_items < 0 || (n_kv_items && !kv_items) || (n_q_items && !q_items))
+    return PRL_E_INVALID;
+  if (head_dim != D) return PRL_E_UNSUPPORTED;
+  if (heads > 65535) return PRL_E_UNSUPPORTED;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const float c2 = scale * 1.4426950408889634f;
+  if (n_kv_items)
+    hipLaunchKernelGGL(attn_bwd_dkdv, dim3((unsigned)n_kv_items, (unsigned)heads), dim3(256), 0, s,
+                       (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, (const __bf16*)dout, lse2, delta,
+                       kv_items, (__bf16*)dk, (__bf16*)dv, tokens, (int)heads, c2, scale);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  if (n_q_items)
+    hipLaunchKernelGGL(attn_bwd_dq, dim3((unsigned)n_q_items, (unsigned)heads), dim3(256), 0, s, (const __bf16*)q,
+                       (const __bf16*)k, (const __bf16*)v, (const __bf16*)dout, lse2, delta, q_items, (__bf16*)dq,
+                       tokens, (int)heads, c2, scale);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

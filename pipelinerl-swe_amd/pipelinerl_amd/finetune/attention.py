@@ -7,12 +7,14 @@ to the model at rl/__init__.py:188-189).  This registers an HF attention impleme
 (``torch.nn.attention.varlen.varlen_attn``), given cumulative sequence offsets computed ONCE
 per micro-batch on the host (``cu_seq_lens_q/k``, ``max_length_q/k`` — the FlashAttention
 kwargs HF propagates to every layer).  If varlen is unavailable for the inputs it runs causal
-SDPA per sequence (same result, no T x T mask either way).
+SDPA per sequence (same result, no T x T mask either way).  PRL_ATTN_BWD=hip selects the build's HIP
+flash-attention backward (csrc/attn_bwd.hip) for bf16, head dim 128.
 """
 
 from __future__ import annotations
 
 import logging
+import os
 
 import torch
 import torch.nn.functional as F
@@ -22,6 +24,67 @@ logger = logging.getLogger(__name__)
 PRL_VARLEN = "prl_varlen"
 _registered = False
 _varlen_ok: bool | None = None
+_ITEMS: dict[tuple, tuple] = {}
+BLOCK = 128  # keys / queries per workgroup of the HIP backward (csrc/attn_bwd.hip)
+
+
+def _items(bounds: list[int], device) -> tuple:
+    """(kv_items, q_items) int32 [n, 3] device tensors: (seq_start, seq_end, block_start) per
+    128-row block of every sequence (the same list serves both kernels)."""
+    key = (tuple(bounds), str(device))
+    hit = _ITEMS.get(key)
+    if hit is None:
+        rows = [(a, b, x) for a, b in zip(bounds[:-1], bounds[1:]) for x in range(a, b, BLOCK)]
+        t = torch.tensor(rows if rows else [(0, 0, 0)], dtype=torch.int32).to(device)
+        hit = (t, len(rows))
+        if len(_ITEMS) > 64:
+            _ITEMS.clear()
+        _ITEMS[key] = hit
+    return hit
+
+
+class PackedCausalAttention(torch.autograd.Function):
+    """torch's varlen flash-attention forward (keeps its log-sum-exp), HIP backward
+    (prl_attn_bwd: ~2x the MI355X throughput of the library backward; tools/attn_backend_probe.py).
+    q, k, v: [T, H, 128] bf16 with equal head counts."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, cu, mx: int, bounds: list[int]):
+        out, lse, _, _, _ = torch.ops.aten._flash_attention_forward(q, k, v, cu, cu, mx, mx, 0.0, True, False)
+        nseq = len(bounds) - 1
+        # torch's varlen log-sum-exp on ROCm: [nseq, H, max_len] (checked: tools/lse_layout_probe.py)
+        if not (lse.dim() == 3 and tuple(lse.shape[:2]) == (nseq, q.shape[1]) and lse.shape[2] >= mx
+                and lse.is_contiguous() and lse.dtype == torch.float32 and cu.numel() == nseq + 1):
+            raise RuntimeError(f"unexpected flash-attention log-sum-exp layout {tuple(lse.shape)}")
+        ctx.save_for_backward(q, k, v, out, lse, cu)
+        ctx.bounds = bounds
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        from .. import _native
+
+        q, k, v, out, lse, cu = ctx.saved_tensors
+        dout = dout.contiguous()
+        T, H, D = q.shape
+        lib = _native.load()
+        st = torch.cuda.current_stream(q.device).cuda_stream
+        lse2 = torch.empty((H, T), dtype=torch.float32, device=q.device)
+        delta = torch.empty((H, T), dtype=torch.float32, device=q.device)
+        _native.check(lib.prl_attn_bwd_preprocess(out.data_ptr(), dout.data_ptr(), lse.data_ptr(), cu.data_ptr(),
+                                                  lse.shape[0], lse.shape[2], lse2.data_ptr(), delta.data_ptr(), T, H,
+                                                  D, st), "prl_attn_bwd_preprocess")
+        items, n = _items(ctx.bounds, q.device)
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        _native.check(lib.prl_attn_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), dout.data_ptr(), lse2.data_ptr(),
+                                       delta.data_ptr(), items.data_ptr(), n, items.data_ptr(), n, dq.data_ptr(),
+                                       dk.data_ptr(), dv.data_ptr(), T, H, D, D ** -0.5, st), "prl_attn_bwd")
+        return dq, dk, dv, None, None, None
+
+
+def _hip_backward_ok(q, k) -> bool:
+    return (q.dtype == torch.bfloat16 and q.shape[-1] == 128 and q.shape == k.shape
+            and os.environ.get("PRL_ATTN_BWD", "torch") == "hip")
 
 
 def varlen_attention_forward(module, query, key, value, attention_mask, scaling=None, dropout=0.0, **kwargs):
@@ -49,9 +112,14 @@ def varlen_attention_forward(module, query, key, value, attention_mask, scaling=
     global _varlen_ok
     if (scaling is None or abs(scaling - default_scale) < 1e-12) and q.is_cuda and _varlen_ok is not False:
         try:
-            from torch.nn.attention.varlen import varlen_attn
+            q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+            bounds = kwargs.get("cu_seq_lens_host")
+            if bounds is not None and _hip_backward_ok(q, k):
+                out = PackedCausalAttention.apply(q, k, v, cu, mx, list(bounds))
+            else:
+                from torch.nn.attention.varlen import varlen_attn
 
-            out = varlen_attn(q.contiguous(), k.contiguous(), v.contiguous(), cu, cu, mx, mx, is_causal=True)
+                out = varlen_attn(q, k, v, cu, cu, mx, mx, is_causal=True)
             _varlen_ok = True
             return out.unsqueeze(0), None
         except (RuntimeError, NotImplementedError) as e:

@@ -5,8 +5,13 @@ T = 16384 packed as 8 x 2048 (and 2 x 8192).  Prints one JSON line per case."""
 import json
 import time
 
+import sys
+from pathlib import Path
+
 import torch
 import torch.nn.functional as F
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "pipelinerl-swe_amd"))
 from torch.nn.attention.varlen import varlen_attn
 
 
@@ -45,12 +50,19 @@ def case(T, seq, hq=12, hkv=2, D=128):
         o = F.scaled_dot_product_attention(qb, kb, vb, is_causal=True, enable_gqa=True)
         o.backward(do.view(B, seq, hq, D).transpose(1, 2))
 
+    def hip_bwd():
+        from pipelinerl_amd.finetune.attention import PackedCausalAttention
+
+        PackedCausalAttention.apply(q, k.repeat_interleave(rep, 1), v.repeat_interleave(rep, 1), cu, seq,
+                                    list(range(0, T + 1, seq))).backward(do)
+
     def fwd_only():
         with torch.no_grad():
             varlen_attn(q, k, v, cu, cu, seq, seq, is_causal=True)
 
-    order = (("varlen_repeated_kv", repeated), ("varlen_gqa_native", native), ("sdpa_batched", batched),
-             ("varlen_fwd_only", fwd_only), ("varlen_repeated_kv_again", repeated), ("varlen_gqa_native_again", native))
+    order = (("varlen_repeated_kv", repeated), ("prl_hip_backward", hip_bwd), ("varlen_gqa_native", native),
+             ("sdpa_batched", batched), ("varlen_fwd_only", fwd_only), ("prl_hip_backward_again", hip_bwd),
+             ("varlen_repeated_kv_again", repeated))
     for name, fn in order:
         try:
             ms = bench(fn)
