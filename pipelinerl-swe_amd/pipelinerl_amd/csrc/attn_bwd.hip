@@ -9,7 +9,9 @@
 // Two kernels, no atomics, no score matrix in HBM:
 //   attn_bwd_dkdv  one workgroup = 128 keys of one (sequence, head); each wave owns 32 keys and
 //                  keeps dK^T, dV^T (128 x 32 fp32 each) in accumulators while the workgroup
-//                  sweeps the causal query tiles (32 rows, staged in LDS row-major + transposed)
+//                  sweeps the causal query tiles (32 rows, one swizzled LDS image per tile, read
+//                  by rows and with ds_read_b64_tr_b16; the next tile is register-staged
+//                  behind the current tile's MFMAs)
 //   attn_bwd_dq    one workgroup = 128 queries; each wave owns 32 queries (dQ^T in accumulators)
 //                  and sweeps the causal key tiles
 // MFMA: v_mfma_f32_32x32x16_bf16.  Lane layouts (probed, tools/mfma_layout_probe.hip):
@@ -18,7 +20,7 @@
 // S and dP are computed with the KEY (dK/dV kernel) or the QUERY (dQ kernel) on the lane, so
 // their accumulators are the B operands of the next product as they stand: the reduction index
 // of that product is taken in the permuted order sigma(8h+i) = 8(i/4) + 4h + (i%4) (+16 for the
-// second half), and the A operand is read from the transposed LDS image in the same order.
+// second half), and the A operand is read transposed (ds_read_b64_tr_b16) in the same order.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -40,32 +42,57 @@ __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
 }
 __device__ __forceinline__ bf16x8 ld8(const __bf16* p) { return __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(p)); }
 __device__ __forceinline__ bf16x8 zero8() { return __builtin_bit_cast(bf16x8, u32x4{0, 0, 0, 0}); }
-// two 4-element runs -> one A fragment (sigma order)
-__device__ __forceinline__ bf16x8 ld4x2(const __bf16* p0, const __bf16* p1) {
-  const u32x2 a = *reinterpret_cast<const u32x2*>(p0), b = *reinterpret_cast<const u32x2*>(p1);
-  return __builtin_bit_cast(bf16x8, u32x4{a[0], a[1], b[0], b[1]});
-}
 __device__ __forceinline__ void st4(__bf16* p, float a, float b, float c, float d) {
   bf16x4 v = {(__bf16)a, (__bf16)b, (__bf16)c, (__bf16)d};
   *reinterpret_cast<u32x2*>(p) = __builtin_bit_cast(u32x2, v);
 }
 
-// Stage a 32-row tile of X[T, H, D] (rows r0.., head h) into LDS: row-major [32][128] and
-// transposed [128][32]; rows >= r1 are zero.  256 threads, 2 chunks of 8 elements each.
-template <bool TRANS>
-__device__ __forceinline__ void stage_tile(const __bf16* __restrict__ X, int64_t rs, int h, int r0, int r1,
-                                           __bf16* __restrict__ rowm, __bf16* __restrict__ trans, int tid) {
+// LDS tile image: 32 rows x 128 bf16 (256-B rows), 16-B chunks XOR-swizzled so that both the
+// row reads (ds_read_b128, MFMA operands with the row on the lane) and the transposed reads
+// (ds_read_b64_tr_b16, operands that need the tile's columns on the lane) are conflict-free
+// (cdna_hip_programming.md T10, image (b)).  Byte offset of chunk ch (0..15) of row r:
+__device__ __forceinline__ int toff(int r, int ch) { return 256 * r + 16 * (ch ^ (((r & 3) << 2) | ((r >> 2) & 3))); }
+
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+__device__ __forceinline__ bf16x4 tr_read(const char* base, int off) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + off));
+}
+__device__ __forceinline__ bf16x8 row_read(const char* base, int r, int ch) {
+  return __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(base + toff(r, ch)));
+}
+// A operand [m = column d][k = row, sigma order] of a 32x32x16 MFMA from a tile image: d chunk dc
+// (columns 32dc .. 32dc+31), k-step ks (rows 16ks ..): elements 0..3 = rows 16ks+4h+0..3,
+// elements 4..7 = rows 16ks+8+4h+0..3, column 32dc + (lane & 31).  Lane 4q+p of each 16-lane
+// group addresses row R+q, columns d0+4p..+3 (d0 = the group's first column).
+__device__ __forceinline__ bf16x8 tr_operand(const char* base, int lane, int dc, int ks) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int h = g >> 1;
+  const int ch = 4 * dc + 2 * (g & 1) + (p >> 1);
+  const int r0 = 16 * ks + 4 * h + q;
+  const bf16x4 a = tr_read(base, toff(r0, ch) + 8 * (p & 1));
+  const bf16x4 b = tr_read(base, toff(r0 + 8, ch) + 8 * (p & 1));
+  return bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+
+// register staging of a 32-row tile of X[T, H, D] (rows r0.., head h): 2 chunks per thread
+struct Stage {
+  u32x4 x[2];
+};
+__device__ __forceinline__ Stage stage_load(const __bf16* __restrict__ X, int64_t rs, int h, int r0, int r1, int tid) {
+  Stage st;
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int c = tid + 256 * j;
-    const int r = c >> 4, d8 = (c & 15) * 8;
-    const int t = r0 + r;
-    const bf16x8 x = t < r1 ? ld8(X + (int64_t)t * rs + h * D + d8) : zero8();
-    *reinterpret_cast<u32x4*>(rowm + r * D + d8) = __builtin_bit_cast(u32x4, x);
-    if (TRANS) {
+    const int t = r0 + (c >> 4);
+    st.x[j] = t < r1 ? *reinterpret_cast<const u32x4*>(X + (int64_t)t * rs + h * D + (c & 15) * 8) : u32x4{0, 0, 0, 0};
+  }
+  return st;
+}
+__device__ __forceinline__ void stage_store(const Stage& st, char* base, int tid) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) trans[(d8 + i) * TILE + r] = x[i];
-    }
+  for (int j = 0; j < 2; ++j) {
+    const int c = tid + 256 * j;
+    *reinterpret_cast<u32x4*>(base + toff(c >> 4, c & 15)) = st.x[j];
   }
 }
 
@@ -75,7 +102,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv(const __bf16* __restrict__ 
                                                      const float* __restrict__ lse2, const float* __restrict__ delta,
                                                      const int32_t* __restrict__ items, __bf16* __restrict__ dk,
                                                      __bf16* __restrict__ dv, int64_t T, int H, float c2, float scale) {
-  __shared__ __attribute__((aligned(16))) __bf16 sQ[TILE * D], sdO[TILE * D], sQt[D * TILE], sdOt[D * TILE];
+  __shared__ __attribute__((aligned(16))) char sQ[TILE * D * 2], sdO[TILE * D * 2];
   __shared__ float sL[TILE], sDl[TILE];
   const int it = blockIdx.x, h = blockIdx.y, tid = threadIdx.x;
   const int s1 = items[3 * it + 1], kb = items[3 * it + 2];
@@ -96,22 +123,36 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv(const __bf16* __restrict__ 
     dKt[i] = f32x16{};
     dVt[i] = f32x16{};
   }
+  Stage nq = stage_load(q, rs, h, kb, s1, tid), nd = stage_load(dout, rs, h, kb, s1, tid);
+  float nl = 0.f, ndl = 0.f;
+  if (tid < TILE && kb + tid < s1) {
+    nl = lse2[(int64_t)h * T + kb + tid];
+    ndl = delta[(int64_t)h * T + kb + tid];
+  }
   for (int q0 = kb; q0 < s1; q0 += TILE) {
-    __syncthreads();
-    stage_tile<true>(q, rs, h, q0, s1, sQ, sQt, tid);
-    stage_tile<true>(dout, rs, h, q0, s1, sdO, sdOt, tid);
+    __syncthreads();  // every wave is done with the previous tile
+    stage_store(nq, sQ, tid);
+    stage_store(nd, sdO, tid);
     if (tid < TILE) {
-      const int t = q0 + tid;
-      sL[tid] = t < s1 ? lse2[(int64_t)h * T + t] : 0.f;
-      sDl[tid] = t < s1 ? delta[(int64_t)h * T + t] : 0.f;
+      sL[tid] = nl;
+      sDl[tid] = ndl;
     }
     __syncthreads();
-    if (kw >= s1 || kw > q0 + TILE - 1) continue;  // every key of this wave is after every query
+    const int qn = q0 + TILE;  // prefetch the next tile behind this tile's MFMAs
+    if (qn < s1) {
+      nq = stage_load(q, rs, h, qn, s1, tid);
+      nd = stage_load(dout, rs, h, qn, s1, tid);
+      if (tid < TILE && qn + tid < s1) {
+        nl = lse2[(int64_t)h * T + qn + tid];
+        ndl = delta[(int64_t)h * T + qn + tid];
+      }
+    }
+    if (kw >= s1 || kw > q0 + TILE - 1) continue;  // wave-uniform: every key of this wave is after every query
     f32x16 S = f32x16{}, dP = f32x16{};
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
-      S = mfma(ld8(sQ + l32 * D + 16 * c + 8 * hi), kf[c], S);
-      dP = mfma(ld8(sdO + l32 * D + 16 * c + 8 * hi), vf[c], dP);
+      S = mfma(row_read(sQ, l32, 2 * c + hi), kf[c], S);
+      dP = mfma(row_read(sdO, l32, 2 * c + hi), vf[c], dP);
     }
     bf16x8 pb[2], sb[2];
 #pragma unroll
@@ -124,15 +165,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv(const __bf16* __restrict__ 
       sb[r >> 3][r & 7] = (__bf16)(p * (dP[r] - sDl[qi]));
     }
 #pragma unroll
-    for (int dc = 0; dc < 4; ++dc) {
-      const int d = 32 * dc + l32;
+    for (int dc = 0; dc < 4; ++dc)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        const int o0 = d * TILE + 16 * ks + 4 * hi, o1 = o0 + 8;
-        dVt[dc] = mfma(ld4x2(sdOt + o0, sdOt + o1), pb[ks], dVt[dc]);
-        dKt[dc] = mfma(ld4x2(sQt + o0, sQt + o1), sb[ks], dKt[dc]);
+        dVt[dc] = mfma(tr_operand(sdO, lane, dc, ks), pb[ks], dVt[dc]);
+        dKt[dc] = mfma(tr_operand(sQ, lane, dc, ks), sb[ks], dKt[dc]);
       }
-    }
   }
   if (!kval) return;
   __bf16* dkr = dk + (int64_t)key * rs + h * D;
@@ -153,7 +191,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq(const __bf16* __restrict__ q,
                                                    const float* __restrict__ lse2, const float* __restrict__ delta,
                                                    const int32_t* __restrict__ items, __bf16* __restrict__ dq,
                                                    int64_t T, int H, float c2, float scale) {
-  __shared__ __attribute__((aligned(16))) __bf16 sK[TILE * D], sV[TILE * D], sKt[D * TILE];
+  __shared__ __attribute__((aligned(16))) char sK[TILE * D * 2], sV[TILE * D * 2];
   const int it = blockIdx.x, h = blockIdx.y, tid = threadIdx.x;
   const int s0 = items[3 * it], s1 = items[3 * it + 1], qb = items[3 * it + 2];
   const int lane = tid & 63, w = tid >> 6, hi = lane >> 5, l32 = lane & 31;
@@ -173,17 +211,22 @@ __global__ __launch_bounds__(256) void attn_bwd_dq(const __bf16* __restrict__ q,
 #pragma unroll
   for (int i = 0; i < 4; ++i) dQt[i] = f32x16{};
   const int kend = (qb + 128 < s1 ? qb + 128 : s1);  // causal: keys <= the block's last query
+  Stage nk = stage_load(k, rs, h, s0, s1, tid), nv = stage_load(v, rs, h, s0, s1, tid);
   for (int k0 = s0; k0 < kend; k0 += TILE) {
     __syncthreads();
-    stage_tile<true>(k, rs, h, k0, s1, sK, sKt, tid);
-    stage_tile<false>(v, rs, h, k0, s1, sV, nullptr, tid);
+    stage_store(nk, sK, tid);
+    stage_store(nv, sV, tid);
     __syncthreads();
-    if (qw >= s1 || k0 > qw + TILE - 1) continue;  // every key of the tile is after every query of this wave
+    if (k0 + TILE < kend) {
+      nk = stage_load(k, rs, h, k0 + TILE, s1, tid);
+      nv = stage_load(v, rs, h, k0 + TILE, s1, tid);
+    }
+    if (qw >= s1 || k0 > qw + TILE - 1) continue;  // wave-uniform: the tile is after every query of this wave
     f32x16 St = f32x16{}, dPt = f32x16{};
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
-      St = mfma(ld8(sK + l32 * D + 16 * c + 8 * hi), qf[c], St);
-      dPt = mfma(ld8(sV + l32 * D + 16 * c + 8 * hi), of[c], dPt);
+      St = mfma(row_read(sK, l32, 2 * c + hi), qf[c], St);
+      dPt = mfma(row_read(sV, l32, 2 * c + hi), of[c], dPt);
     }
     bf16x8 sb[2];
 #pragma unroll
@@ -194,14 +237,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dq(const __bf16* __restrict__ q,
       sb[r >> 3][r & 7] = (__bf16)(p * (dPt[r] - dq_delta));
     }
 #pragma unroll
-    for (int dc = 0; dc < 4; ++dc) {
-      const int d = 32 * dc + l32;
+    for (int dc = 0; dc < 4; ++dc)
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const int o0 = d * TILE + 16 * ks + 4 * hi, o1 = o0 + 8;
-        dQt[dc] = mfma(ld4x2(sKt + o0, sKt + o1), sb[ks], dQt[dc]);
-      }
-    }
+      for (int ks = 0; ks < 2; ++ks) dQt[dc] = mfma(tr_operand(sK, lane, dc, ks), sb[ks], dQt[dc]);
   }
   if (!qval) return;
   __bf16* dqr = dq + (int64_t)qq * rs + h * D;
