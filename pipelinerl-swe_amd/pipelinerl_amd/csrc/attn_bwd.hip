@@ -35,7 +35,8 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int D = 128;
-constexpr int TILE = 32;
+constexpr int TILE = 32;   // rows per MFMA tile
+constexpr int STAGE = 64;  // rows staged per barrier pair (two tiles)
 
 __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
@@ -74,14 +75,15 @@ __device__ __forceinline__ bf16x8 tr_operand(const char* base, int lane, int dc,
   return bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 }
 
-// register staging of a 32-row tile of X[T, H, D] (rows r0.., head h): 2 chunks per thread
+// register staging of a 64-row stage of X[T, H, D] (rows r0.., head h): 4 chunks per thread
+constexpr int kStageChunks = STAGE * 16 / 256;
 struct Stage {
-  u32x4 x[2];
+  u32x4 x[kStageChunks];
 };
 __device__ __forceinline__ Stage stage_load(const __bf16* __restrict__ X, int64_t rs, int h, int r0, int r1, int tid) {
   Stage st;
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
+  for (int j = 0; j < kStageChunks; ++j) {
     const int c = tid + 256 * j;
     const int t = r0 + (c >> 4);
     st.x[j] = t < r1 ? *reinterpret_cast<const u32x4*>(X + (int64_t)t * rs + h * D + (c & 15) * 8) : u32x4{0, 0, 0, 0};
@@ -90,21 +92,20 @@ __device__ __forceinline__ Stage stage_load(const __bf16* __restrict__ X, int64_
 }
 __device__ __forceinline__ void stage_store(const Stage& st, char* base, int tid) {
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
+  for (int j = 0; j < kStageChunks; ++j) {
     const int c = tid + 256 * j;
     *reinterpret_cast<u32x4*>(base + toff(c >> 4, c & 15)) = st.x[j];
   }
 }
 
 // items: int32 triplets (seq_start, seq_end, block_start), block = 128 keys (dkdv) / queries (dq)
-__global__ __launch_bounds__(256) void attn_bwd_dkdv(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
+__device__ __forceinline__ void attn_bwd_dkdv(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
                                                      const __bf16* __restrict__ v, const __bf16* __restrict__ dout,
                                                      const float* __restrict__ lse2, const float* __restrict__ delta,
                                                      const int32_t* __restrict__ items, __bf16* __restrict__ dk,
-                                                     __bf16* __restrict__ dv, int64_t T, int H, float c2, float scale) {
-  __shared__ __attribute__((aligned(16))) char sQ[TILE * D * 2], sdO[TILE * D * 2];
-  __shared__ float sL[TILE], sDl[TILE];
-  const int it = blockIdx.x, h = blockIdx.y, tid = threadIdx.x;
+                                                     __bf16* __restrict__ dv, int64_t T, int H, float c2, float scale,
+                                                     int it, char* sQ, char* sdO, float* sL, float* sDl) {
+  const int h = blockIdx.y, tid = threadIdx.x;
   const int s1 = items[3 * it + 1], kb = items[3 * it + 2];
   const int lane = tid & 63, w = tid >> 6, hi = lane >> 5, l32 = lane & 31;
   const int64_t rs = (int64_t)H * D;
@@ -125,52 +126,60 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv(const __bf16* __restrict__ 
   }
   Stage nq = stage_load(q, rs, h, kb, s1, tid), nd = stage_load(dout, rs, h, kb, s1, tid);
   float nl = 0.f, ndl = 0.f;
-  if (tid < TILE && kb + tid < s1) {
+  if (tid < STAGE && kb + tid < s1) {
     nl = lse2[(int64_t)h * T + kb + tid];
     ndl = delta[(int64_t)h * T + kb + tid];
   }
-  for (int q0 = kb; q0 < s1; q0 += TILE) {
-    __syncthreads();  // every wave is done with the previous tile
+  for (int q00 = kb; q00 < s1; q00 += STAGE) {
+    __syncthreads();  // every wave is done with the previous stage
     stage_store(nq, sQ, tid);
     stage_store(nd, sdO, tid);
-    if (tid < TILE) {
+    if (tid < STAGE) {
       sL[tid] = nl;
       sDl[tid] = ndl;
     }
     __syncthreads();
-    const int qn = q0 + TILE;  // prefetch the next tile behind this tile's MFMAs
+    const int qn = q00 + STAGE;  // prefetch the next stage behind this stage's MFMAs
     if (qn < s1) {
       nq = stage_load(q, rs, h, qn, s1, tid);
       nd = stage_load(dout, rs, h, qn, s1, tid);
-      if (tid < TILE && qn + tid < s1) {
+      if (tid < STAGE && qn + tid < s1) {
         nl = lse2[(int64_t)h * T + qn + tid];
         ndl = delta[(int64_t)h * T + qn + tid];
       }
     }
-    if (kw >= s1 || kw > q0 + TILE - 1) continue;  // wave-uniform: every key of this wave is after every query
-    f32x16 S = f32x16{}, dP = f32x16{};
+#pragma unroll 1
+    for (int half = 0; half < STAGE / TILE; ++half) {
+      const int q0 = q00 + TILE * half;
+      if (kw >= s1 || kw > q0 + TILE - 1 || q0 >= s1) continue;  // wave-uniform
+      const char* tQ = sQ + half * TILE * 256;
+      const char* tdO = sdO + half * TILE * 256;
+      const float* tL = sL + half * TILE;
+      const float* tDl = sDl + half * TILE;
+      f32x16 S = f32x16{}, dP = f32x16{};
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      S = mfma(row_read(sQ, l32, 2 * c + hi), kf[c], S);
-      dP = mfma(row_read(sdO, l32, 2 * c + hi), vf[c], dP);
-    }
-    bf16x8 pb[2], sb[2];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int qi = 8 * (r >> 2) + 4 * hi + (r & 3);
-      const int t = q0 + qi;
-      const bool ok = kval && key <= t && t < s1;
-      const float p = ok ? exp2f(S[r] * c2 - sL[qi]) : 0.f;
-      pb[r >> 3][r & 7] = (__bf16)p;
-      sb[r >> 3][r & 7] = (__bf16)(p * (dP[r] - sDl[qi]));
-    }
-#pragma unroll
-    for (int dc = 0; dc < 4; ++dc)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        dVt[dc] = mfma(tr_operand(sdO, lane, dc, ks), pb[ks], dVt[dc]);
-        dKt[dc] = mfma(tr_operand(sQ, lane, dc, ks), sb[ks], dKt[dc]);
+      for (int c = 0; c < 8; ++c) {
+        S = mfma(row_read(tQ, l32, 2 * c + hi), kf[c], S);
+        dP = mfma(row_read(tdO, l32, 2 * c + hi), vf[c], dP);
       }
+      bf16x8 pb[2], sb[2];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int qi = 8 * (r >> 2) + 4 * hi + (r & 3);
+        const int t = q0 + qi;
+        const bool ok = kval && key <= t && t < s1;
+        const float p = ok ? exp2f(S[r] * c2 - tL[qi]) : 0.f;
+        pb[r >> 3][r & 7] = (__bf16)p;
+        sb[r >> 3][r & 7] = (__bf16)(p * (dP[r] - tDl[qi]));
+      }
+#pragma unroll
+      for (int dc = 0; dc < 4; ++dc)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          dVt[dc] = mfma(tr_operand(tdO, lane, dc, ks), pb[ks], dVt[dc]);
+          dKt[dc] = mfma(tr_operand(tQ, lane, dc, ks), sb[ks], dKt[dc]);
+        }
+    }
   }
   if (!kval) return;
   __bf16* dkr = dk + (int64_t)key * rs + h * D;
@@ -186,13 +195,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv(const __bf16* __restrict__ 
     }
 }
 
-__global__ __launch_bounds__(256) void attn_bwd_dq(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
+__device__ __forceinline__ void attn_bwd_dq(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
                                                    const __bf16* __restrict__ v, const __bf16* __restrict__ dout,
                                                    const float* __restrict__ lse2, const float* __restrict__ delta,
                                                    const int32_t* __restrict__ items, __bf16* __restrict__ dq,
-                                                   int64_t T, int H, float c2, float scale) {
-  __shared__ __attribute__((aligned(16))) char sK[TILE * D * 2], sV[TILE * D * 2];
-  const int it = blockIdx.x, h = blockIdx.y, tid = threadIdx.x;
+                                                   int64_t T, int H, float c2, float scale, int it, char* sK, char* sV) {
+  const int h = blockIdx.y, tid = threadIdx.x;
   const int s0 = items[3 * it], s1 = items[3 * it + 1], qb = items[3 * it + 2];
   const int lane = tid & 63, w = tid >> 6, hi = lane >> 5, l32 = lane & 31;
   const int64_t rs = (int64_t)H * D;
@@ -212,34 +220,40 @@ __global__ __launch_bounds__(256) void attn_bwd_dq(const __bf16* __restrict__ q,
   for (int i = 0; i < 4; ++i) dQt[i] = f32x16{};
   const int kend = (qb + 128 < s1 ? qb + 128 : s1);  // causal: keys <= the block's last query
   Stage nk = stage_load(k, rs, h, s0, s1, tid), nv = stage_load(v, rs, h, s0, s1, tid);
-  for (int k0 = s0; k0 < kend; k0 += TILE) {
+  for (int k00 = s0; k00 < kend; k00 += STAGE) {
     __syncthreads();
     stage_store(nk, sK, tid);
     stage_store(nv, sV, tid);
     __syncthreads();
-    if (k0 + TILE < kend) {
-      nk = stage_load(k, rs, h, k0 + TILE, s1, tid);
-      nv = stage_load(v, rs, h, k0 + TILE, s1, tid);
+    if (k00 + STAGE < kend) {
+      nk = stage_load(k, rs, h, k00 + STAGE, s1, tid);
+      nv = stage_load(v, rs, h, k00 + STAGE, s1, tid);
     }
-    if (qw >= s1 || k0 > qw + TILE - 1) continue;  // wave-uniform: the tile is after every query of this wave
-    f32x16 St = f32x16{}, dPt = f32x16{};
+#pragma unroll 1
+    for (int half = 0; half < STAGE / TILE; ++half) {
+      const int k0 = k00 + TILE * half;
+      if (qw >= s1 || k0 > qw + TILE - 1 || k0 >= kend) continue;  // wave-uniform
+      const char* tK = sK + half * TILE * 256;
+      const char* tV = sV + half * TILE * 256;
+      f32x16 St = f32x16{}, dPt = f32x16{};
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      St = mfma(row_read(sK, l32, 2 * c + hi), qf[c], St);
-      dPt = mfma(row_read(sV, l32, 2 * c + hi), of[c], dPt);
+      for (int c = 0; c < 8; ++c) {
+        St = mfma(row_read(tK, l32, 2 * c + hi), qf[c], St);
+        dPt = mfma(row_read(tV, l32, 2 * c + hi), of[c], dPt);
+      }
+      bf16x8 sb[2];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int kj = k0 + 8 * (r >> 2) + 4 * hi + (r & 3);
+        const bool ok = qval && kj <= qq && kj < s1;
+        const float p = ok ? exp2f(St[r] * c2 - lq) : 0.f;
+        sb[r >> 3][r & 7] = (__bf16)(p * (dPt[r] - dq_delta));
+      }
+#pragma unroll
+      for (int dc = 0; dc < 4; ++dc)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) dQt[dc] = mfma(tr_operand(tK, lane, dc, ks), sb[ks], dQt[dc]);
     }
-    bf16x8 sb[2];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int kj = k0 + 8 * (r >> 2) + 4 * hi + (r & 3);
-      const bool ok = qval && kj <= qq && kj < s1;
-      const float p = ok ? exp2f(St[r] * c2 - lq) : 0.f;
-      sb[r >> 3][r & 7] = (__bf16)(p * (dPt[r] - dq_delta));
-    }
-#pragma unroll
-    for (int dc = 0; dc < 4; ++dc)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) dQt[dc] = mfma(tr_operand(sK, lane, dc, ks), sb[ks], dQt[dc]);
   }
   if (!qval) return;
   __bf16* dqr = dq + (int64_t)qq * rs + h * D;
@@ -253,23 +267,44 @@ __global__ __launch_bounds__(256) void attn_bwd_dq(const __bf16* __restrict__ q,
     }
 }
 
+// One launch for both roles: workgroups [0, n_kv) compute dK/dV of a key block, the rest dQ of a
+// query block, so the lighter dQ workgroups fill the causal tail of the dK/dV ones.
+__global__ __launch_bounds__(256) void attn_bwd_fused(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
+                                                      const __bf16* __restrict__ v, const __bf16* __restrict__ dout,
+                                                      const float* __restrict__ lse2, const float* __restrict__ delta,
+                                                      const int32_t* __restrict__ kv_items, int n_kv,
+                                                      const int32_t* __restrict__ q_items, __bf16* __restrict__ dq,
+                                                      __bf16* __restrict__ dk, __bf16* __restrict__ dv, int64_t T,
+                                                      int H, float c2, float scale) {
+  __shared__ __attribute__((aligned(16))) char s0[STAGE * D * 2], s1[STAGE * D * 2];
+  __shared__ float sL[STAGE], sDl[STAGE];
+  if ((int)blockIdx.x < n_kv)
+    attn_bwd_dkdv(q, k, v, dout, lse2, delta, kv_items, dk, dv, T, H, c2, scale, blockIdx.x, s0, s1, sL, sDl);
+  else
+    attn_bwd_dq(q, k, v, dout, lse2, delta, q_items, dq, T, H, c2, scale, blockIdx.x - n_kv, s0, s1);
+}
+
 // delta[h][t] = sum_d O dO (fp32);  lse2[h][t] = L * log2(e), with L in torch's varlen layout
 // [nseq][H][lse_len] (row of sequence b starting at token cu[b]).  One wave per (t, h).
 __global__ __launch_bounds__(256) void attn_bwd_pre(const __bf16* __restrict__ out, const __bf16* __restrict__ dout,
                                                     const float* __restrict__ lse, const int32_t* __restrict__ cu,
                                                     int nseq, int64_t lse_len, float* __restrict__ lse2,
                                                     float* __restrict__ delta, int64_t T, int H) {
-  const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= T * H) return;
-  const int64_t t = row / H;
-  const int h = (int)(row - t * H);
-  const __bf16* o = out + row * D;
-  const __bf16* g = dout + row * D;
-  float s = (float)o[2 * lane] * (float)g[2 * lane] + (float)o[2 * lane + 1] * (float)g[2 * lane + 1];
+  // 16 lanes per (t, h) row of 128 elements: 8 per lane, 16 rows per workgroup
+  const int sub = threadIdx.x & 15;
+  const int64_t row = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
+  const bool live = row < T * H;
+  float s = 0.f;
+  if (live) {
+    const bf16x8 o = ld8(out + row * D + 8 * sub), g = ld8(dout + row * D + 8 * sub);
 #pragma unroll
-  for (int m = 32; m > 0; m >>= 1) s += __shfl_xor(s, m, 64);
-  if (lane == 0) {
+    for (int i = 0; i < 8; ++i) s = __builtin_fmaf((float)o[i], (float)g[i], s);
+  }
+#pragma unroll
+  for (int m = 8; m > 0; m >>= 1) s += __shfl_xor(s, m, 16);
+  if (live && sub == 0) {
+    const int64_t t = row / H;
+    const int h = (int)(row - t * H);
     int lo = 0, hi = nseq - 1;  // last b with cu[b] <= t
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
@@ -296,7 +331,7 @@ int prl_attn_bwd_preprocess(const void* out, const void* dout, const float* lse,
   if (head_dim != D) return PRL_E_UNSUPPORTED;
   if (tokens == 0) return PRL_OK;
   const int64_t rows = tokens * heads;
-  hipLaunchKernelGGL(attn_bwd_pre, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, static_cast<hipStream_t>(stream),
+  hipLaunchKernelGGL(attn_bwd_pre, dim3((unsigned)((rows + 15) / 16)), dim3(256), 0, static_cast<hipStream_t>(stream),
                      (const __bf16*)out, (const __bf16*)dout, lse, cu_seqlens, (int)nseq, lse_len, lse2, delta, tokens,
                      (int)heads);
   return (int)hipGetLastError();
@@ -312,16 +347,10 @@ int prl_attn_bwd(const void* q, const void* k, const void* v, const void* dout, 
   if (heads > 65535) return PRL_E_UNSUPPORTED;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const float c2 = scale * 1.4426950408889634f;
-  if (n_kv_items)
-    hipLaunchKernelGGL(attn_bwd_dkdv, dim3((unsigned)n_kv_items, (unsigned)heads), dim3(256), 0, s,
-                       (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, (const __bf16*)dout, lse2, delta,
-                       kv_items, (__bf16*)dk, (__bf16*)dv, tokens, (int)heads, c2, scale);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return (int)e;
-  if (n_q_items)
-    hipLaunchKernelGGL(attn_bwd_dq, dim3((unsigned)n_q_items, (unsigned)heads), dim3(256), 0, s, (const __bf16*)q,
-                       (const __bf16*)k, (const __bf16*)v, (const __bf16*)dout, lse2, delta, q_items, (__bf16*)dq,
-                       tokens, (int)heads, c2, scale);
+  if (n_kv_items + n_q_items == 0) return PRL_OK;
+  hipLaunchKernelGGL(attn_bwd_fused, dim3((unsigned)(n_kv_items + n_q_items), (unsigned)heads), dim3(256), 0, s,
+                     (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, (const __bf16*)dout, lse2, delta, kv_items,
+                     (int)n_kv_items, q_items, (__bf16*)dq, (__bf16*)dk, (__bf16*)dv, tokens, (int)heads, c2, scale);
   return (int)hipGetLastError();
 }
 

@@ -7,8 +7,9 @@ to the model at rl/__init__.py:188-189).  This registers an HF attention impleme
 (``torch.nn.attention.varlen.varlen_attn``), given cumulative sequence offsets computed ONCE
 per micro-batch on the host (``cu_seq_lens_q/k``, ``max_length_q/k`` — the FlashAttention
 kwargs HF propagates to every layer).  If varlen is unavailable for the inputs it runs causal
-SDPA per sequence (same result, no T x T mask either way).  PRL_ATTN_BWD=hip selects the build's HIP
-flash-attention backward (csrc/attn_bwd.hip) for bf16, head dim 128.
+SDPA per sequence (same result, no T x T mask either way).  For bf16, head dim 128 the backward is
+the build's HIP flash-attention backward (csrc/attn_bwd.hip; 1.41x / 1.15x the library's at
+8 x 2048 / 2 x 8192 on MI355X); PRL_ATTN_BWD=torch keeps the library's.
 """
 
 from __future__ import annotations
@@ -45,7 +46,7 @@ def _items(bounds: list[int], device) -> tuple:
 
 class PackedCausalAttention(torch.autograd.Function):
     """torch's varlen flash-attention forward (keeps its log-sum-exp), HIP backward
-    (prl_attn_bwd: ~2x the MI355X throughput of the library backward; tools/attn_backend_probe.py).
+    (prl_attn_bwd; tools/attn_backend_probe.py, profiles/r01_attention_probe.jsonl).
     q, k, v: [T, H, 128] bf16 with equal head counts."""
 
     @staticmethod
@@ -84,7 +85,7 @@ class PackedCausalAttention(torch.autograd.Function):
 
 def _hip_backward_ok(q, k) -> bool:
     return (q.dtype == torch.bfloat16 and q.shape[-1] == 128 and q.shape == k.shape
-            and os.environ.get("PRL_ATTN_BWD", "torch") == "hip")
+            and os.environ.get("PRL_ATTN_BWD", "hip") == "hip")
 
 
 def varlen_attention_forward(module, query, key, value, attention_mask, scaling=None, dropout=0.0, **kwargs):
