@@ -31,6 +31,7 @@ namespace prl_attn {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
@@ -41,6 +42,7 @@ constexpr int STAGE = 64;  // rows staged per barrier pair (two tiles)
 __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 __device__ __forceinline__ bf16x8 ld8(const __bf16* p) { return __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(p)); }
 __device__ __forceinline__ bf16x8 zero8() { return __builtin_bit_cast(bf16x8, u32x4{0, 0, 0, 0}); }
 __device__ __forceinline__ void st4(__bf16* p, float a, float b, float c, float d) {
@@ -162,15 +164,22 @@ __device__ __forceinline__ void attn_bwd_dkdv(const __bf16* __restrict__ q, cons
         S = mfma(row_read(tQ, l32, 2 * c + hi), kf[c], S);
         dP = mfma(row_read(tdO, l32, 2 * c + hi), vf[c], dP);
       }
+      // the 16 query rows of this lane's accumulator: 4 runs of 4 consecutive rows
+      f32x4 Lr[4], Dr[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        Lr[g] = *reinterpret_cast<const f32x4*>(tL + 8 * g + 4 * hi);
+        Dr[g] = *reinterpret_cast<const f32x4*>(tDl + 8 * g + 4 * hi);
+      }
       bf16x8 pb[2], sb[2];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int qi = 8 * (r >> 2) + 4 * hi + (r & 3);
         const int t = q0 + qi;
         const bool ok = kval && key <= t && t < s1;
-        const float p = ok ? exp2f(S[r] * c2 - tL[qi]) : 0.f;
+        const float p = ok ? fexp2(__builtin_fmaf(S[r], c2, -Lr[r >> 2][r & 3])) : 0.f;
         pb[r >> 3][r & 7] = (__bf16)p;
-        sb[r >> 3][r & 7] = (__bf16)(p * (dP[r] - tDl[qi]));
+        sb[r >> 3][r & 7] = (__bf16)(p * (dP[r] - Dr[r >> 2][r & 3]));
       }
 #pragma unroll
       for (int dc = 0; dc < 4; ++dc)
@@ -246,7 +255,7 @@ __device__ __forceinline__ void attn_bwd_dq(const __bf16* __restrict__ q, const 
       for (int r = 0; r < 16; ++r) {
         const int kj = k0 + 8 * (r >> 2) + 4 * hi + (r & 3);
         const bool ok = qval && kj <= qq && kj < s1;
-        const float p = ok ? exp2f(St[r] * c2 - lq) : 0.f;
+        const float p = ok ? fexp2(__builtin_fmaf(St[r], c2, -lq)) : 0.f;
         sb[r >> 3][r & 7] = (__bf16)(p * (dPt[r] - dq_delta));
       }
 #pragma unroll
@@ -277,7 +286,7 @@ __global__ __launch_bounds__(256) void attn_bwd_fused(const __bf16* __restrict__
                                                       __bf16* __restrict__ dk, __bf16* __restrict__ dv, int64_t T,
                                                       int H, float c2, float scale) {
   __shared__ __attribute__((aligned(16))) char s0[STAGE * D * 2], s1[STAGE * D * 2];
-  __shared__ float sL[STAGE], sDl[STAGE];
+  __shared__ __attribute__((aligned(16))) float sL[STAGE], sDl[STAGE];
   if ((int)blockIdx.x < n_kv)
     attn_bwd_dkdv(q, k, v, dout, lse2, delta, kv_items, dk, dv, T, H, c2, scale, blockIdx.x, s0, s1, sL, sDl);
   else
