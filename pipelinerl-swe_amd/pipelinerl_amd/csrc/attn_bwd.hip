@@ -100,25 +100,30 @@ __device__ __forceinline__ void stage_store(const Stage& st, char* base, int tid
   }
 }
 
-// items: int32 triplets (seq_start, seq_end, block_start), block = 128 keys (dkdv) / queries (dq)
+// items: int32 triplets (seq_start, seq_end, block_start), block = 128 keys (dkdv) / queries (dq).
+// GQA: k / v / dk / dv have Hkv heads, q / dout / dq have H = rep * Hkv; the dK/dV role of kv head
+// g sweeps the query heads g*rep .. g*rep+rep-1 (all of its group), so dK / dV are complete sums
+// in registers with no atomics.
 __device__ __forceinline__ void attn_bwd_dkdv(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
-                                                     const __bf16* __restrict__ v, const __bf16* __restrict__ dout,
-                                                     const float* __restrict__ lse2, const float* __restrict__ delta,
-                                                     const int32_t* __restrict__ items, __bf16* __restrict__ dk,
-                                                     __bf16* __restrict__ dv, int64_t T, int H, float c2, float scale,
-                                                     int it, char* sQ, char* sdO, float* sL, float* sDl) {
-  const int h = blockIdx.y, tid = threadIdx.x;
+                                              const __bf16* __restrict__ v, const __bf16* __restrict__ dout,
+                                              const float* __restrict__ lse2, const float* __restrict__ delta,
+                                              const int32_t* __restrict__ items, __bf16* __restrict__ dk,
+                                              __bf16* __restrict__ dv, int64_t T, int H, int Hkv, float c2,
+                                              float scale, int it, int g, char* sQ, char* sdO, float* sL,
+                                              float* sDl) {
+  const int tid = threadIdx.x;
   const int s1 = items[3 * it + 1], kb = items[3 * it + 2];
   const int lane = tid & 63, w = tid >> 6, hi = lane >> 5, l32 = lane & 31;
-  const int64_t rs = (int64_t)H * D;
+  const int64_t rsq = (int64_t)H * D, rsk = (int64_t)Hkv * D;
+  const int rep = H / Hkv;
   const int kw = kb + 32 * w;
   const int key = kw + l32;
   const bool kval = key < s1;
   bf16x8 kf[8], vf[8];
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
-    kf[c] = kval ? ld8(k + (int64_t)key * rs + h * D + 16 * c + 8 * hi) : zero8();
-    vf[c] = kval ? ld8(v + (int64_t)key * rs + h * D + 16 * c + 8 * hi) : zero8();
+    kf[c] = kval ? ld8(k + (int64_t)key * rsk + g * D + 16 * c + 8 * hi) : zero8();
+    vf[c] = kval ? ld8(v + (int64_t)key * rsk + g * D + 16 * c + 8 * hi) : zero8();
   }
   f32x16 dKt[4], dVt[4];
 #pragma unroll
@@ -126,7 +131,9 @@ __device__ __forceinline__ void attn_bwd_dkdv(const __bf16* __restrict__ q, cons
     dKt[i] = f32x16{};
     dVt[i] = f32x16{};
   }
-  Stage nq = stage_load(q, rs, h, kb, s1, tid), nd = stage_load(dout, rs, h, kb, s1, tid);
+#pragma unroll 1
+  for (int h = g * rep; h < (g + 1) * rep; ++h) {
+  Stage nq = stage_load(q, rsq, h, kb, s1, tid), nd = stage_load(dout, rsq, h, kb, s1, tid);
   float nl = 0.f, ndl = 0.f;
   if (tid < STAGE && kb + tid < s1) {
     nl = lse2[(int64_t)h * T + kb + tid];
@@ -143,8 +150,8 @@ __device__ __forceinline__ void attn_bwd_dkdv(const __bf16* __restrict__ q, cons
     __syncthreads();
     const int qn = q00 + STAGE;  // prefetch the next stage behind this stage's MFMAs
     if (qn < s1) {
-      nq = stage_load(q, rs, h, qn, s1, tid);
-      nd = stage_load(dout, rs, h, qn, s1, tid);
+      nq = stage_load(q, rsq, h, qn, s1, tid);
+      nd = stage_load(dout, rsq, h, qn, s1, tid);
       if (tid < STAGE && qn + tid < s1) {
         nl = lse2[(int64_t)h * T + qn + tid];
         ndl = delta[(int64_t)h * T + qn + tid];
@@ -167,9 +174,9 @@ __device__ __forceinline__ void attn_bwd_dkdv(const __bf16* __restrict__ q, cons
       // the 16 query rows of this lane's accumulator: 4 runs of 4 consecutive rows
       f32x4 Lr[4], Dr[4];
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        Lr[g] = *reinterpret_cast<const f32x4*>(tL + 8 * g + 4 * hi);
-        Dr[g] = *reinterpret_cast<const f32x4*>(tDl + 8 * g + 4 * hi);
+      for (int gg = 0; gg < 4; ++gg) {
+        Lr[gg] = *reinterpret_cast<const f32x4*>(tL + 8 * gg + 4 * hi);
+        Dr[gg] = *reinterpret_cast<const f32x4*>(tDl + 8 * gg + 4 * hi);
       }
       bf16x8 pb[2], sb[2];
 #pragma unroll
@@ -190,9 +197,10 @@ __device__ __forceinline__ void attn_bwd_dkdv(const __bf16* __restrict__ q, cons
         }
     }
   }
+  }
   if (!kval) return;
-  __bf16* dkr = dk + (int64_t)key * rs + h * D;
-  __bf16* dvr = dv + (int64_t)key * rs + h * D;
+  __bf16* dkr = dk + (int64_t)key * rsk + g * D;
+  __bf16* dvr = dv + (int64_t)key * rsk + g * D;
 #pragma unroll
   for (int dc = 0; dc < 4; ++dc)
 #pragma unroll
@@ -208,11 +216,13 @@ __device__ __forceinline__ void attn_bwd_dq(const __bf16* __restrict__ q, const 
                                                    const __bf16* __restrict__ v, const __bf16* __restrict__ dout,
                                                    const float* __restrict__ lse2, const float* __restrict__ delta,
                                                    const int32_t* __restrict__ items, __bf16* __restrict__ dq,
-                                                   int64_t T, int H, float c2, float scale, int it, char* sK, char* sV) {
-  const int h = blockIdx.y, tid = threadIdx.x;
+                                                   int64_t T, int H, int Hkv, float c2, float scale, int it, int h,
+                                                   char* sK, char* sV) {
+  const int tid = threadIdx.x;
   const int s0 = items[3 * it], s1 = items[3 * it + 1], qb = items[3 * it + 2];
   const int lane = tid & 63, w = tid >> 6, hi = lane >> 5, l32 = lane & 31;
-  const int64_t rs = (int64_t)H * D;
+  const int64_t rs = (int64_t)H * D, rsk = (int64_t)Hkv * D;
+  const int g = h / (H / Hkv);  // this query head's kv head
   const int qw = qb + 32 * w;
   const int qq = qw + l32;
   const bool qval = qq < s1;
@@ -228,15 +238,15 @@ __device__ __forceinline__ void attn_bwd_dq(const __bf16* __restrict__ q, const 
 #pragma unroll
   for (int i = 0; i < 4; ++i) dQt[i] = f32x16{};
   const int kend = (qb + 128 < s1 ? qb + 128 : s1);  // causal: keys <= the block's last query
-  Stage nk = stage_load(k, rs, h, s0, s1, tid), nv = stage_load(v, rs, h, s0, s1, tid);
+  Stage nk = stage_load(k, rsk, g, s0, s1, tid), nv = stage_load(v, rsk, g, s0, s1, tid);
   for (int k00 = s0; k00 < kend; k00 += STAGE) {
     __syncthreads();
     stage_store(nk, sK, tid);
     stage_store(nv, sV, tid);
     __syncthreads();
     if (k00 + STAGE < kend) {
-      nk = stage_load(k, rs, h, k00 + STAGE, s1, tid);
-      nv = stage_load(v, rs, h, k00 + STAGE, s1, tid);
+      nk = stage_load(k, rsk, g, k00 + STAGE, s1, tid);
+      nv = stage_load(v, rsk, g, k00 + STAGE, s1, tid);
     }
 #pragma unroll 1
     for (int half = 0; half < STAGE / TILE; ++half) {
@@ -276,21 +286,24 @@ __device__ __forceinline__ void attn_bwd_dq(const __bf16* __restrict__ q, const 
     }
 }
 
-// One launch for both roles: workgroups [0, n_kv) compute dK/dV of a key block, the rest dQ of a
-// query block, so the lighter dQ workgroups fill the causal tail of the dK/dV ones.
+// One launch for both roles: workgroups [0, n_kv * Hkv) compute dK/dV of a (key block, kv head),
+// the rest dQ of a (query block, query head), so the lighter dQ workgroups fill the causal tail.
 __global__ __launch_bounds__(256) void attn_bwd_fused(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
                                                       const __bf16* __restrict__ v, const __bf16* __restrict__ dout,
                                                       const float* __restrict__ lse2, const float* __restrict__ delta,
                                                       const int32_t* __restrict__ kv_items, int n_kv,
                                                       const int32_t* __restrict__ q_items, __bf16* __restrict__ dq,
                                                       __bf16* __restrict__ dk, __bf16* __restrict__ dv, int64_t T,
-                                                      int H, float c2, float scale) {
+                                                      int H, int Hkv, float c2, float scale) {
   __shared__ __attribute__((aligned(16))) char s0[STAGE * D * 2], s1[STAGE * D * 2];
   __shared__ __attribute__((aligned(16))) float sL[STAGE], sDl[STAGE];
-  if ((int)blockIdx.x < n_kv)
-    attn_bwd_dkdv(q, k, v, dout, lse2, delta, kv_items, dk, dv, T, H, c2, scale, blockIdx.x, s0, s1, sL, sDl);
+  const int b = blockIdx.x;
+  if (b < n_kv * Hkv)
+    attn_bwd_dkdv(q, k, v, dout, lse2, delta, kv_items, dk, dv, T, H, Hkv, c2, scale, b / Hkv, b % Hkv, s0, s1, sL,
+                  sDl);
   else
-    attn_bwd_dq(q, k, v, dout, lse2, delta, q_items, dq, T, H, c2, scale, blockIdx.x - n_kv, s0, s1);
+    attn_bwd_dq(q, k, v, dout, lse2, delta, q_items, dq, T, H, Hkv, c2, scale, (b - n_kv * Hkv) / H,
+                (b - n_kv * Hkv) % H, s0, s1);
 }
 
 // delta[h][t] = sum_d O dO (fp32);  lse2[h][t] = L * log2(e), with L in torch's varlen layout
@@ -348,18 +361,20 @@ int prl_attn_bwd_preprocess(const void* out, const void* dout, const float* lse,
 
 int prl_attn_bwd(const void* q, const void* k, const void* v, const void* dout, const float* lse2, const float* delta,
                  const int32_t* kv_items, int32_t n_kv_items, const int32_t* q_items, int32_t n_q_items, void* dq,
-                 void* dk, void* dv, int64_t tokens, int32_t heads, int32_t head_dim, float scale, void* stream) {
-  if (!q || !k || !v || !dout || !lse2 || !delta || !dq || !dk || !dv || tokens < 0 || heads <= 0 ||
-      n_kv_items < 0 || n_q_items < 0 || (n_kv_items && !kv_items) || (n_q_items && !q_items))
+                 void* dk, void* dv, int64_t tokens, int32_t heads, int32_t kv_heads, int32_t head_dim, float scale,
+                 void* stream) {
+  if (!q || !k || !v || !dout || !lse2 || !delta || !dq || !dk || !dv || tokens < 0 || heads <= 0 || kv_heads <= 0 ||
+      heads % kv_heads || n_kv_items < 0 || n_q_items < 0 || (n_kv_items && !kv_items) || (n_q_items && !q_items))
     return PRL_E_INVALID;
   if (head_dim != D) return PRL_E_UNSUPPORTED;
-  if (heads > 65535) return PRL_E_UNSUPPORTED;
-  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t blocks = (int64_t)n_kv_items * kv_heads + (int64_t)n_q_items * heads;
+  if (blocks > 0x7FFFFFFF) return PRL_E_UNSUPPORTED;
+  if (blocks == 0) return PRL_OK;
   const float c2 = scale * 1.4426950408889634f;
-  if (n_kv_items + n_q_items == 0) return PRL_OK;
-  hipLaunchKernelGGL(attn_bwd_fused, dim3((unsigned)(n_kv_items + n_q_items), (unsigned)heads), dim3(256), 0, s,
+  hipLaunchKernelGGL(attn_bwd_fused, dim3((unsigned)blocks), dim3(256), 0, static_cast<hipStream_t>(stream),
                      (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, (const __bf16*)dout, lse2, delta, kv_items,
-                     (int)n_kv_items, q_items, (__bf16*)dq, (__bf16*)dk, (__bf16*)dv, tokens, (int)heads, c2, scale);
+                     (int)n_kv_items, q_items, (__bf16*)dq, (__bf16*)dk, (__bf16*)dv, tokens, (int)heads,
+                     (int)kv_heads, c2, scale);
   return (int)hipGetLastError();
 }
 

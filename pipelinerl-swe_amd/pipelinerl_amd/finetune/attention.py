@@ -30,14 +30,18 @@ BLOCK = 128  # keys / queries per workgroup of the HIP backward (csrc/attn_bwd.h
 
 
 def _items(bounds: list[int], device) -> tuple:
-    """(kv_items, q_items) int32 [n, 3] device tensors: (seq_start, seq_end, block_start) per
-    128-row block of every sequence (the same list serves both kernels)."""
+    """(kv_items, q_items, n) int32 [n, 3] device tensors: (seq_start, seq_end, block_start) per
+    128-row block of every sequence, heaviest first: key blocks by the causal query rows after
+    them, query blocks by the key rows before them (the workgroups are dispatched in list order,
+    so the long ones start first and the short ones fill the tail)."""
     key = (tuple(bounds), str(device))
     hit = _ITEMS.get(key)
     if hit is None:
         rows = [(a, b, x) for a, b in zip(bounds[:-1], bounds[1:]) for x in range(a, b, BLOCK)]
-        t = torch.tensor(rows if rows else [(0, 0, 0)], dtype=torch.int32).to(device)
-        hit = (t, len(rows))
+        kv = sorted(rows, key=lambda r: -(r[1] - r[2]))
+        qb = sorted(rows, key=lambda r: -(min(r[2] + BLOCK, r[1]) - r[0]))
+        mk = lambda rr: torch.tensor(rr if rr else [(0, 0, 0)], dtype=torch.int32).to(device)  # noqa: E731
+        hit = (mk(kv), mk(qb), len(rows))
         if len(_ITEMS) > 64:
             _ITEMS.clear()
         _ITEMS[key] = hit
@@ -47,7 +51,7 @@ def _items(bounds: list[int], device) -> tuple:
 class PackedCausalAttention(torch.autograd.Function):
     """torch's varlen flash-attention forward (keeps its log-sum-exp), HIP backward
     (prl_attn_bwd; tools/attn_backend_probe.py, profiles/r01_attention_probe.jsonl).
-    q, k, v: [T, H, 128] bf16 with equal head counts."""
+    q: [T, H, 128], k / v: [T, Hkv, 128] bf16 (GQA native: no repeated k / v)."""
 
     @staticmethod
     def forward(ctx, q, k, v, cu, mx: int, bounds: list[int]):
@@ -75,16 +79,18 @@ class PackedCausalAttention(torch.autograd.Function):
         _native.check(lib.prl_attn_bwd_preprocess(out.data_ptr(), dout.data_ptr(), lse.data_ptr(), cu.data_ptr(),
                                                   lse.shape[0], lse.shape[2], lse2.data_ptr(), delta.data_ptr(), T, H,
                                                   D, st), "prl_attn_bwd_preprocess")
-        items, n = _items(ctx.bounds, q.device)
+        kv_items, q_items, n = _items(ctx.bounds, q.device)
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
         _native.check(lib.prl_attn_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), dout.data_ptr(), lse2.data_ptr(),
-                                       delta.data_ptr(), items.data_ptr(), n, items.data_ptr(), n, dq.data_ptr(),
-                                       dk.data_ptr(), dv.data_ptr(), T, H, D, D ** -0.5, st), "prl_attn_bwd")
+                                       delta.data_ptr(), kv_items.data_ptr(), n, q_items.data_ptr(), n, dq.data_ptr(),
+                                       dk.data_ptr(), dv.data_ptr(), T, H, k.shape[1], D, D ** -0.5, st),
+                      "prl_attn_bwd")
         return dq, dk, dv, None, None, None
 
 
 def _hip_backward_ok(q, k) -> bool:
-    return (q.dtype == torch.bfloat16 and q.shape[-1] == 128 and q.shape == k.shape
+    return (q.dtype == torch.bfloat16 and k.dtype == torch.bfloat16 and q.shape[-1] == 128 == k.shape[-1]
+            and q.shape[0] == k.shape[0] and q.shape[1] % k.shape[1] == 0
             and os.environ.get("PRL_ATTN_BWD", "hip") == "hip")
 
 
@@ -102,20 +108,20 @@ def varlen_attention_forward(module, query, key, value, attention_mask, scaling=
     q = query[0].transpose(0, 1)
     k = key[0].transpose(0, 1)
     v = value[0].transpose(0, 1)
-    if Hkv != Hq:
-        # GQA: the varlen kernel also takes Hkv < Hq directly (same results, tests/test_model_ops_gpu.py),
-        # but its backward is slower that way (2.16 vs 2.09 ms at 8 x 2048, 6.32 vs 5.64 ms at 2 x 8192:
-        # tools/attn_backend_probe.py), so k / v are repeated per query head
+    mx = int(kwargs["max_length_q"])
+    bounds = kwargs.get("cu_seq_lens_host")
+    hip_bwd = bounds is not None and q.is_cuda and _hip_backward_ok(q, k)
+    if Hkv != Hq and not hip_bwd:
+        # GQA with the library backward: its native-GQA backward is slower than with repeated k / v
+        # (6.32 vs 5.64 ms at 2 x 8192, tools/attn_backend_probe.py); the HIP backward takes GQA as is
         k = k.repeat_interleave(Hq // Hkv, dim=1)
         v = v.repeat_interleave(Hq // Hkv, dim=1)
-    mx = int(kwargs["max_length_q"])
     default_scale = D ** -0.5
     global _varlen_ok
     if (scaling is None or abs(scaling - default_scale) < 1e-12) and q.is_cuda and _varlen_ok is not False:
         try:
             q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
-            bounds = kwargs.get("cu_seq_lens_host")
-            if bounds is not None and _hip_backward_ok(q, k):
+            if hip_bwd:
                 out = PackedCausalAttention.apply(q, k, v, cu, mx, list(bounds))
             else:
                 from torch.nn.attention.varlen import varlen_attn
@@ -127,7 +133,9 @@ def varlen_attention_forward(module, query, key, value, attention_mask, scaling=
             if _varlen_ok is None:
                 logger.warning(f"varlen flash attention unavailable ({e}); using per-sequence SDPA")
             _varlen_ok = False
-    bounds = kwargs.get("cu_seq_lens_host")
+    if k.shape[1] != Hq:  # the per-sequence SDPA fallback takes equal head counts
+        k = k.repeat_interleave(Hq // Hkv, dim=1)
+        v = v.repeat_interleave(Hq // Hkv, dim=1)
     if bounds is None:
         bounds = cu.tolist()
     outs = []

@@ -50,9 +50,8 @@ def test_hip_backward_matches(bounds):
     cu = torch.tensor(bounds, dtype=torch.int32, device=DEV)
     mx = max(b - a for a, b in zip(bounds[:-1], bounds[1:]))
 
-    def ours(qq, kk, vv):
-        return PackedCausalAttention.apply(qq, kk.repeat_interleave(rep, 1), vv.repeat_interleave(rep, 1), cu, mx,
-                                           bounds)
+    def ours(qq, kk, vv):  # GQA native: k / v keep their 2 heads
+        return PackedCausalAttention.apply(qq, kk, vv, cu, mx, bounds)
 
     def lib(qq, kk, vv):
         return varlen_attn(qq, kk.repeat_interleave(rep, 1), vv.repeat_interleave(rep, 1), cu, cu, mx, mx,

@@ -53,8 +53,7 @@ def case(T, seq, hq=12, hkv=2, D=128):
     def hip_bwd():
         from pipelinerl_amd.finetune.attention import PackedCausalAttention
 
-        PackedCausalAttention.apply(q, k.repeat_interleave(rep, 1), v.repeat_interleave(rep, 1), cu, seq,
-                                    list(range(0, T + 1, seq))).backward(do)
+        PackedCausalAttention.apply(q, k, v, cu, seq, list(range(0, T + 1, seq))).backward(do)
 
     def fwd_only():
         with torch.no_grad():
