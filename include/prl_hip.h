@@ -231,12 +231,20 @@ int prl_rope_backward(const void* dq_out, const void* dk_out, const void* cos, c
                       void* stream);
 
 /* ---- Flash-attention backward for packed causal attention (csrc/attn_bwd.hip), bf16,
- * head_dim 128, heads of q / k / v equal (GQA callers repeat k / v).  Tensors [tokens, heads,
- * 128] token-major.  lse: the forward's log-sum-exp in torch's varlen layout
+ * head_dim 128, GQA (q / dout / dq: heads, k / v / dk / dv: kv_heads, heads % kv_heads == 0).
+ * Tensors [tokens, heads, 128] token-major.  lse: the forward's log-sum-exp in torch's varlen layout
  * [nseq][heads][lse_len] (sequence b's row starts at token cu_seqlens[b]; lse_len >= its length).
  * Replaces the backward of torch's varlen flash attention used by the trainer's packed
  * attention (finetune/attention.py; the reference's flash-attn varlen, finetune_loop.py:381). */
-/* lse2 = lse * log2(e), delta = rowsum(out * dout), both fp32 [heads][tokens]. */
+/* Forward: out [tokens, heads, 128] bf16 and lse2[heads][tokens] = log2 sum_j exp2(log2(e) s S_tj)
+ * (the backward's log-sum-exp input, base 2); q_items as for prl_attn_bwd. */
+int prl_attn_fwd(const void* q, const void* k, const void* v, const int32_t* q_items,
+                 int32_t n_q_items, void* out, float* lse2, int64_t tokens, int32_t heads,
+                 int32_t kv_heads, int32_t head_dim, float scale, void* stream);
+/* delta[heads][tokens] = rowsum(out * dout) (fp32), when lse2 comes from prl_attn_fwd. */
+int prl_attn_bwd_delta(const void* out, const void* dout, float* delta, int64_t tokens,
+                       int32_t heads, int32_t head_dim, void* stream);
+/* With torch's forward: lse2 = lse * log2(e), delta = rowsum(out * dout), both fp32 [heads][tokens]. */
 int prl_attn_bwd_preprocess(const void* out, const void* dout, const float* lse,
                             const int32_t* cu_seqlens, int32_t nseq, int64_t lse_len, float* lse2,
                             float* delta, int64_t tokens, int32_t heads, int32_t head_dim, void* stream);
@@ -245,7 +253,7 @@ int prl_attn_bwd_preprocess(const void* out, const void* dout, const float* lse,
 int prl_attn_bwd(const void* q, const void* k, const void* v, const void* dout, const float* lse2,
                  const float* delta, const int32_t* kv_items, int32_t n_kv_items, const int32_t* q_items,
                  int32_t n_q_items, void* dq, void* dk, void* dv, int64_t tokens, int32_t heads,
-                 int32_t head_dim, float scale, void* stream);
+                 int32_t kv_heads, int32_t head_dim, float scale, void* stream);
 
 #ifdef __cplusplus
 }

@@ -93,6 +93,9 @@ _SIGNATURES = {
                                   c_int32, c_int32, c_void_p]),
     "prl_attn_bwd_preprocess": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int64, c_void_p, c_void_p,
                                         c_int64, c_int32, c_int32, c_void_p]),
+    "prl_attn_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_int64, c_int32,
+                             c_int32, c_int32, c_float, c_void_p]),
+    "prl_attn_bwd_delta": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32, c_void_p]),
     "prl_attn_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,
                              c_int32, c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32, c_int32, c_float,
                              c_void_p]),

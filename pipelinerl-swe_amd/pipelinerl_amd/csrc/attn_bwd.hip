@@ -306,6 +306,121 @@ __global__ __launch_bounds__(256) void attn_bwd_fused(const __bf16* __restrict__
                 (b - n_kv * Hkv) % H, s0, s1);
 }
 
+// Forward (same structure as the dQ role): one workgroup = 128 queries of one query head, each
+// wave owns 32 queries with the query on the MFMA lane; per 32-key tile S^T = K Q^T, an online
+// base-2 softmax per query (lane) with a lazy rescale of the output accumulators (only when the
+// running max grows by more than 8), O^T += V^T P with V^T read transposed from the tile image.
+// Writes O [T, H, 128] bf16 and lse2[h][t] = log2 sum_j 2^(c2 S_tj) (the backward's input).
+constexpr float kRescale = 8.0f;
+__global__ __launch_bounds__(256) void attn_fwd(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
+                                                const __bf16* __restrict__ v, const int32_t* __restrict__ items,
+                                                __bf16* __restrict__ out, float* __restrict__ lse2, int64_t T, int H,
+                                                int Hkv, float c2) {
+  __shared__ __attribute__((aligned(16))) char sK[STAGE * D * 2], sV[STAGE * D * 2];
+  const int tid = threadIdx.x;
+  const int it = blockIdx.x / H, h = blockIdx.x % H;
+  const int s0 = items[3 * it], s1 = items[3 * it + 1], qb = items[3 * it + 2];
+  const int lane = tid & 63, w = tid >> 6, hi = lane >> 5, l32 = lane & 31;
+  const int64_t rs = (int64_t)H * D, rsk = (int64_t)Hkv * D;
+  const int g = h / (H / Hkv);
+  const int qw = qb + 32 * w;
+  const int qq = qw + l32;
+  const bool qval = qq < s1;
+  bf16x8 qf[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) qf[c] = qval ? ld8(q + (int64_t)qq * rs + h * D + 16 * c + 8 * hi) : zero8();
+  f32x16 Ot[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) Ot[i] = f32x16{};
+  float m = -1e30f, l = 0.f;  // running max (base-2 units) and sum for query qq
+  const int kend = (qb + 128 < s1 ? qb + 128 : s1);
+  Stage nk = stage_load(k, rsk, g, s0, s1, tid), nv = stage_load(v, rsk, g, s0, s1, tid);
+  for (int k00 = s0; k00 < kend; k00 += STAGE) {
+    __syncthreads();
+    stage_store(nk, sK, tid);
+    stage_store(nv, sV, tid);
+    __syncthreads();
+    if (k00 + STAGE < kend) {
+      nk = stage_load(k, rsk, g, k00 + STAGE, s1, tid);
+      nv = stage_load(v, rsk, g, k00 + STAGE, s1, tid);
+    }
+#pragma unroll 1
+    for (int half = 0; half < STAGE / TILE; ++half) {
+      const int k0 = k00 + TILE * half;
+      if (qw >= s1 || k0 > qw + TILE - 1 || k0 >= kend) continue;  // wave-uniform
+      const char* tK = sK + half * TILE * 256;
+      const char* tV = sV + half * TILE * 256;
+      f32x16 St = f32x16{};
+#pragma unroll
+      for (int c = 0; c < 8; ++c) St = mfma(row_read(tK, l32, 2 * c + hi), qf[c], St);
+      float x[16];
+      float tmax = -1e30f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int kj = k0 + 8 * (r >> 2) + 4 * hi + (r & 3);
+        const bool ok = qval && kj <= qq && kj < s1;
+        x[r] = ok ? St[r] * c2 : -1e30f;
+        tmax = fmaxf(tmax, x[r]);
+      }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));  // the other half of this query's keys
+      if (tmax > m + kRescale) {  // lazy rebase (wave-uniform decision not needed: per lane)
+        const float f = fexp2(m - tmax);
+        l *= f;
+#pragma unroll
+        for (int dc = 0; dc < 4; ++dc)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) Ot[dc][r] *= f;
+        m = tmax;
+      }
+      bf16x8 pb[2];
+      float ps = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = fexp2(x[r] - m);
+        ps += p;
+        pb[r >> 3][r & 7] = (__bf16)p;
+      }
+      l += ps + __shfl_xor(ps, 32, 64);
+#pragma unroll
+      for (int dc = 0; dc < 4; ++dc)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) Ot[dc] = mfma(tr_operand(tV, lane, dc, ks), pb[ks], Ot[dc]);
+    }
+  }
+  if (!qval) return;
+  const float inv = 1.0f / l;
+  __bf16* orow = out + (int64_t)qq * rs + h * D;
+#pragma unroll
+  for (int dc = 0; dc < 4; ++dc)
+#pragma unroll
+    for (int gg = 0; gg < 4; ++gg) {
+      const int d0 = 32 * dc + 8 * gg + 4 * hi;
+      st4(orow + d0, Ot[dc][4 * gg] * inv, Ot[dc][4 * gg + 1] * inv, Ot[dc][4 * gg + 2] * inv,
+          Ot[dc][4 * gg + 3] * inv);
+    }
+  if (hi == 0) lse2[(int64_t)h * T + qq] = m + __builtin_log2f(l);
+}
+
+// delta[h][t] = sum_d O dO (fp32) for the HIP forward's [H][T] lse2 (no layout conversion)
+__global__ __launch_bounds__(256) void attn_bwd_delta(const __bf16* __restrict__ out, const __bf16* __restrict__ dout,
+                                                      float* __restrict__ delta, int64_t T, int H) {
+  const int sub = threadIdx.x & 15;
+  const int64_t row = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
+  const bool live = row < T * H;
+  float s = 0.f;
+  if (live) {
+    const bf16x8 o = ld8(out + row * D + 8 * sub), g = ld8(dout + row * D + 8 * sub);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s = __builtin_fmaf((float)o[i], (float)g[i], s);
+  }
+#pragma unroll
+  for (int m = 8; m > 0; m >>= 1) s += __shfl_xor(s, m, 16);
+  if (live && sub == 0) {
+    const int64_t t = row / H;
+    delta[(int64_t)(row - t * H) * T + t] = s;
+  }
+}
+
 // delta[h][t] = sum_d O dO (fp32);  lse2[h][t] = L * log2(e), with L in torch's varlen layout
 // [nseq][H][lse_len] (row of sequence b starting at token cu[b]).  One wave per (t, h).
 __global__ __launch_bounds__(256) void attn_bwd_pre(const __bf16* __restrict__ out, const __bf16* __restrict__ dout,
@@ -355,6 +470,34 @@ int prl_attn_bwd_preprocess(const void* out, const void* dout, const float* lse,
   const int64_t rows = tokens * heads;
   hipLaunchKernelGGL(attn_bwd_pre, dim3((unsigned)((rows + 15) / 16)), dim3(256), 0, static_cast<hipStream_t>(stream),
                      (const __bf16*)out, (const __bf16*)dout, lse, cu_seqlens, (int)nseq, lse_len, lse2, delta, tokens,
+                     (int)heads);
+  return (int)hipGetLastError();
+}
+
+int prl_attn_fwd(const void* q, const void* k, const void* v, const int32_t* q_items, int32_t n_q_items, void* out,
+                 float* lse2, int64_t tokens, int32_t heads, int32_t kv_heads, int32_t head_dim, float scale,
+                 void* stream) {
+  if (!q || !k || !v || !out || !lse2 || tokens < 0 || heads <= 0 || kv_heads <= 0 || heads % kv_heads ||
+      n_q_items < 0 || (n_q_items && !q_items))
+    return PRL_E_INVALID;
+  if (head_dim != D) return PRL_E_UNSUPPORTED;
+  const int64_t blocks = (int64_t)n_q_items * heads;
+  if (blocks > 0x7FFFFFFF) return PRL_E_UNSUPPORTED;
+  if (blocks == 0) return PRL_OK;
+  hipLaunchKernelGGL(attn_fwd, dim3((unsigned)blocks), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, q_items, (__bf16*)out, lse2, tokens,
+                     (int)heads, (int)kv_heads, scale * 1.4426950408889634f);
+  return (int)hipGetLastError();
+}
+
+int prl_attn_bwd_delta(const void* out, const void* dout, float* delta, int64_t tokens, int32_t heads,
+                       int32_t head_dim, void* stream) {
+  if (!out || !dout || !delta || tokens < 0 || heads <= 0) return PRL_E_INVALID;
+  if (head_dim != D) return PRL_E_UNSUPPORTED;
+  if (tokens == 0) return PRL_OK;
+  const int64_t rows = tokens * heads;
+  hipLaunchKernelGGL(attn_bwd_delta, dim3((unsigned)((rows + 15) / 16)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), (const __bf16*)out, (const __bf16*)dout, delta, tokens,
                      (int)heads);
   return (int)hipGetLastError();
 }

@@ -49,12 +49,27 @@ def _items(bounds: list[int], device) -> tuple:
 
 
 class PackedCausalAttention(torch.autograd.Function):
-    """torch's varlen flash-attention forward (keeps its log-sum-exp), HIP backward
-    (prl_attn_bwd; tools/attn_backend_probe.py, profiles/r01_attention_probe.jsonl).
+    """HIP flash-attention forward (prl_attn_fwd; PRL_ATTN_FWD=torch: torch's varlen forward, its
+    log-sum-exp converted) and HIP backward (prl_attn_bwd; tools/attn_backend_probe.py,
+    profiles/r01_attention_probe.jsonl).
     q: [T, H, 128], k / v: [T, Hkv, 128] bf16 (GQA native: no repeated k / v)."""
 
     @staticmethod
     def forward(ctx, q, k, v, cu, mx: int, bounds: list[int]):
+        from .. import _native
+
+        T, H, D = q.shape
+        ctx.bounds = bounds
+        ctx.hip_fwd = os.environ.get("PRL_ATTN_FWD", "hip") == "hip"
+        if ctx.hip_fwd:  # HIP forward: writes the backward's base-2 log-sum-exp [H, T] directly
+            _, q_items, n = _items(bounds, q.device)
+            out = torch.empty_like(q)
+            lse2 = torch.empty((H, T), dtype=torch.float32, device=q.device)
+            _native.check(_native.load().prl_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), q_items.data_ptr(), n,
+                                                      out.data_ptr(), lse2.data_ptr(), T, H, k.shape[1], D, D ** -0.5,
+                                                      torch.cuda.current_stream(q.device).cuda_stream), "prl_attn_fwd")
+            ctx.save_for_backward(q, k, v, out, lse2, cu)
+            return out
         out, lse, _, _, _ = torch.ops.aten._flash_attention_forward(q, k, v, cu, cu, mx, mx, 0.0, True, False)
         nseq = len(bounds) - 1
         # torch's varlen log-sum-exp on ROCm: [nseq, H, max_len] (checked: tools/lse_layout_probe.py)
@@ -62,7 +77,6 @@ class PackedCausalAttention(torch.autograd.Function):
                 and lse.is_contiguous() and lse.dtype == torch.float32 and cu.numel() == nseq + 1):
             raise RuntimeError(f"unexpected flash-attention log-sum-exp layout {tuple(lse.shape)}")
         ctx.save_for_backward(q, k, v, out, lse, cu)
-        ctx.bounds = bounds
         return out
 
     @staticmethod
@@ -74,11 +88,16 @@ class PackedCausalAttention(torch.autograd.Function):
         T, H, D = q.shape
         lib = _native.load()
         st = torch.cuda.current_stream(q.device).cuda_stream
-        lse2 = torch.empty((H, T), dtype=torch.float32, device=q.device)
         delta = torch.empty((H, T), dtype=torch.float32, device=q.device)
-        _native.check(lib.prl_attn_bwd_preprocess(out.data_ptr(), dout.data_ptr(), lse.data_ptr(), cu.data_ptr(),
-                                                  lse.shape[0], lse.shape[2], lse2.data_ptr(), delta.data_ptr(), T, H,
-                                                  D, st), "prl_attn_bwd_preprocess")
+        if ctx.hip_fwd:
+            lse2 = lse
+            _native.check(lib.prl_attn_bwd_delta(out.data_ptr(), dout.data_ptr(), delta.data_ptr(), T, H, D, st),
+                          "prl_attn_bwd_delta")
+        else:
+            lse2 = torch.empty((H, T), dtype=torch.float32, device=q.device)
+            _native.check(lib.prl_attn_bwd_preprocess(out.data_ptr(), dout.data_ptr(), lse.data_ptr(), cu.data_ptr(),
+                                                      lse.shape[0], lse.shape[2], lse2.data_ptr(), delta.data_ptr(),
+                                                      T, H, D, st), "prl_attn_bwd_preprocess")
         kv_items, q_items, n = _items(ctx.bounds, q.device)
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
         _native.check(lib.prl_attn_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), dout.data_ptr(), lse2.data_ptr(),
