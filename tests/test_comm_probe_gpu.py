@@ -2,7 +2,6 @@
 GradBuckets side stream) on one MI355X: two ranks share cuda:0 over gloo, since RCCL needs one
 GPU per rank; the driver's multi-GPU bench runs the same code over RCCL."""
 
-import os
 import sys
 from pathlib import Path
 
