@@ -137,18 +137,18 @@ def varlen_attention_forward(module, query, key, value, attention_mask, scaling=
         v = v.repeat_interleave(Hq // Hkv, dim=1)
     default_scale = D ** -0.5
     global _varlen_ok
-    if (scaling is None or abs(scaling - default_scale) < 1e-12) and q.is_cuda and _varlen_ok is not False:
+    default_scaling = scaling is None or abs(scaling - default_scale) < 1e-12
+    if hip_bwd and default_scaling:  # the build's kernels: errors propagate (no silent fallback)
+        out = PackedCausalAttention.apply(q.contiguous(), k.contiguous(), v.contiguous(), cu, mx, list(bounds))
+        return out.unsqueeze(0), None
+    if default_scaling and q.is_cuda and _varlen_ok is not False:
         try:
-            q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
-            if hip_bwd:
-                out = PackedCausalAttention.apply(q, k, v, cu, mx, list(bounds))
-            else:
-                from torch.nn.attention.varlen import varlen_attn
+            from torch.nn.attention.varlen import varlen_attn
 
-                out = varlen_attn(q, k, v, cu, cu, mx, mx, is_causal=True)
+            out = varlen_attn(q.contiguous(), k.contiguous(), v.contiguous(), cu, cu, mx, mx, is_causal=True)
             _varlen_ok = True
             return out.unsqueeze(0), None
-        except (RuntimeError, NotImplementedError) as e:
+        except (RuntimeError, NotImplementedError) as e:  # the library's varlen kernels only
             if _varlen_ok is None:
                 logger.warning(f"varlen flash attention unavailable ({e}); using per-sequence SDPA")
             _varlen_ok = False
