@@ -67,7 +67,8 @@ def load_model(args, model_class: str, current_dir: Path, device: torch.device):
     kw["attn_implementation"] = attn
     p = Path(src)
     if p.exists() and not has_weights(p):  # a config-only directory: random init of that architecture
-        model = AutoModelForCausalLM.from_config(AutoConfig.from_pretrained(src), **kw)
+        with torch.device(device):  # on the device: a CPU init of billions of parameters takes minutes
+            model = AutoModelForCausalLM.from_config(AutoConfig.from_pretrained(src), **kw)
     else:
         model = AutoModelForCausalLM.from_pretrained(src, **kw)
     if device.type == "cuda" and args.get("fused_model_ops", True):  # HIP RMSNorm / SwiGLU / RoPE
