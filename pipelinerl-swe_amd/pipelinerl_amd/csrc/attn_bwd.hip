@@ -312,7 +312,10 @@ __global__ __launch_bounds__(256) void attn_bwd_fused(const __bf16* __restrict__
 // running max grows by more than 8), O^T += V^T P with V^T read transposed from the tile image.
 // Writes O [T, H, 128] bf16 and lse2[h][t] = log2 sum_j 2^(c2 S_tj) (the backward's input).
 constexpr float kRescale = 8.0f;
-__global__ __launch_bounds__(256) void attn_fwd(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
+#ifndef PRL_ATTN_FWD_MINB
+#define PRL_ATTN_FWD_MINB 2  // 2 workgroups per CU = 2 waves per SIMD: one wave's softmax under the other's MFMAs
+#endif
+__global__ __launch_bounds__(256, PRL_ATTN_FWD_MINB) void attn_fwd(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
                                                 const __bf16* __restrict__ v, const int32_t* __restrict__ items,
                                                 __bf16* __restrict__ out, float* __restrict__ lse2, int64_t T, int H,
                                                 int Hkv, float c2) {
@@ -353,16 +356,20 @@ __global__ __launch_bounds__(256) void attn_fwd(const __bf16* __restrict__ q, co
       f32x16 St = f32x16{};
 #pragma unroll
       for (int c = 0; c < 8; ++c) St = mfma(row_read(tK, l32, 2 * c + hi), qf[c], St);
-      float x[16];
-      float tmax = -1e30f;
+      // every key of the tile visible to every query of the wave: no mask (all but the diagonal
+      // tile of each wave); otherwise masked scores become -1e30 (p = 0 once m is finite: the first
+      // tile of a sequence always holds key s0, visible to every query)
+      if (!(k0 + TILE - 1 <= qw && k0 + TILE <= s1)) {  // wave-uniform
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int kj = k0 + 8 * (r >> 2) + 4 * hi + (r & 3);
-        const bool ok = qval && kj <= qq && kj < s1;
-        x[r] = ok ? St[r] * c2 : -1e30f;
-        tmax = fmaxf(tmax, x[r]);
+        for (int r = 0; r < 16; ++r) {
+          const int kj = k0 + 8 * (r >> 2) + 4 * hi + (r & 3);
+          if (!(qval && kj <= qq && kj < s1)) St[r] = -1e30f;
+        }
       }
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));  // the other half of this query's keys
+      float tmax = St[0];
+#pragma unroll
+      for (int r = 1; r < 16; ++r) tmax = fmaxf(tmax, St[r]);
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * c2;  // the other half of this query's keys; c2 > 0
       if (tmax > m + kRescale) {  // lazy rebase (wave-uniform decision not needed: per lane)
         const float f = fexp2(m - tmax);
         l *= f;
@@ -376,7 +383,7 @@ __global__ __launch_bounds__(256) void attn_fwd(const __bf16* __restrict__ q, co
       float ps = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float p = fexp2(x[r] - m);
+        const float p = fexp2(__builtin_fmaf(St[r], c2, -m));
         ps += p;
         pb[r >> 3][r & 7] = (__bf16)p;
       }
