@@ -100,6 +100,109 @@ __device__ __forceinline__ void stage_store(const Stage& st, char* base, int tid
   }
 }
 
+#ifndef PRL_ATTN_INTERLEAVE
+#define PRL_ATTN_INTERLEAVE 1  // 0: one tile at a time everywhere (A/B builds, tools/build_variants.py)
+#endif
+// Backward scheduling.  One wave per SIMD (dK^T and dV^T alone hold 128 accumulator registers), so
+// nothing hides a tile's softmax VALU work (~7 vector instructions per MFMA) unless the wave's own
+// MFMAs of ANOTHER tile sit beside it.  Away from the diagonal, tiles are processed in pairs a, b:
+//   [S_a dP_a]   [S_b dP_b  |  softmax a]   [dV dK += a  |  softmax b]   [dV dK += b]
+// the "|" regions are interleaved by sched_group_barrier groups (1 MFMA, its LDS reads, then
+// vector work), so the matrix pipe stays busy through both softmaxes.  The accumulation order of
+// every accumulator is unchanged: the results are bit-identical to one tile at a time.
+#define SGB(mask, n) __builtin_amdgcn_sched_group_barrier(mask, n, 0)
+constexpr int kSgMfma = 0x008, kSgValu = 0x002, kSgDsRead = 0x100;
+__device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0); }
+template <int NMFMA, int NREAD, int NVALU>
+__device__ __forceinline__ void interleave() {
+#pragma unroll
+  for (int i = 0; i < NMFMA; ++i) {
+    SGB(kSgDsRead, NREAD);
+    SGB(kSgMfma, 1);
+    SGB(kSgValu, NVALU);
+  }
+}
+
+// ---- dK / dV role: 32-query tiles against the wave's 32 keys (key on the lane) ----
+__device__ __forceinline__ bool dkdv_live(int kw, int q0, int s1) {  // wave-uniform
+  return !(kw >= s1 || kw > q0 + TILE - 1 || q0 >= s1);
+}
+// S = Q K^T and dP = dO V^T with the key on the lane (K, V rows in registers: kf, vf)
+__device__ __forceinline__ void dkdv_scores(const char* tQ, const char* tdO, const bf16x8* kf, const bf16x8* vf,
+                                            int l32, int hi, f32x16& S, f32x16& dP) {
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    S = mfma(row_read(tQ, l32, 2 * c + hi), kf[c], S);
+    dP = mfma(row_read(tdO, l32, 2 * c + hi), vf[c], dP);
+  }
+}
+// P = 2^(c2 S - L2), dS = P (dP - delta) in bf16, the 16 query rows of this lane's accumulator in
+// 4 runs of 4 consecutive rows.  MASK = false when the whole tile is at or below the diagonal for
+// every key of the wave: rows past the sequence end are zero-filled (zero Q, dO, L, delta) and add
+// exact zeros; keys past the end only touch their own (unwritten) lanes.
+template <bool MASK>
+__device__ __forceinline__ void dkdv_probs(const f32x16& S, const f32x16& dP, const float* tL, const float* tDl, int q0,
+                                           int key, bool kval, int s1, int hi, float c2, bf16x8* pb, bf16x8* sb) {
+#pragma unroll
+  for (int gg = 0; gg < 4; ++gg) {
+    const f32x4 Lr = *reinterpret_cast<const f32x4*>(tL + 8 * gg + 4 * hi);
+    const f32x4 Dr = *reinterpret_cast<const f32x4*>(tDl + 8 * gg + 4 * hi);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = 4 * gg + j;
+      float p = fexp2(__builtin_fmaf(S[r], c2, -Lr[j]));
+      if (MASK) {
+        const int t = q0 + 8 * gg + 4 * hi + j;
+        p = (kval && key <= t && t < s1) ? p : 0.f;
+      }
+      pb[r >> 3][r & 7] = (__bf16)p;
+      sb[r >> 3][r & 7] = (__bf16)(p * (dP[r] - Dr[j]));
+    }
+  }
+}
+// dV^T += dO^T P, dK^T += Q^T dS (unscaled)
+__device__ __forceinline__ void dkdv_acc(const char* tQ, const char* tdO, int lane, const bf16x8* pb, const bf16x8* sb,
+                                         f32x16* dKt, f32x16* dVt) {
+#pragma unroll
+  for (int dc = 0; dc < 4; ++dc)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      dVt[dc] = mfma(tr_operand(tdO, lane, dc, ks), pb[ks], dVt[dc]);
+      dKt[dc] = mfma(tr_operand(tQ, lane, dc, ks), sb[ks], dKt[dc]);
+    }
+}
+// one tile, masked (the diagonal and ragged ends)
+__device__ __forceinline__ void dkdv_tile(const char* tQ, const char* tdO, const float* tL, const float* tDl, int q0,
+                                          const bf16x8* kf, const bf16x8* vf, int key, bool kval, int s1, int lane,
+                                          float c2, f32x16* dKt, f32x16* dVt) {
+  const int hi = lane >> 5, l32 = lane & 31;
+  f32x16 S = f32x16{}, dP = f32x16{};
+  dkdv_scores(tQ, tdO, kf, vf, l32, hi, S, dP);
+  bf16x8 pb[2], sb[2];
+  dkdv_probs<true>(S, dP, tL, tDl, q0, key, kval, s1, hi, c2, pb, sb);
+  dkdv_acc(tQ, tdO, lane, pb, sb, dKt, dVt);
+}
+// two unmasked tiles (a = the stage's first 32 rows, b = the next 32), interleaved
+__device__ __forceinline__ void dkdv_pair(const char* tQ, const char* tdO, const float* tL, const float* tDl,
+                                          const bf16x8* kf, const bf16x8* vf, int key, bool kval, int s1, int lane,
+                                          float c2, f32x16* dKt, f32x16* dVt) {
+  const int hi = lane >> 5, l32 = lane & 31;
+  const char *tQb = tQ + TILE * 256, *tdOb = tdO + TILE * 256;
+  f32x16 Sa = f32x16{}, dPa = f32x16{}, Sb = f32x16{}, dPb = f32x16{};
+  bf16x8 pa[2], sa[2], pb[2], sb[2];
+  dkdv_scores(tQ, tdO, kf, vf, l32, hi, Sa, dPa);
+  sched_fence();
+  dkdv_scores(tQb, tdOb, kf, vf, l32, hi, Sb, dPb);
+  dkdv_probs<false>(Sa, dPa, tL, tDl, 0, key, kval, s1, hi, c2, pa, sa);
+  interleave<16, 1, 8>();
+  sched_fence();
+  dkdv_acc(tQ, tdO, lane, pa, sa, dKt, dVt);
+  dkdv_probs<false>(Sb, dPb, tL + TILE, tDl + TILE, 0, key, kval, s1, hi, c2, pb, sb);
+  interleave<16, 2, 8>();
+  sched_fence();
+  dkdv_acc(tQb, tdOb, lane, pb, sb, dKt, dVt);
+}
+
 // items: int32 triplets (seq_start, seq_end, block_start), block = 128 keys (dkdv) / queries (dq).
 // GQA: k / v / dk / dv have Hkv heads, q / dout / dq have H = rep * Hkv; the dK/dV role of kv head
 // g sweeps the query heads g*rep .. g*rep+rep-1 (all of its group), so dK / dV are complete sums
@@ -157,44 +260,16 @@ __device__ __forceinline__ void attn_bwd_dkdv(const __bf16* __restrict__ q, cons
         ndl = delta[(int64_t)h * T + qn + tid];
       }
     }
+    if (PRL_ATTN_INTERLEAVE && kw < s1 && q00 >= kw + TILE - 1 && q00 + TILE < s1) {  // wave-uniform
+      dkdv_pair(sQ, sdO, sL, sDl, kf, vf, key, kval, s1, lane, c2, dKt, dVt);
+      continue;
+    }
 #pragma unroll 1
     for (int half = 0; half < STAGE / TILE; ++half) {
       const int q0 = q00 + TILE * half;
-      if (kw >= s1 || kw > q0 + TILE - 1 || q0 >= s1) continue;  // wave-uniform
-      const char* tQ = sQ + half * TILE * 256;
-      const char* tdO = sdO + half * TILE * 256;
-      const float* tL = sL + half * TILE;
-      const float* tDl = sDl + half * TILE;
-      f32x16 S = f32x16{}, dP = f32x16{};
-#pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        S = mfma(row_read(tQ, l32, 2 * c + hi), kf[c], S);
-        dP = mfma(row_read(tdO, l32, 2 * c + hi), vf[c], dP);
-      }
-      // the 16 query rows of this lane's accumulator: 4 runs of 4 consecutive rows
-      f32x4 Lr[4], Dr[4];
-#pragma unroll
-      for (int gg = 0; gg < 4; ++gg) {
-        Lr[gg] = *reinterpret_cast<const f32x4*>(tL + 8 * gg + 4 * hi);
-        Dr[gg] = *reinterpret_cast<const f32x4*>(tDl + 8 * gg + 4 * hi);
-      }
-      bf16x8 pb[2], sb[2];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int qi = 8 * (r >> 2) + 4 * hi + (r & 3);
-        const int t = q0 + qi;
-        const bool ok = kval && key <= t && t < s1;
-        const float p = ok ? fexp2(__builtin_fmaf(S[r], c2, -Lr[r >> 2][r & 3])) : 0.f;
-        pb[r >> 3][r & 7] = (__bf16)p;
-        sb[r >> 3][r & 7] = (__bf16)(p * (dP[r] - Dr[r >> 2][r & 3]));
-      }
-#pragma unroll
-      for (int dc = 0; dc < 4; ++dc)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          dVt[dc] = mfma(tr_operand(tdO, lane, dc, ks), pb[ks], dVt[dc]);
-          dKt[dc] = mfma(tr_operand(tQ, lane, dc, ks), sb[ks], dKt[dc]);
-        }
+      if (!dkdv_live(kw, q0, s1)) continue;  // wave-uniform
+      dkdv_tile(sQ + half * TILE * 256, sdO + half * TILE * 256, sL + half * TILE, sDl + half * TILE, q0, kf, vf, key,
+                kval, s1, lane, c2, dKt, dVt);
     }
   }
   }
@@ -210,6 +285,70 @@ __device__ __forceinline__ void attn_bwd_dkdv(const __bf16* __restrict__ q, cons
           scale * dKt[dc][4 * g + 3]);
       st4(dvr + d0, dVt[dc][4 * g], dVt[dc][4 * g + 1], dVt[dc][4 * g + 2], dVt[dc][4 * g + 3]);
     }
+}
+
+// ---- dQ role: 32-key tiles against the wave's 32 queries (query on the lane) ----
+__device__ __forceinline__ bool dq_live(int qw, int k0, int s1, int kend) {  // wave-uniform
+  return !(qw >= s1 || k0 > qw + TILE - 1 || k0 >= kend);
+}
+__device__ __forceinline__ void dq_scores(const char* tK, const char* tV, const bf16x8* qf, const bf16x8* of, int l32,
+                                          int hi, f32x16& St, f32x16& dPt) {
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    St = mfma(row_read(tK, l32, 2 * c + hi), qf[c], St);
+    dPt = mfma(row_read(tV, l32, 2 * c + hi), of[c], dPt);
+  }
+}
+// dS^T in bf16.  MASK = false when every key of the tile is at or below every query of the wave
+// and inside the sequence (a key past the end has S = 0 and would give 2^(-L2), unbounded).
+template <bool MASK>
+__device__ __forceinline__ void dq_probs(const f32x16& St, const f32x16& dPt, int k0, int qq, bool qval, int s1, int hi,
+                                         float c2, float lq, float dq_delta, bf16x8* sb) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    float p = fexp2(__builtin_fmaf(St[r], c2, -lq));
+    if (MASK) {
+      const int kj = k0 + 8 * (r >> 2) + 4 * hi + (r & 3);
+      p = (qval && kj <= qq && kj < s1) ? p : 0.f;
+    }
+    sb[r >> 3][r & 7] = (__bf16)(p * (dPt[r] - dq_delta));
+  }
+}
+__device__ __forceinline__ void dq_acc(const char* tK, int lane, const bf16x8* sb, f32x16* dQt) {
+#pragma unroll
+  for (int dc = 0; dc < 4; ++dc)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) dQt[dc] = mfma(tr_operand(tK, lane, dc, ks), sb[ks], dQt[dc]);
+}
+// one tile, masked
+__device__ __forceinline__ void dq_tile(const char* tK, const char* tV, int k0, const bf16x8* qf, const bf16x8* of,
+                                        int qq, bool qval, int s1, int lane, float c2, float lq, float dq_delta,
+                                        f32x16* dQt) {
+  const int hi = lane >> 5, l32 = lane & 31;
+  f32x16 St = f32x16{}, dPt = f32x16{};
+  dq_scores(tK, tV, qf, of, l32, hi, St, dPt);
+  bf16x8 sb[2];
+  dq_probs<true>(St, dPt, k0, qq, qval, s1, hi, c2, lq, dq_delta, sb);
+  dq_acc(tK, lane, sb, dQt);
+}
+// two unmasked tiles, interleaved as in dkdv_pair
+__device__ __forceinline__ void dq_pair(const char* tK, const char* tV, const bf16x8* qf, const bf16x8* of, int qq,
+                                        bool qval, int s1, int lane, float c2, float lq, float dq_delta, f32x16* dQt) {
+  const int hi = lane >> 5, l32 = lane & 31;
+  const char *tKb = tK + TILE * 256, *tVb = tV + TILE * 256;
+  f32x16 Sa = f32x16{}, dPa = f32x16{}, Sb = f32x16{}, dPb = f32x16{};
+  bf16x8 sa[2], sb[2];
+  dq_scores(tK, tV, qf, of, l32, hi, Sa, dPa);
+  sched_fence();
+  dq_scores(tKb, tVb, qf, of, l32, hi, Sb, dPb);
+  dq_probs<false>(Sa, dPa, 0, qq, qval, s1, hi, c2, lq, dq_delta, sa);
+  interleave<16, 1, 5>();
+  sched_fence();
+  dq_acc(tK, lane, sa, dQt);
+  dq_probs<false>(Sb, dPb, 0, qq, qval, s1, hi, c2, lq, dq_delta, sb);
+  interleave<8, 2, 10>();
+  sched_fence();
+  dq_acc(tKb, lane, sb, dQt);
 }
 
 __device__ __forceinline__ void attn_bwd_dq(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
@@ -248,30 +387,15 @@ __device__ __forceinline__ void attn_bwd_dq(const __bf16* __restrict__ q, const 
       nk = stage_load(k, rsk, g, k00 + STAGE, s1, tid);
       nv = stage_load(v, rsk, g, k00 + STAGE, s1, tid);
     }
+    if (PRL_ATTN_INTERLEAVE && qw < s1 && k00 + STAGE - 1 <= qw && k00 + STAGE <= s1) {  // wave-uniform
+      dq_pair(sK, sV, qf, of, qq, qval, s1, lane, c2, lq, dq_delta, dQt);
+      continue;
+    }
 #pragma unroll 1
     for (int half = 0; half < STAGE / TILE; ++half) {
       const int k0 = k00 + TILE * half;
-      if (qw >= s1 || k0 > qw + TILE - 1 || k0 >= kend) continue;  // wave-uniform
-      const char* tK = sK + half * TILE * 256;
-      const char* tV = sV + half * TILE * 256;
-      f32x16 St = f32x16{}, dPt = f32x16{};
-#pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        St = mfma(row_read(tK, l32, 2 * c + hi), qf[c], St);
-        dPt = mfma(row_read(tV, l32, 2 * c + hi), of[c], dPt);
-      }
-      bf16x8 sb[2];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int kj = k0 + 8 * (r >> 2) + 4 * hi + (r & 3);
-        const bool ok = qval && kj <= qq && kj < s1;
-        const float p = ok ? fexp2(__builtin_fmaf(St[r], c2, -lq)) : 0.f;
-        sb[r >> 3][r & 7] = (__bf16)(p * (dPt[r] - dq_delta));
-      }
-#pragma unroll
-      for (int dc = 0; dc < 4; ++dc)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) dQt[dc] = mfma(tr_operand(tK, lane, dc, ks), sb[ks], dQt[dc]);
+      if (!dq_live(qw, k0, s1, kend)) continue;  // wave-uniform
+      dq_tile(sK + half * TILE * 256, sV + half * TILE * 256, k0, qf, of, qq, qval, s1, lane, c2, lq, dq_delta, dQt);
     }
   }
   if (!qval) return;
