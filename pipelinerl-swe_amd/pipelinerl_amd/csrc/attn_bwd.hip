@@ -113,16 +113,22 @@ __device__ __forceinline__ void stage_store(const Stage& st, char* base, int tid
 #define SGB(mask, n) __builtin_amdgcn_sched_group_barrier(mask, n, 0)
 constexpr int kSgMfma = 0x008, kSgValu = 0x002, kSgDsRead = 0x100;
 __device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0); }
+#ifndef PRL_ATTN_LEAD
+#define PRL_ATTN_LEAD 8  // tools/build_variants.py sweep: 0 / 1 / 3 / 6 / 8 / 12 / 16 -> 8 (6-12 within 1 %)
+#endif
+// NMFMA groups of (1 MFMA, NVALU vector instructions); the LDS reads run PRL_ATTN_LEAD MFMAs ahead
+// of the MFMA that consumes them (NREAD reads per MFMA), so their latency is not in front of it
 template <int NMFMA, int NREAD, int NVALU>
 __device__ __forceinline__ void interleave() {
+  constexpr int kLead = PRL_ATTN_LEAD < NMFMA ? PRL_ATTN_LEAD : NMFMA;
+  SGB(kSgDsRead, NREAD * kLead);
 #pragma unroll
   for (int i = 0; i < NMFMA; ++i) {
-    SGB(kSgDsRead, NREAD);
     SGB(kSgMfma, 1);
-    SGB(kSgValu, NVALU);
+    if (i + kLead < NMFMA) SGB(kSgDsRead, NREAD);
+    if (NVALU) SGB(kSgValu, NVALU);
   }
 }
-
 // ---- dK / dV role: 32-query tiles against the wave's 32 keys (key on the lane) ----
 __device__ __forceinline__ bool dkdv_live(int kw, int q0, int s1) {  // wave-uniform
   return !(kw >= s1 || kw > q0 + TILE - 1 || q0 >= s1);
