@@ -445,6 +445,51 @@ constexpr float kRescale = 8.0f;
 #ifndef PRL_ATTN_FWD_MINB
 #define PRL_ATTN_FWD_MINB 2  // 2 workgroups per CU = 2 waves per SIMD: one wave's softmax under the other's MFMAs
 #endif
+// one 32-key tile of the forward: S^T = K Q^T, online softmax update of (m, l, O^T), O^T += V^T P.
+// MASK: masked scores become -1e30 (p = 0 once m is finite: the first tile of a sequence always
+// holds key s0, visible to every query)
+template <bool MASK>
+__device__ __forceinline__ void fwd_tile(const char* tK, const char* tV, int k0, const bf16x8* qf, int qq, bool qval,
+                                         int s1, int lane, float c2, float& m, float& l, f32x16* Ot) {
+  const int hi = lane >> 5, l32 = lane & 31;
+  f32x16 St = f32x16{};
+#pragma unroll
+  for (int c = 0; c < 8; ++c) St = mfma(row_read(tK, l32, 2 * c + hi), qf[c], St);
+  if (MASK) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int kj = k0 + 8 * (r >> 2) + 4 * hi + (r & 3);
+      if (!(qval && kj <= qq && kj < s1)) St[r] = -1e30f;
+    }
+  }
+  float tmax = St[0];
+#pragma unroll
+  for (int r = 1; r < 16; ++r) tmax = fmaxf(tmax, St[r]);
+  tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * c2;  // the other half of this query's keys; c2 > 0
+  if (tmax > m + kRescale) {  // lazy rebase, per lane
+    const float f = fexp2(m - tmax);
+    l *= f;
+#pragma unroll
+    for (int dc = 0; dc < 4; ++dc)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) Ot[dc][r] *= f;
+    m = tmax;
+  }
+  bf16x8 pb[2];
+  float ps = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float p = fexp2(__builtin_fmaf(St[r], c2, -m));
+    ps += p;
+    pb[r >> 3][r & 7] = (__bf16)p;
+  }
+  l += ps + __shfl_xor(ps, 32, 64);
+#pragma unroll
+  for (int dc = 0; dc < 4; ++dc)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) Ot[dc] = mfma(tr_operand(tV, lane, dc, ks), pb[ks], Ot[dc]);
+}
+
 __global__ __launch_bounds__(256, PRL_ATTN_FWD_MINB) void attn_fwd(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
                                                 const __bf16* __restrict__ v, const int32_t* __restrict__ items,
                                                 __bf16* __restrict__ out, float* __restrict__ lse2, int64_t T, int H,
@@ -481,47 +526,12 @@ __global__ __launch_bounds__(256, PRL_ATTN_FWD_MINB) void attn_fwd(const __bf16*
     for (int half = 0; half < STAGE / TILE; ++half) {
       const int k0 = k00 + TILE * half;
       if (qw >= s1 || k0 > qw + TILE - 1 || k0 >= kend) continue;  // wave-uniform
-      const char* tK = sK + half * TILE * 256;
-      const char* tV = sV + half * TILE * 256;
-      f32x16 St = f32x16{};
-#pragma unroll
-      for (int c = 0; c < 8; ++c) St = mfma(row_read(tK, l32, 2 * c + hi), qf[c], St);
-      // every key of the tile visible to every query of the wave: no mask (all but the diagonal
-      // tile of each wave); otherwise masked scores become -1e30 (p = 0 once m is finite: the first
-      // tile of a sequence always holds key s0, visible to every query)
-      if (!(k0 + TILE - 1 <= qw && k0 + TILE <= s1)) {  // wave-uniform
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int kj = k0 + 8 * (r >> 2) + 4 * hi + (r & 3);
-          if (!(qval && kj <= qq && kj < s1)) St[r] = -1e30f;
-        }
-      }
-      float tmax = St[0];
-#pragma unroll
-      for (int r = 1; r < 16; ++r) tmax = fmaxf(tmax, St[r]);
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * c2;  // the other half of this query's keys; c2 > 0
-      if (tmax > m + kRescale) {  // lazy rebase (wave-uniform decision not needed: per lane)
-        const float f = fexp2(m - tmax);
-        l *= f;
-#pragma unroll
-        for (int dc = 0; dc < 4; ++dc)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) Ot[dc][r] *= f;
-        m = tmax;
-      }
-      bf16x8 pb[2];
-      float ps = 0.f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = fexp2(__builtin_fmaf(St[r], c2, -m));
-        ps += p;
-        pb[r >> 3][r & 7] = (__bf16)p;
-      }
-      l += ps + __shfl_xor(ps, 32, 64);
-#pragma unroll
-      for (int dc = 0; dc < 4; ++dc)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) Ot[dc] = mfma(tr_operand(tV, lane, dc, ks), pb[ks], Ot[dc]);
+      // every key of the tile visible to every query of the wave: the unmasked body (all but the
+      // diagonal tile of each wave); wave-uniform, two separate code paths
+      if (k0 + TILE - 1 <= qw && k0 + TILE <= s1)
+        fwd_tile<false>(sK + half * TILE * 256, sV + half * TILE * 256, k0, qf, qq, qval, s1, lane, c2, m, l, Ot);
+      else
+        fwd_tile<true>(sK + half * TILE * 256, sV + half * TILE * 256, k0, qf, qq, qval, s1, lane, c2, m, l, Ot);
     }
   }
   if (!qval) return;
