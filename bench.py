@@ -22,6 +22,12 @@ under "trainer_step" (pipelinerl_amd/trainer_probe.py): Qwen2.5-1.5B shapes (ran
 RMSNorm / SwiGLU / RoPE, label-row lm_head + fused loss head, backward), the bucketed RCCL
 gradient all-reduce overlapped with the last backward, clip, fused AdamW.
 
+At N > 1, last, BASELINE.json configs[3] (C4) is measured under "split_pipeline": ranks
+[0, N/2) train Qwen2.5-7B shapes data-parallel while ranks [N/2, N) act as actors; trainer rank 0
+broadcasts each step's weights to them (WeightUpdateManager -> WorkerExtension) while the
+trainers run the next step.  The trainers' step time with and without the broadcast in flight
+gives hidden_frac (1.0 = the broadcast latency is fully overlapped).
+
 Prints ONE JSON line (rank 0).  roofline.achieved = algorithmic bytes per launch
 (T*V*2 read + T*V*2 dlogits write + 37*T side data) / the average duration
 of the prl_grpo_forward launch measured with HIP events on its stream.
@@ -119,15 +125,25 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-comm-probe", action="store_true", help="N > 1: skip the all-reduce / broadcast probes")
     ap.add_argument("--no-trainer-step", action="store_true", help="skip the full trainer-step probe")
+    ap.add_argument("--no-split-pipeline", action="store_true",
+                    help="N > 1: skip the split trainer/actor probe (configs[3]: 7B, overlapped weight broadcast)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # PRL_BENCH_REHEARSE=gloo: rehearsal of the N > 1 control flow on ONE GPU (every rank on
+    # cuda:0, gloo collectives); the measured multi-GPU runs use RCCL, one GPU per rank
+    rehearse = os.environ.get("PRL_BENCH_REHEARSE") == "gloo"
+    if rehearse:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     from pipelinerl_amd import _native
     from pipelinerl_amd.finetune.rl.fused import GrpoParams, grpo_loss
@@ -201,6 +217,25 @@ def main():
         trainer = trainer_step_probe("1.5b", tokens=T, micro_batches=2, steps=2, warmup=1, device=dev,
                                      fused_head=True)
 
+    split = None
+    if world > 1 and not args.no_split_pipeline:
+        # configs[3] (C4): half the ranks train Qwen2.5-7B shapes data-parallel, the other half are
+        # actors receiving every step's weights from trainer rank 0 while the trainers run the next
+        # step; reports the step time with and without the broadcast in flight (hidden_frac)
+        from pipelinerl_amd import comm_probe
+        from pipelinerl_amd.trainer_probe import TrainerStep, split_pipeline_probe
+
+        logits = fields = None
+        torch.cuda.empty_cache()
+        actors = world // 2
+        split = split_pipeline_probe(
+            actors, steps=2, warmup=1, device=dev,
+            make_trainer=lambda g: TrainerStep("7b", tokens=16384, micro_batches=2, device=dev, group=g),
+            make_actor_module=lambda: comm_probe.ShapedModule(comm_probe.qwen2_param_shapes("7b"), device=dev,
+                                                              fill=0.0))
+        split["model"] = "Qwen2.5-7b shapes (random init, bf16), 2 x 16384-token micro-batches per trainer rank"
+        torch.cuda.empty_cache()
+
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
         tokens_total = T * world * args.steps
@@ -238,6 +273,8 @@ def main():
             out["exchange"] = comm
         if trainer is not None:
             out["trainer_step"] = trainer
+        if split is not None:
+            out["split_pipeline"] = split
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

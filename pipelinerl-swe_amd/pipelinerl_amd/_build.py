@@ -22,6 +22,7 @@ INCLUDE = REPO / "include"
 CSRC = PKG / "csrc"
 LIB = PKG / "libprl_hip.so"
 COMM_LIB = PKG / "libprl_comm.so"
+GEMM_LIB = PKG / "libprl_gemm.so"
 ARCH = "gfx950"
 SOURCES = ["grpo_loss.hip", "flat_pack.hip", "model_ops.hip", "attn_bwd.hip"]
 
@@ -59,6 +60,26 @@ def build_comm(force: bool = False) -> Path:
         raise RuntimeError(f"hipcc failed for comm.cpp:\n{r.stderr[-8000:]}")
     os.replace(tmp, COMM_LIB)
     return COMM_LIB
+
+
+def build_gemm(force: bool = False) -> Path:
+    """libprl_gemm.so: host code over hipBLASLt (no device code).  It does not link hipBLASLt: it
+    dlopens the ROCm installation's copy (path baked in here) at first use, next to the copy torch
+    bundles; its HIP runtime dependency resolves to the one torch loaded."""
+    src, hdr = CSRC / "gemm.cpp", INCLUDE / "prl_gemm.h"
+    if not force and GEMM_LIB.exists() and GEMM_LIB.stat().st_mtime > max(src.stat().st_mtime,
+                                                                           hdr.stat().st_mtime):
+        return GEMM_LIB
+    rocm = Path(hipcc()).resolve().parents[1]
+    tmp = GEMM_LIB.with_suffix(".so.tmp")
+    cmd = [hipcc(), "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", f"--offload-arch={ARCH}", f"-I{INCLUDE}",
+           f"-I{rocm / 'include'}", f"-DPRL_HIPBLASLT_PATH=\"{rocm / 'lib' / 'libhipblaslt.so.1'}\"", str(src),
+           "-o", str(tmp), "-ldl"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for gemm.cpp:\n{r.stderr[-8000:]}")
+    os.replace(tmp, GEMM_LIB)
+    return GEMM_LIB
 
 
 def build(force: bool = False, resource_usage: bool = False, verbose: bool = False,
@@ -109,3 +130,4 @@ if __name__ == "__main__":
     out = build(force=True, resource_usage="--resource-usage" in sys.argv, verbose=True)
     print(out)
     print(build_comm(force=True))
+    print(build_gemm(force=True))

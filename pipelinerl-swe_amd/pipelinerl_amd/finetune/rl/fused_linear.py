@@ -9,8 +9,8 @@ final hidden states and the ``lm_head`` weight and, for the label rows only, in 
 
   logits_c  = h_c @ W^T                      (hipBLASLt GEMM, [c, V])
   prl_grpo_forward_rows(logits_c)            (HIP loss kernel; dlogits written in place)
-  dh_c      = dlogits_c @ W                  (GEMM)
-  dW       += dlogits_c^T @ h_c              (GEMM, fp32 accumulator)
+  dh_c      = dlogits_c @ W                  (GEMM, prl_gemm for bf16)
+  dW       += dlogits_c^T @ h_c              (GEMM, fp32 accumulator, prl_gemm for bf16)
 
 then one ``prl_grpo_stats`` pass over all rows.  Peak extra memory is one [c, V] chunk plus an
 fp32 [V, H] accumulator instead of two [T, V] tensors, and the three lm_head GEMMs and the
@@ -28,7 +28,7 @@ import ctypes
 
 import torch
 
-from ... import _native
+from ... import _native, gemm
 from ..._native import NSTAT, PRL_BF16, PRL_F32
 from .fused import GrpoParams, _workspace
 
@@ -87,6 +87,7 @@ class LinearGrpoLossFn(torch.autograd.Function):
             hrow = qsel + torch.div(qsel, L - 1, rounding_mode="floor")  # q = b*(L-1)+t -> b*L+t
             R = int(qsel.numel())
             step = max(1, int(chunk_rows))
+            use_prl = w.dtype == torch.bfloat16 and w.is_contiguous() and Hd % 8 == 0 and V % 8 == 0
             for a in range(0, R, step):
                 idx = hrow[a:a + step]
                 qc = qsel[a:a + step].contiguous()
@@ -98,7 +99,10 @@ class LinearGrpoLossFn(torch.autograd.Function):
                 _native.check(lib.prl_grpo_forward_rows(ctypes.byref(cb), ctypes.byref(cp), qc.data_ptr(),
                                                         qc.numel(), ctypes.byref(co), stream),
                               "prl_grpo_forward_rows")
-                if write_grad:
+                if write_grad and use_prl:  # ROCm hipBLASLt (include/prl_gemm.h)
+                    dh.index_copy_(0, idx, gemm.linear_dgrad(lg, w))
+                    gemm.linear_wgrad(lg, hc, out=dw, accumulate=True)
+                elif write_grad:
                     dh.index_copy_(0, idx, torch.mm(lg, w))
                     _accumulate_dw(dw, lg, hc)
                 del lg, hc

@@ -77,59 +77,100 @@ def rl_config(samples_per_step: int, fused_head: bool = False):
                     batch_size=samples_per_step, fused_lm_head=fused_head)
 
 
+def _sync(device) -> None:
+    if torch.device(device).type == "cuda":
+        torch.cuda.synchronize(device)
+
+
+class TrainerStep:
+    """One rank's optimizer step as the trainer loop runs it (finetune_loop.py rl_finetuning_worker):
+    ``micro_batches`` packed micro-batches (the last one armed so the bucketed gradient all-reduce
+    over ``group`` overlaps its backward), clip 0.3, the weight manager's snapshot fence, AdamW.
+
+    ``model`` / ``step_fn`` default to the product path (Qwen2 shapes on the device, rl_step with
+    the HIP loss head); tests inject a CPU model and loss to exercise the control flow on gloo.
+    """
+
+    def __init__(self, name: str = "1.5b", tokens: int = 16384, seq: int = 2048, prompt: int = 256,
+                 micro_batches: int = 4, device=None, fused_head: bool = False, grad_ckpt: bool = False,
+                 fused_ops: bool = True, group=None, model=None, step_fn=None, vocab: int | None = None):
+        from .finetune.grad_sync import GradBuckets
+        from .finetune.optim import get_optimizer
+
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.group = group
+        world = dist.get_world_size(group) if dist.is_initialized() else 1
+        rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.world, self.tokens, self.micro_batches = world, tokens, micro_batches
+        self.model = model if model is not None else qwen2_model(name, self.device, grad_ckpt, fused_ops)
+        if step_fn is None:
+            from .finetune.rl import rl_step as step_fn
+        self.step_fn = step_fn
+        self.opt = get_optimizer("adamw_torch", self.model, 1e-6, 0.01)
+        self.grads = GradBuckets(list(self.model.parameters()), group=group) if world > 1 else None
+        V = vocab or QWEN[name]["vocab_size"]
+        self.batches = [packed_batch(tokens, seq, prompt, V, self.device, seed=rank * 97 + i)
+                        for i in range(micro_batches)]
+        self.cfg = rl_config(micro_batches * (tokens // seq) * world, fused_head)
+
+    def step(self, wum=None, version: int = 0) -> None:
+        for i, b in enumerate(self.batches):
+            if self.grads is not None and i == len(self.batches) - 1:
+                self.grads.arm()
+            loss, _ = self.step_fn(self.model, b, 0, 100, self.cfg)
+            loss.backward()
+        if self.grads is not None:
+            self.grads.finish()
+        torch.nn.utils.clip_grad_norm_(self.model.parameters(), 0.3)
+        if wum is not None:
+            wum.before_optimizer_step()  # the previous snapshot is read before params change
+        self.opt.step()
+        if self.grads is not None:
+            self.grads.zero_()
+        else:
+            self.opt.zero_grad(set_to_none=True)
+        if wum is not None:
+            wum.send_weight_update(version)  # returns at once: overlapped with the next step
+
+    def timed(self, steps: int, warmup: int, wum=None, version0: int = 0) -> float:
+        """Seconds per optimizer step (max over the group's ranks)."""
+        v = version0
+        for _ in range(warmup):
+            v += 1
+            self.step(wum, v)
+        _sync(self.device)
+        if self.world > 1:
+            dist.barrier(self.group)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            v += 1
+            self.step(wum, v)
+        _sync(self.device)
+        if self.world > 1:
+            dist.barrier(self.group)
+        dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=self.device)
+        if self.world > 1:
+            dist.all_reduce(dt, op=dist.ReduceOp.MAX, group=self.group)
+        return float(dt) / steps
+
+    def close(self) -> None:
+        if self.grads is not None:
+            self.grads.remove()
+        self.model = self.opt = self.grads = self.batches = None
+        if self.device.type == "cuda":
+            torch.cuda.empty_cache()
+
+
 def trainer_step_probe(name: str = "1.5b", tokens: int = 16384, seq: int = 2048, prompt: int = 256,
                        micro_batches: int = 4, steps: int = 3, warmup: int = 1, device=None,
                        fused_head: bool = False, grad_ckpt: bool = False, fused_ops: bool = True) -> dict:
-    from .finetune.grad_sync import GradBuckets
-    from .finetune.optim import get_optimizer
-    from .finetune.rl import rl_step
-
     device = device or torch.device("cuda", torch.cuda.current_device())
-    world = dist.get_world_size() if dist.is_initialized() else 1
-    rank = dist.get_rank() if dist.is_initialized() else 0
     torch.cuda.reset_peak_memory_stats(device)
-    model = qwen2_model(name, device, grad_ckpt, fused_ops)
-    opt = get_optimizer("adamw_torch", model, 1e-6, 0.01)
-    grads = GradBuckets(list(model.parameters())) if world > 1 else None
-    batches = [packed_batch(tokens, seq, prompt, QWEN[name]["vocab_size"], device, seed=rank * 97 + i)
-               for i in range(micro_batches)]
-    cfg = rl_config(micro_batches * (tokens // seq) * world, fused_head)
-
-    def one_step():
-        for i, b in enumerate(batches):
-            if grads is not None and i == len(batches) - 1:
-                grads.arm()
-            loss, _ = rl_step(model, b, 0, 100, cfg)
-            loss.backward()
-        if grads is not None:
-            grads.finish()
-        torch.nn.utils.clip_grad_norm_(model.parameters(), 0.3)
-        opt.step()
-        if grads is not None:
-            grads.zero_()
-        else:
-            opt.zero_grad(set_to_none=True)
-
-    for _ in range(warmup):
-        one_step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        one_step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
-    if world > 1:
-        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-    sec = float(dt) / steps
+    ts = TrainerStep(name, tokens, seq, prompt, micro_batches, device, fused_head, grad_ckpt, fused_ops)
+    sec = ts.timed(steps, warmup)
+    world = ts.world
     peak = torch.cuda.max_memory_allocated(device) / 1e9
-    if grads is not None:
-        grads.remove()
-    del model, opt, grads, batches
-    torch.cuda.empty_cache()
+    ts.close()
     total = tokens * micro_batches * world
     return {"model": f"Qwen2.5-{name} shapes (random init, bf16)", "tokens_per_micro_batch": tokens,
             "micro_batches_per_step": micro_batches, "seq_len": seq, "prompt_len": prompt,
@@ -137,3 +178,79 @@ def trainer_step_probe(name: str = "1.5b", tokens: int = 16384, seq: int = 2048,
             "ms_per_optimizer_step": round(sec * 1e3, 2),
             "tokens_per_s": round(total / sec, 1), "tokens_per_s_per_gpu": round(total / sec / world, 1),
             "peak_mem_gb": round(peak, 2), "steps": steps, "warmup": warmup}
+
+
+def split_pipeline_probe(actors: int, steps: int = 2, warmup: int = 1, device=None, transport: str = "bucketed",
+                         bucket_bytes: int = 256 << 20, make_trainer=None, make_actor_module=None,
+                         packer=None) -> dict:
+    """BASELINE.json configs[3] (C4) on one node: ranks [0, W-actors) train data-parallel, ranks
+    [W-actors, W) are actors.  Trainer rank 0 broadcasts every optimizer step's weights to the
+    actors over their own group (WeightUpdateManager -> WorkerExtension.receive_weight_update,
+    finetune_loop.py:174-256 / vllm1.py:81-94) while the trainers run the next step.
+
+    The trainers' step is timed twice: without weight updates, then with one update per step in
+    flight.  ``hidden_frac`` = 1 - (extra step time) / (broadcast latency): 1.0 means the
+    broadcast is fully overlapped (north_star), 0 means it is serialised as in the reference.
+
+    make_trainer(dp_group) -> TrainerStep; make_actor_module() -> a module whose
+    named_parameters() match the trainer model's (actors hold the inference copy).
+    All ranks must call this collectively.  Returns the same dict on every rank.
+    """
+    from .actor import StandaloneWorker
+    from .weight_update import ParameterInfo, WeightUpdateManager, WeightUpdateRequest
+
+    world, rank = dist.get_world_size(), dist.get_rank()
+    if not 1 <= actors < world:
+        raise ValueError(f"need 1 <= actors < world ({actors}, {world})")
+    n_tr = world - actors
+    trainer_ranks = list(range(n_tr))
+    # every rank creates every group, in the same order (torch.distributed requirement)
+    dp_group = dist.new_group(trainer_ranks)
+    bc_group = dist.new_group([0] + list(range(n_tr, world)))
+    is_trainer = rank < n_tr
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    result = {}
+    nupdates = warmup + steps
+    if is_trainer:
+        ts = make_trainer(dp_group)
+        infos = [ParameterInfo(name=n, shape=list(p.shape), dtype=str(torch.bfloat16))
+                 for n, p in ts.model.named_parameters()]
+        sec_plain = ts.timed(steps, warmup)
+        wum = None
+        if rank == 0:
+            wum = WeightUpdateManager([], ts.model, None, bc_group, transport=transport, bucket_bytes=bucket_bytes,
+                                      overlap=True, packer=packer, write_message=lambda s, m: None)
+            dist.broadcast_object_list([[i.model_dump() for i in infos]], src=0, group=bc_group)
+        lat = []
+        sec_bcast = ts.timed(steps, warmup, wum=wum)
+        if wum is not None:
+            wum.wait()
+            lat = [wum.last_latency_s]
+            wum.close()
+        ts.close()
+        result = {"plain_s": sec_plain, "bcast_s": sec_bcast, "latency_s": lat[0] if lat else 0.0}
+    else:
+        holder = [None]
+        dist.broadcast_object_list(holder, src=0, group=bc_group)
+        infos = [ParameterInfo(**d) for d in holder[0]]
+        module = make_actor_module()
+        worker = StandaloneWorker(module, rank=0, device=dev)
+        worker.process_group = bc_group
+        for v in range(nupdates):
+            worker.receive_weight_update(WeightUpdateRequest(
+                version=v + 1, parameters_info=infos, transport=transport,
+                bucket_bytes=bucket_bytes if transport == "bucketed" else 0))
+        _sync(dev)
+        result = {"received": nupdates}
+    # rank 0's view to everyone (object collective on the default group)
+    out = [result]
+    dist.broadcast_object_list(out, src=0)
+    r0 = out[0]
+    extra = max(0.0, r0["bcast_s"] - r0["plain_s"])
+    lat = r0["latency_s"]
+    nbytes = sum(2 * int(torch.Size(i.shape).numel()) for i in infos)
+    return {"trainers": n_tr, "actors": actors, "transport": transport, "updates": nupdates,
+            "ms_per_step_no_broadcast": round(r0["plain_s"] * 1e3, 2),
+            "ms_per_step_with_broadcast": round(r0["bcast_s"] * 1e3, 2),
+            "broadcast_latency_ms": round(lat * 1e3, 2), "broadcast_bytes": nbytes,
+            "hidden_frac": round(1.0 - min(1.0, extra / lat), 4) if lat > 0 else None}

@@ -66,3 +66,25 @@ def test_comm_library_exports_header_symbols():
     assert lib.prl_comm_error_string(3001).decode() == "invalid argument"
     h = ctypes.c_void_p()
     assert lib.prl_comm_init(None, 0, 1, 0, ctypes.byref(h)) == 3001  # argument checks before any HIP call
+
+
+def test_gemm_library_exports_header_symbols():
+    """libprl_gemm.so (hipBLASLt C ABI, include/prl_gemm.h) loads without a GPU, exports every
+    declared function, and rejects bad arguments before opening hipBLASLt or touching a device."""
+    from pipelinerl_amd import gemm
+
+    lib = gemm.load()
+    text = gemm.HEADER_PATH.read_text()
+    declared = sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(prl_gemm_\w+)\s*\(", text, flags=re.M)))
+    assert len(declared) >= 5
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert lib.prl_gemm_abi_version() == 1
+    assert lib.prl_gemm_error_string(4001).decode() == "invalid argument"
+    # m = 0, a bad op, null pointers, lda < m: all PRL_GEMM_E_INVALID
+    assert lib.prl_gemm_bf16(0, 0, 0, 4, 4, 1, 4, 1, 4, 0.0, 1, 4, 1, -1, None) == 4001
+    assert lib.prl_gemm_bf16(2, 0, 4, 4, 4, 1, 4, 1, 4, 0.0, 1, 4, 1, -1, None) == 4001
+    assert lib.prl_gemm_bf16(0, 0, 4, 4, 4, None, 4, 1, 4, 0.0, 1, 4, 1, -1, None) == 4001
+    assert lib.prl_gemm_bf16(0, 0, 8, 4, 4, 1, 4, 1, 4, 0.0, 1, 8, 1, -1, None) == 4001
+    assert lib.prl_gemm_bf16(0, 0, 4, 4, 4, 1, 4, 1, 4, 0.5, 1, 4, 1, -1, None) == 4001  # beta in {0, 1}
+    assert lib.prl_gemm_heuristic_index(0, 0, 0, 1, 1, 1, 1, 1, 1, 0.0) == -1

@@ -1,0 +1,73 @@
+"""prl_gemm (include/prl_gemm.h: the ROCm hipBLASLt through a C ABI) on MI355X: the three linear
+passes and the fp32 accumulating weight gradient against fp32 GEMMs of the same bf16 operands,
+ragged shapes, strided-free views, a tuned solution index, and the library it runs on."""
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _rand(shape, g, scale=1.0):
+    return (torch.randn(shape, generator=g, device=DEV) * scale).to(torch.bfloat16)
+
+
+def _close(got, ref, rtol=1e-2):
+    err = float((got.float() - ref).abs().max())
+    assert err <= rtol * float(ref.abs().max()) + 1e-6, err
+
+
+def test_library_is_rocm_hipblaslt():
+    from pipelinerl_amd import gemm
+
+    s = gemm.library()
+    assert "libhipblaslt.so" in s and "torch" not in s, s
+
+
+@pytest.mark.parametrize("T,N,K", [(4096, 1536, 1536), (1000, 256, 1536), (37, 24, 8), (8192, 8960, 1536)])
+def test_linear_passes_match_fp32(T, N, K):
+    from pipelinerl_amd import gemm
+
+    g = torch.Generator(device=DEV).manual_seed(T + N + K)
+    x, w, dy = _rand((T, K), g), _rand((N, K), g, 0.05), _rand((T, N), g)
+    _close(gemm.linear_fwd(x, w), x.float() @ w.float().t())
+    _close(gemm.linear_dgrad(dy, w), dy.float() @ w.float())
+    _close(gemm.linear_wgrad(dy, x), dy.float().t() @ x.float())
+    # leading batch dims are flattened like F.linear's
+    y3 = gemm.linear_fwd(x.view(1, T, K), w)
+    assert y3.shape == (1, T, N) and torch.equal(y3[0], gemm.linear_fwd(x, w))
+
+
+def test_wgrad_fp32_accumulates_over_chunks():
+    from pipelinerl_amd import gemm
+
+    g = torch.Generator(device=DEV).manual_seed(3)
+    V, H, T = 4096, 256, 3000
+    h, dl = _rand((T, H), g), _rand((T, V), g)
+    dw = torch.zeros((V, H), dtype=torch.float32, device=DEV)
+    for a in range(0, T, 1024):  # ragged last chunk
+        gemm.linear_wgrad(dl[a:a + 1024], h[a:a + 1024], out=dw, accumulate=True)
+    ref = dl.double().t() @ h.double()
+    assert float((dw.double() - ref).abs().max()) <= 1e-4 * float(ref.abs().max())
+
+
+def test_solution_index_and_errors():
+    from pipelinerl_amd import gemm
+
+    lib = gemm.load()
+    g = torch.Generator(device=DEV).manual_seed(9)
+    T, N, K = 2048, 512, 256
+    x, dy = _rand((T, K), g), _rand((T, N), g)
+    idx = lib.prl_gemm_heuristic_index(0, 1, K, N, T, K, N, K, 1, 0.0)
+    assert idx >= 0
+    ref = gemm.linear_wgrad(dy, x)
+    out = torch.empty_like(ref)
+    gemm.gemm(0, 1, K, N, T, x, K, dy, N, out, K, solution=idx)  # the heuristic's own index
+    assert torch.equal(out, ref)
+    gemm.gemm(0, 1, K, N, T, x, K, dy, N, out, K, solution=10 ** 9)  # unknown index: heuristic
+    assert torch.equal(out, ref)
+    with pytest.raises(gemm.GemmError):
+        gemm.linear_wgrad(dy, x, out=torch.empty((N, K + 1), dtype=torch.bfloat16, device=DEV))
+    with pytest.raises(gemm.GemmError):
+        gemm.gemm(0, 0, K, N, T, x.float(), K, dy, N, out, K)

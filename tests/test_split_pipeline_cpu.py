@@ -1,0 +1,77 @@
+"""The split trainer / actor probe (trainer_probe.split_pipeline_probe, BASELINE configs[3]) on
+CPU gloo: W - A trainer ranks train data-parallel on a tiny bf16 Qwen2 with the test-only torch
+loss while trainer rank 0 broadcasts every step's weights to A actor ranks.  Checks the group
+layout, that every update is received (the actors end with the trainer's weights, bit-exact)
+and that the report is complete."""
+
+import os
+import sys
+from pathlib import Path
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _tiny():
+    from transformers import Qwen2Config, Qwen2ForCausalLM
+
+    torch.manual_seed(0)
+    cfg = Qwen2Config(vocab_size=96, hidden_size=32, intermediate_size=64, num_hidden_layers=2,
+                      num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=256,
+                      tie_word_embeddings=True)
+    return Qwen2ForCausalLM(cfg).to(torch.bfloat16)
+
+
+def _run(rank, port, world, actors, out):
+    sys.path[:0] = [str(ROOT), str(ROOT / "pipelinerl-swe_amd"), str(ROOT / "tests")]
+    os.environ["OMP_NUM_THREADS"] = "1"
+    import torch.distributed as dist
+    from cpu_rl_step import cpu_rl_step
+    from pipelinerl_amd.trainer_probe import TrainerStep, split_pipeline_probe
+    from test_weight_update_cpu import TorchFlatPacker
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    dev = torch.device("cpu")
+    holder = {}
+
+    def make_trainer(group):
+        ts = TrainerStep(tokens=64, seq=32, prompt=8, micro_batches=2, device=dev, group=group, model=_tiny(),
+                         step_fn=cpu_rl_step, vocab=96)
+        holder["model"] = ts.model
+        return ts
+
+    def make_actor():
+        m = _tiny()
+        for p in m.parameters():
+            p.data.zero_()
+        holder["model"] = m
+        return m
+
+    res = split_pipeline_probe(actors, steps=2, warmup=1, device=dev, bucket_bytes=4096,
+                               make_trainer=make_trainer, make_actor_module=make_actor, packer=TorchFlatPacker())
+    params = {n: p.detach().clone() for n, p in holder["model"].named_parameters()}
+    torch.save({"res": res, "params": params}, Path(out) / f"r{rank}.pt")
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,actors", [(2, 1), (4, 2)])
+def test_split_pipeline_gloo(tmp_path, world, actors):
+    from test_weight_update_cpu import free_port
+
+    mp.spawn(_run, args=(free_port(), world, actors, str(tmp_path)), nprocs=world, join=True)
+    got = [torch.load(tmp_path / f"r{r}.pt") for r in range(world)]
+    n_tr = world - actors
+    r0 = got[0]["res"]
+    assert all(g["res"] == r0 for g in got)  # one report, on every rank
+    assert r0["trainers"] == n_tr and r0["actors"] == actors and r0["updates"] == 3
+    assert r0["broadcast_latency_ms"] > 0 and 0.0 <= r0["hidden_frac"] <= 1.0
+    assert r0["broadcast_bytes"] == sum(2 * p.numel() for p in got[0]["params"].values())
+    for r in range(n_tr, world):  # actors hold the trainer's last snapshot exactly
+        for n, p in got[0]["params"].items():
+            assert torch.equal(got[r]["params"][n], p), (r, n)
+    for r in range(1, n_tr):  # DP replicas stay identical
+        for n, p in got[0]["params"].items():
+            assert torch.equal(got[r]["params"][n], p), (r, n)

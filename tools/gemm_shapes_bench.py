@@ -33,8 +33,14 @@ for name, (K, N) in layers.items():
     for pas, fn in (("fwd", lambda: torch.nn.functional.linear(x, w)), ("dgrad", lambda: dy @ w),
                     ("wgrad", lambda: dy.t() @ x)):
         sec = bench(fn)
-        print(json.dumps({"model": model, "T": T, "layer": name, "K": K, "N": N, "pass": pas,
-                          "ms": round(sec * 1e3, 4), "TFLOPs": round(flops / sec / 1e12, 1)}), flush=True)
+        rec = {"model": model, "T": T, "layer": name, "K": K, "N": N, "pass": pas,
+               "ms": round(sec * 1e3, 4), "TFLOPs": round(flops / sec / 1e12, 1)}
+        if "--check" in sys.argv:  # max error vs an fp32 GEMM of the same bf16 operands, / max |ref|
+            ref = {"fwd": lambda: x.float() @ w.float().t(), "dgrad": lambda: dy.float() @ w.float(),
+                   "wgrad": lambda: dy.float().t() @ x.float()}[pas]()
+            rec["rel_err"] = float((fn().float() - ref).abs().max() / ref.abs().max())
+            del ref
+        print(json.dumps(rec), flush=True)
     del x, w, dy
     torch.cuda.empty_cache()
 
