@@ -37,11 +37,13 @@ enum PrlGemmDtype { PRL_GEMM_F32 = 0, PRL_GEMM_BF16 = 1 };
 int prl_gemm_abi_version(void);
 const char* prl_gemm_error_string(int code);
 
-/* D = op(A) op(B) + beta * D.  `solution` >= 0 selects a hipBLASLt solution index (falls back
- * to the heuristic if it does not support the problem), -1 = heuristic. */
+/* D = op(A) op(B) (+ bias broadcast over D's columns) + beta * D.  `bias`: nullable, bf16, m
+ * elements, bf16 D only (a linear layer's bias: m = output features).  `solution` >= 0 selects a
+ * hipBLASLt solution index (falls back to the heuristic if it does not support the problem),
+ * -1 = heuristic. */
 int prl_gemm_bf16(int op_a, int op_b, int64_t m, int64_t n, int64_t k, const void* A, int64_t lda,
-                  const void* B, int64_t ldb, float beta, void* D, int64_t ldd, int d_dtype, int solution,
-                  void* stream);
+                  const void* B, int64_t ldb, const void* bias, float beta, void* D, int64_t ldd, int d_dtype,
+                  int solution, void* stream);
 
 /* Solution index prl_gemm_bf16 would use for this problem with solution = -1 (-1 if none). */
 int prl_gemm_heuristic_index(int op_a, int op_b, int64_t m, int64_t n, int64_t k, int64_t lda,

@@ -65,12 +65,12 @@ struct Api {
 Api g_api;
 
 struct Key {
-  int op_a, op_b, d_dtype, accumulate;
+  int op_a, op_b, d_dtype, accumulate, bias;
   int64_t m, n, k, lda, ldb, ldd;
   int solution;
   bool operator<(const Key& o) const {
-    return std::tie(op_a, op_b, d_dtype, accumulate, m, n, k, lda, ldb, ldd, solution) <
-           std::tie(o.op_a, o.op_b, o.d_dtype, o.accumulate, o.m, o.n, o.k, o.lda, o.ldb, o.ldd, o.solution);
+    return std::tie(op_a, op_b, d_dtype, accumulate, bias, m, n, k, lda, ldb, ldd, solution) <
+           std::tie(o.op_a, o.op_b, o.d_dtype, o.accumulate, o.bias, o.m, o.n, o.k, o.lda, o.ldb, o.ldd, o.solution);
   }
 };
 
@@ -181,6 +181,12 @@ int make_layouts(const Key& k, Plan* p) {
   hipblasOperation_t oa = op(k.op_a), ob = op(k.op_b);
   RET(hb(g_api.desc_set(p->desc, HIPBLASLT_MATMUL_DESC_TRANSA, &oa, sizeof(oa))));
   RET(hb(g_api.desc_set(p->desc, HIPBLASLT_MATMUL_DESC_TRANSB, &ob, sizeof(ob))));
+  if (k.bias) {  // bf16 bias along D's rows (the output features), added before rounding
+    hipblasLtEpilogue_t epi = HIPBLASLT_EPILOGUE_BIAS;
+    int32_t bt = HIP_R_16BF;
+    RET(hb(g_api.desc_set(p->desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &epi, sizeof(epi))));
+    RET(hb(g_api.desc_set(p->desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt))));
+  }
   int64_t ar = k.op_a == PRL_GEMM_N ? k.m : k.k, ac = k.op_a == PRL_GEMM_N ? k.k : k.m;
   int64_t br = k.op_b == PRL_GEMM_N ? k.k : k.n, bc = k.op_b == PRL_GEMM_N ? k.n : k.k;
   RET(hb(g_api.layout_create(&p->la, HIP_R_16BF, ar, ac, k.lda)));
@@ -244,15 +250,16 @@ int plan_for(int dev, hipblasLtHandle_t h, const Key& k, Plan** out) {
 }
 
 Key make_key(int op_a, int op_b, int64_t m, int64_t n, int64_t k, int64_t lda, int64_t ldb, int64_t ldd,
-             int d_dtype, float beta, int solution) {
-  return Key{op_a, op_b, d_dtype, beta != 0.f ? 1 : 0, m, n, k, lda, ldb, ldd, solution < 0 ? -1 : solution};
+             int d_dtype, float beta, int solution, bool bias = false) {
+  return Key{op_a, op_b, d_dtype, beta != 0.f ? 1 : 0, bias ? 1 : 0, m, n, k, lda, ldb, ldd,
+             solution < 0 ? -1 : solution};
 }
 
 }  // namespace
 
 extern "C" {
 
-int prl_gemm_abi_version(void) { return 1; }
+int prl_gemm_abi_version(void) { return 2; }
 
 const char* prl_gemm_error_string(int code) {
   if (code == 0) return "ok";
@@ -273,10 +280,11 @@ const char* prl_gemm_error_string(int code) {
 }
 
 int prl_gemm_bf16(int op_a, int op_b, int64_t m, int64_t n, int64_t k, const void* A, int64_t lda,
-                  const void* B, int64_t ldb, float beta, void* D, int64_t ldd, int d_dtype, int solution,
-                  void* stream) {
+                  const void* B, int64_t ldb, const void* bias, float beta, void* D, int64_t ldd, int d_dtype,
+                  int solution, void* stream) {
   if (!valid(op_a, op_b, m, n, k, lda, ldb, ldd, d_dtype) || !A || !B || !D) return PRL_GEMM_E_INVALID;
   if (beta != 0.f && beta != 1.f) return PRL_GEMM_E_INVALID;
+  if (bias && d_dtype != PRL_GEMM_BF16) return PRL_GEMM_E_INVALID;
   int dev;
   RET(hp(hipGetDevice(&dev)));
   hipStream_t st = (hipStream_t)stream;
@@ -287,7 +295,8 @@ int prl_gemm_bf16(int op_a, int op_b, int64_t m, int64_t n, int64_t k, const voi
   void* ws;
   RET(workspace_for(dev, st, &ws));
   Plan* p;
-  RET(plan_for(dev, h, make_key(op_a, op_b, m, n, k, lda, ldb, ldd, d_dtype, beta, solution), &p));
+  RET(plan_for(dev, h, make_key(op_a, op_b, m, n, k, lda, ldb, ldd, d_dtype, beta, solution, bias != nullptr), &p));
+  if (bias) RET(hb(g_api.desc_set(p->desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias))));
   float alpha = 1.f;
   return hb(g_api.matmul(h, p->desc, &alpha, A, p->la, B, p->lb, &beta, D, p->ld, D, p->ld, &p->algo, ws,
                             kWorkspaceBytes, st));

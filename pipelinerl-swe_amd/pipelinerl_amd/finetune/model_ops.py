@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import ctypes
 import logging
+import os
 import sys
 import types
 
@@ -127,15 +128,22 @@ class RopeFn(torch.autograd.Function):
 
 
 class PrlLinearFn(torch.autograd.Function):
-    """F.linear whose backward GEMMs (dX = dY W, dW = dY^T X) run through prl_gemm (the ROCm
-    hipBLASLt, include/prl_gemm.h): 1.3-2.9x faster weight gradients and 1.05-1.15x faster input
-    gradients than torch's bundled library at the trainer's shapes (tools/gemm_sweep.py,
-    profiles/r01_gemm_sweep.jsonl).  The forward stays torch's (no faster there).  bf16 only."""
+    """F.linear whose GEMMs run through prl_gemm (the ROCm hipBLASLt, include/prl_gemm.h).
+
+    Backward (dX = dY W, dW = dY^T X) always: 1.3-2.9x faster weight gradients and 1.05-1.15x
+    faster input gradients than torch's bundled library with the library heuristic alone
+    (tools/gemm_sweep.py, profiles/r01_gemm_sweep.jsonl), more with the swept solutions of
+    gemm_solutions.json.  Forward only where a swept solution exists for the shape (bias in the
+    GEMM epilogue); elsewhere torch's F.linear, which the heuristic does not beat.  bf16 only."""
 
     @staticmethod
     def forward(ctx, x, w, b):
         ctx.save_for_backward(x, w)
         ctx.has_bias = b is not None
+        T = x.numel() // x.shape[-1]
+        sol = gemm.solution_for("fwd", T, w.shape[0], w.shape[1])
+        if sol >= 0 and (b is None or (b.dtype == torch.bfloat16 and b.is_contiguous())):
+            return gemm.linear_fwd(x, w, b, solution=sol)
         return torch.nn.functional.linear(x, w, b)
 
     @staticmethod
@@ -222,7 +230,8 @@ def patch_model(model) -> dict:
             n_mlp += 1
         elif name.endswith("Attention"):
             mods.add(type(m).__module__)
-    for mname, lin in model.named_modules():
+    # PRL_LINEAR_GEMM=torch keeps torch's own linear layers (A/B measurements)
+    for mname, lin in (model.named_modules() if os.environ.get("PRL_LINEAR_GEMM", "") != "torch" else ()):
         if isinstance(lin, torch.nn.Linear) and (".layers." in f".{mname}" or mname.endswith("lm_head")):
             if not getattr(lin, "_prl_linear", False):
                 lin.forward = types.MethodType(_prl_linear_forward, lin)

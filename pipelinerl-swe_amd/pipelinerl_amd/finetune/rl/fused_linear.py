@@ -92,7 +92,9 @@ class LinearGrpoLossFn(torch.autograd.Function):
                 idx = hrow[a:a + step]
                 qc = qsel[a:a + step].contiguous()
                 hc = h2.index_select(0, idx)
-                lg = torch.mm(hc, w.t())  # [c, V] contiguous
+                # [c, V] contiguous
+                lg = gemm.linear_fwd(hc, w) if use_prl and gemm.solution_for("fwd", hc.shape[0], V, Hd) >= 0 \
+                    else torch.mm(hc, w.t())
                 cb = _c_batch(lg.data_ptr(), lg.dtype, B, L, V, V, fields)
                 co = _native.PrlGrpoOutputs(*[rows[i].data_ptr() for i in range(8)], None,
                                             lg.data_ptr() if write_grad else None, None)

@@ -25,6 +25,7 @@ _PKG = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ["PRL_GEMM_LIB"]) if os.environ.get("PRL_GEMM_LIB") else _PKG / "libprl_gemm.so"
 HEADER_PATH = _PKG.parents[1] / "include" / "prl_gemm.h"
 SOLUTIONS_PATH = _PKG / "gemm_solutions.json"
+ABI_VERSION = 2
 N_, T_ = 0, 1
 F32, BF16 = 0, 1
 
@@ -53,8 +54,8 @@ def load():
         "prl_gemm_abi_version": (c.c_int, []),
         "prl_gemm_error_string": (c.c_char_p, [c.c_int]),
         "prl_gemm_bf16": (c.c_int, [c.c_int, c.c_int, c.c_int64, c.c_int64, c.c_int64, c.c_void_p, c.c_int64,
-                                    c.c_void_p, c.c_int64, c.c_float, c.c_void_p, c.c_int64, c.c_int, c.c_int,
-                                    c.c_void_p]),
+                                    c.c_void_p, c.c_int64, c.c_void_p, c.c_float, c.c_void_p, c.c_int64, c.c_int,
+                                    c.c_int, c.c_void_p]),
         "prl_gemm_heuristic_index": (c.c_int, [c.c_int, c.c_int, c.c_int64, c.c_int64, c.c_int64, c.c_int64,
                                                c.c_int64, c.c_int64, c.c_int, c.c_float]),
         "prl_gemm_library": (c.c_int, [c.c_char_p, c.c_int]),
@@ -62,7 +63,7 @@ def load():
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
         f.restype, f.argtypes = res, args
-    if lib.prl_gemm_abi_version() != 1:
+    if lib.prl_gemm_abi_version() != ABI_VERSION:
         raise GemmError("libprl_gemm.so ABI mismatch")
     _lib = lib
     return lib
@@ -79,27 +80,33 @@ def _stream(t: torch.Tensor) -> int:
 
 def solutions() -> dict:
     global _solutions
-    if _solutions is None:
-        _solutions = json.loads(SOLUTIONS_PATH.read_text()) if SOLUTIONS_PATH.exists() else {}
+    if _solutions is None:  # PRL_GEMM_SOLUTIONS=off: library heuristic only (A/B measurements)
+        off = os.environ.get("PRL_GEMM_SOLUTIONS", "") == "off"
+        _solutions = json.loads(SOLUTIONS_PATH.read_text()) if SOLUTIONS_PATH.exists() and not off else {}
     return _solutions
 
 
 def solution_for(pas: str, T: int, N: int, K: int, d_dtype: int = BF16, accumulate: bool = False) -> int:
-    """Tuned solution index for the nearest tuned token count (log scale), -1 if none."""
+    """Tuned solution index for the nearest tuned token count (log scale) within 2x of T, else -1
+    (the library heuristic): a solution tuned for 65 536 rows is not trusted at 4 096."""
     entries = solutions().get(f"{pas}:{N}:{K}:{'f32' if d_dtype == F32 else 'bf16'}:{int(accumulate)}")
-    if not entries:
+    if not entries or T <= 0:
         return -1
-    best = min(entries, key=lambda e: abs(math.log(max(T, 1)) - math.log(e["T"])))
-    return int(best["index"])
+    best = min(entries, key=lambda e: abs(math.log(T) - math.log(e["T"])))
+    return int(best["index"]) if abs(math.log(T) - math.log(best["T"])) <= math.log(2.0) + 1e-9 else -1
 
 
 def gemm(op_a: int, op_b: int, m: int, n: int, k: int, a: torch.Tensor, lda: int, b: torch.Tensor, ldb: int,
-         d: torch.Tensor, ldd: int, beta: float = 0.0, solution: int = -1) -> torch.Tensor:
+         d: torch.Tensor, ldd: int, beta: float = 0.0, solution: int = -1,
+         bias: torch.Tensor | None = None) -> torch.Tensor:
     if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or d.dtype not in (torch.bfloat16, torch.float32):
         raise GemmError("prl_gemm: bf16 operands, bf16 / fp32 output")
+    if bias is not None and (bias.dtype != torch.bfloat16 or bias.numel() != m or not bias.is_contiguous()):
+        raise GemmError("prl_gemm: bias must be a contiguous bf16 vector of m elements")
     dd = F32 if d.dtype == torch.float32 else BF16
-    _check(load().prl_gemm_bf16(op_a, op_b, m, n, k, a.data_ptr(), lda, b.data_ptr(), ldb, beta, d.data_ptr(), ldd,
-                                dd, solution, _stream(d)), "prl_gemm_bf16")
+    _check(load().prl_gemm_bf16(op_a, op_b, m, n, k, a.data_ptr(), lda, b.data_ptr(), ldb,
+                                bias.data_ptr() if bias is not None else None, beta, d.data_ptr(), ldd, dd, solution,
+                                _stream(d)), "prl_gemm_bf16")
     return d
 
 
@@ -108,13 +115,15 @@ def _rows(t: torch.Tensor) -> torch.Tensor:
     return t2 if t2.is_contiguous() else t2.contiguous()
 
 
-def linear_fwd(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    """Y = X W^T (no bias), X [..., K] bf16, W [N, K] bf16 contiguous."""
+def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None,
+               solution: int | None = None) -> torch.Tensor:
+    """Y = X W^T (+ bias), X [..., K] bf16, W [N, K] bf16 contiguous, bias [N] bf16."""
     x2 = _rows(x)
     T, K = x2.shape
     N = w.shape[0]
     y = torch.empty((T, N), dtype=x.dtype, device=x.device)
-    gemm(T_, N_, N, T, K, w, K, x2, K, y, N, solution=solution_for("fwd", T, N, K))
+    sol = solution_for("fwd", T, N, K) if solution is None else solution
+    gemm(T_, N_, N, T, K, w, K, x2, K, y, N, solution=sol, bias=bias)
     return y.view(*x.shape[:-1], N)
 
 

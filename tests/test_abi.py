@@ -79,12 +79,27 @@ def test_gemm_library_exports_header_symbols():
     assert len(declared) >= 5
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.prl_gemm_abi_version() == 1
+    assert lib.prl_gemm_abi_version() == gemm.ABI_VERSION == 2
     assert lib.prl_gemm_error_string(4001).decode() == "invalid argument"
     # m = 0, a bad op, null pointers, lda < m: all PRL_GEMM_E_INVALID
-    assert lib.prl_gemm_bf16(0, 0, 0, 4, 4, 1, 4, 1, 4, 0.0, 1, 4, 1, -1, None) == 4001
-    assert lib.prl_gemm_bf16(2, 0, 4, 4, 4, 1, 4, 1, 4, 0.0, 1, 4, 1, -1, None) == 4001
-    assert lib.prl_gemm_bf16(0, 0, 4, 4, 4, None, 4, 1, 4, 0.0, 1, 4, 1, -1, None) == 4001
-    assert lib.prl_gemm_bf16(0, 0, 8, 4, 4, 1, 4, 1, 4, 0.0, 1, 8, 1, -1, None) == 4001
-    assert lib.prl_gemm_bf16(0, 0, 4, 4, 4, 1, 4, 1, 4, 0.5, 1, 4, 1, -1, None) == 4001  # beta in {0, 1}
+    assert lib.prl_gemm_bf16(0, 0, 0, 4, 4, 1, 4, 1, 4, None, 0.0, 1, 4, 1, -1, None) == 4001
+    assert lib.prl_gemm_bf16(2, 0, 4, 4, 4, 1, 4, 1, 4, None, 0.0, 1, 4, 1, -1, None) == 4001
+    assert lib.prl_gemm_bf16(0, 0, 4, 4, 4, None, 4, 1, 4, None, 0.0, 1, 4, 1, -1, None) == 4001
+    assert lib.prl_gemm_bf16(0, 0, 8, 4, 4, 1, 4, 1, 4, None, 0.0, 1, 8, 1, -1, None) == 4001
+    assert lib.prl_gemm_bf16(0, 0, 4, 4, 4, 1, 4, 1, 4, None, 0.5, 1, 4, 1, -1, None) == 4001  # beta in {0, 1}
+    assert lib.prl_gemm_bf16(0, 0, 4, 4, 4, 1, 4, 1, 4, 1, 0.0, 1, 4, 0, -1, None) == 4001  # bias needs bf16 D
     assert lib.prl_gemm_heuristic_index(0, 0, 0, 1, 1, 1, 1, 1, 1, 0.0) == -1
+
+
+def test_gemm_solution_window(monkeypatch):
+    """A swept solution is used only within 2x of the token count it was tuned at."""
+    from pipelinerl_amd import gemm
+
+    monkeypatch.setattr(gemm, "_solutions", {"wgrad:8:16:bf16:0": [{"T": 1000, "index": 7}, {"T": 8000, "index": 9}]})
+    assert gemm.solution_for("wgrad", 1000, 8, 16) == 7
+    assert gemm.solution_for("wgrad", 1900, 8, 16) == 7
+    assert gemm.solution_for("wgrad", 3000, 8, 16) == -1  # 3x from 1000, 2.7x from 8000
+    assert gemm.solution_for("wgrad", 16000, 8, 16) == 9
+    assert gemm.solution_for("wgrad", 17000, 8, 16) == -1
+    assert gemm.solution_for("fwd", 1000, 8, 16) == -1 and gemm.solution_for("wgrad", 0, 8, 16) == -1
+    assert gemm.solution_for("wgrad", 1000, 8, 16, gemm.F32, True) == -1

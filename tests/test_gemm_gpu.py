@@ -25,7 +25,8 @@ def test_library_is_rocm_hipblaslt():
     assert "libhipblaslt.so" in s and "torch" not in s, s
 
 
-@pytest.mark.parametrize("T,N,K", [(4096, 1536, 1536), (1000, 256, 1536), (37, 24, 8), (8192, 8960, 1536)])
+@pytest.mark.parametrize("T,N,K", [(4096, 1536, 1536), (1000, 256, 1536), (37, 24, 8), (8192, 8960, 1536),
+                                   (65536, 1536, 1536), (40000, 256, 1536)])
 def test_linear_passes_match_fp32(T, N, K):
     from pipelinerl_amd import gemm
 
@@ -34,9 +35,40 @@ def test_linear_passes_match_fp32(T, N, K):
     _close(gemm.linear_fwd(x, w), x.float() @ w.float().t())
     _close(gemm.linear_dgrad(dy, w), dy.float() @ w.float())
     _close(gemm.linear_wgrad(dy, x), dy.float().t() @ x.float())
+    b = _rand((N,), g)
+    _close(gemm.linear_fwd(x, w, b), x.float() @ w.float().t() + b.float())  # bias epilogue
     # leading batch dims are flattened like F.linear's
     y3 = gemm.linear_fwd(x.view(1, T, K), w)
     assert y3.shape == (1, T, N) and torch.equal(y3[0], gemm.linear_fwd(x, w))
+
+
+def test_tuned_solutions_match_fp32():
+    """Every swept solution in gemm_solutions.json, at its own token count, within bf16 rounding
+    (checked on a row slice of the output for the big problems)."""
+    from pipelinerl_amd import gemm
+
+    for key, entries in sorted(gemm.solutions().items()):
+        pas, N, K, dt, acc = key.split(":")
+        N, K = int(N), int(K)
+        for e in entries:
+            T = e["T"]
+            g = torch.Generator(device=DEV).manual_seed(T % 1000 + N)
+            x, w = _rand((T, K), g), _rand((N, K), g, 0.05)
+            if pas == "fwd":
+                y = gemm.linear_fwd(x, w, solution=e["index"])
+                _close(y[:256], x[:256].float() @ w.float().t())
+            elif pas == "dgrad":
+                dy = _rand((T, N), g)
+                dx = gemm.linear_dgrad(dy, w)
+                _close(dx[:256], dy[:256].float() @ w.float())
+            else:
+                dy = _rand((T, N), g)
+                out = torch.zeros((N, K), device=DEV, dtype=torch.float32 if dt == "f32" else torch.bfloat16)
+                gemm.linear_wgrad(dy, x, out=out, accumulate=acc == "1")
+                ref = dy[:, :512].float().t() @ x.float()
+                _close(out[:512], ref)
+            del x, w
+            torch.cuda.empty_cache()
 
 
 def test_wgrad_fp32_accumulates_over_chunks():

@@ -54,7 +54,7 @@ static Problem make(const char* pass, int64_t T, int64_t N, int64_t K) {
     p = {HIPBLAS_OP_T, HIPBLAS_OP_N, N, T, K, K, K, N};
   } else if (!strcmp(pass, "dgrad")) {  // dX^T[K,T] = W^T (col-major KxN, op N) * dY^T (col-major NxT, op N)
     p = {HIPBLAS_OP_N, HIPBLAS_OP_N, K, T, N, K, N, K};
-  } else if (!strcmp(pass, "wgrad")) {  // dW^T[K,N] = X^T (col-major KxT, op N) * dY (col-major NxT, op T)
+  } else if (!strcmp(pass, "wgrad") || !strcmp(pass, "wgrad32")) {  // dW^T[K,N] = X^T (col-major KxT, op N) * dY (col-major NxT, op T)
     p = {HIPBLAS_OP_N, HIPBLAS_OP_T, K, N, T, K, N, K};
   } else {
     fprintf(stderr, "unknown pass %s\n", pass);
@@ -88,10 +88,12 @@ int main(int argc, char** argv) {
     const char* pass = argv[a];
     int64_t T = atoll(argv[a + 1]), N = atoll(argv[a + 2]), K = atoll(argv[a + 3]);
     Problem p = make(pass, T, N, K);
+    const bool f32 = !strcmp(pass, "wgrad32");  // fp32 dW accumulated over chunks (beta = 1)
+    const hipDataType dt = f32 ? HIP_R_32F : HIP_R_16BF;
     int64_t a_rows = p.opA == HIPBLAS_OP_N ? p.m : p.k, a_cols = p.opA == HIPBLAS_OP_N ? p.k : p.m;
     int64_t b_rows = p.opB == HIPBLAS_OP_N ? p.k : p.n, b_cols = p.opB == HIPBLAS_OP_N ? p.n : p.k;
     size_t a_bytes = (size_t)p.lda * a_cols * 2, b_bytes = (size_t)p.ldb * b_cols * 2,
-           c_bytes = (size_t)p.ldc * p.n * 2;
+           c_bytes = (size_t)p.ldc * p.n * (f32 ? 4 : 2);
     void *A[2], *B[2], *C[2];
     for (int r = 0; r < 2; ++r) {
       CK(hipMalloc(&A[r], a_bytes));
@@ -107,8 +109,9 @@ int main(int argc, char** argv) {
     hipblasLtMatrixLayout_t la, lb, lc;
     CK(hipblasLtMatrixLayoutCreate(&la, HIP_R_16BF, a_rows, a_cols, p.lda));
     CK(hipblasLtMatrixLayoutCreate(&lb, HIP_R_16BF, b_rows, b_cols, p.ldb));
-    CK(hipblasLtMatrixLayoutCreate(&lc, HIP_R_16BF, p.m, p.n, p.ldc));
-    float alpha = 1.f, beta = 0.f;
+    CK(hipblasLtMatrixLayoutCreate(&lc, dt, p.m, p.n, p.ldc));
+    float alpha = 1.f, beta = f32 ? 1.f : 0.f;
+    for (int r = 0; r < 2; ++r) CK(hipMemset(C[r], 0, c_bytes));
 
     // one timed probe launch first; only solutions within 1.3x of the best so far get the full
     // timing (3 warm-up + 10 timed launches) -- keeps a sweep over thousands of solutions short
@@ -151,7 +154,7 @@ int main(int argc, char** argv) {
     std::vector<hipblasLtMatmulHeuristicResult_t> all;
     if (!heur_only)
       CK(hipblaslt_ext::getAllAlgos(h, hipblaslt_ext::GemmType::HIPBLASLT_GEMM, p.opA, p.opB, HIP_R_16BF, HIP_R_16BF,
-                                  HIP_R_16BF, HIP_R_16BF, HIPBLAS_COMPUTE_32F, all));
+                                  dt, dt, HIPBLAS_COMPUTE_32F, all));
     std::vector<std::pair<float, int>> res;
     int supported = 0;
     for (size_t i = 0; i < all.size(); ++i) {
