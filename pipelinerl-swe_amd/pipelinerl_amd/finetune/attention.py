@@ -124,9 +124,11 @@ def varlen_attention_forward(module, query, key, value, attention_mask, scaling=
     B, Hq, T, D = query.shape
     assert B == 1, "packed batches are [1, T]"
     Hkv = key.shape[1]
-    q = query[0].transpose(0, 1)
-    k = key[0].transpose(0, 1)
-    v = value[0].transpose(0, 1)
+    # squeeze, not [0]: select's backward would allocate a zeroed [1, H, T, D] head-major gradient
+    # and copy into it; squeeze's is a view, so dq / dk / dv reach RoPE and v_proj token-major
+    q = query.squeeze(0).transpose(0, 1)
+    k = key.squeeze(0).transpose(0, 1)
+    v = value.squeeze(0).transpose(0, 1)
     mx = int(kwargs["max_length_q"])
     bounds = kwargs.get("cu_seq_lens_host")
     hip_bwd = bounds is not None and q.is_cuda and _hip_backward_ok(q, k)

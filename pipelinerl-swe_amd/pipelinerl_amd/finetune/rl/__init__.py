@@ -96,6 +96,8 @@ def rl_step(model, batch: PipelineBatchEncoding, current_step: int, max_step: in
         model_inputs["pixel_values"] = batch.pixel_values
     if getattr(batch, "image_grid_thw", None) is not None:
         model_inputs["image_grid_thw"] = batch.image_grid_thw
+    if getattr(getattr(model, "config", None), "use_cache", None) is not None:
+        model_inputs["use_cache"] = False  # training: no KV cache (HF would concatenate k / v per layer)
     fused_head = config.fused_lm_head and _lm_head_of(model, has_value_head) is not None
     if fused_head:
         hidden = _decoder_of(model)(**model_inputs).last_hidden_state
