@@ -10,6 +10,11 @@
 //                                               pass wgrad dW[N,K] = dY[T,N]^T X[T,K]
 //   hipblaslt_probe <pass> <T> <N> <K> [<pass> <T> <N> <K> ...]
 // Build: hipcc -O2 --offload-arch=gfx950 tools/hipblaslt_probe.cpp -lhipblaslt -o tools/hipblaslt_probe.bin
+//
+// CAUTION: a full sweep runs every solution the library reports as supporting the problem, and
+// one of them faulted the GPU (illegal address) at fwd T=16384 N=18944 K=3584 (7B gate/up) on
+// MI355X / ROCm 7.2.  A faulting run counts against the GPU pool: sweep only shapes that have
+// swept cleanly before, or use --heuristic-only.
 #include <hip/hip_runtime.h>
 #include <hipblaslt/hipblaslt-ext.hpp>
 #include <hipblaslt/hipblaslt.h>
