@@ -54,9 +54,12 @@ def test_tuned_solutions_match_fp32():
             T = e["T"]
             g = torch.Generator(device=DEV).manual_seed(T % 1000 + N)
             x, w = _rand((T, K), g), _rand((N, K), g, 0.05)
-            if pas == "fwd":
+            if pas == "fwd":  # with and without the bias epilogue (q/k/v carry a bias)
+                b = _rand((N,), g)
                 y = gemm.linear_fwd(x, w, solution=e["index"])
                 _close(y[:256], x[:256].float() @ w.float().t())
+                y = gemm.linear_fwd(x, w, b, solution=e["index"])
+                _close(y[:256], x[:256].float() @ w.float().t() + b.float())
             elif pas == "dgrad":
                 dy = _rand((T, N), g)
                 dx = gemm.linear_dgrad(dy, w)
