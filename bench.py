@@ -246,6 +246,10 @@ def main():
         if not args.no_cpu_baseline and world == 1:
             threads = min(os.cpu_count() or 1, 16)
             cpu = cpu_baseline(args.cpu_rows, V, threads)
+            # the reference's CPU finetune path (configs[0], C1: Qwen2.5-0.5B micro-batch step)
+            from oracle import cpu_trainer
+
+            cpu["trainer_step"] = cpu_trainer.cpu_trainer_step(threads=threads)
         out = {
             "metric": "trainer tokens/s (packed GRPO) at 1/2/4/8 MI355X; loss-kernel HBM GB/s",
             "value": round(tokens_total / elapsed, 1),
