@@ -87,6 +87,22 @@ constexpr int kLoadAux = PRL_LOAD_AUX;
 constexpr int kStoreAux = PRL_STORE_AUX;
 constexpr uint32_t kPadBf16x2 = 0xF1CAF1CAu;  // two bf16 -1.0e30: contributes 2^-huge = 0
 
+#ifndef PRL_ROW_PERMUTE
+#define PRL_ROW_PERMUTE 1  // A/B (tools/build_variants.py row_permute): 7.40 vs 7.46 ms per C2 launch, same box
+#endif
+// Order in which the persistent grid visits the rows: iteration i processes row perm(i).  With
+// PRL_ROW_PERMUTE the rows in flight at any moment are scattered over the whole [rows x V]
+// tensor (i * P mod n, P a prime > n, so a bijection) instead of one contiguous ~76 MB window;
+// per-row outputs are written per row, so results are bit-identical either way.
+__device__ __forceinline__ int64_t perm_row(int64_t i, int64_t n) {
+#if PRL_ROW_PERMUTE
+  return (int64_t)(((uint64_t)i * 2654435761ull) % (uint64_t)n);
+#else
+  (void)n;
+  return i;
+#endif
+}
+
 template <int NV>
 __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
   constexpr int BLOCK = 1024, NW = BLOCK / 64;
@@ -107,7 +123,7 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
   int64_t q = blockIdx.x;
   if (q < nrows) {
     int64_t lrow, tok, qo;
-    map_row(a, q, lrow, tok, qo);
+    map_row(a, perm_row(q, nrows), lrow, tok, qo);
     const auto rs = row_rsrc(lg + lrow * a.ld, row_bytes);
 #pragma unroll
     for (int k = 0; k < NV; ++k)
@@ -116,7 +132,7 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
   int par = 0;
   for (; q < nrows; q += gridDim.x, par ^= 1) {
     int64_t lrow, tok, qo;
-    map_row(a, q, lrow, tok, qo);
+    map_row(a, perm_row(q, nrows), lrow, tok, qo);
     const int64_t tid_raw = a.input_ids[tok];
     const bool bad_id = (uint64_t)tid_raw >= (uint64_t)a.V;
     const int64_t tgt = bad_id ? -1 : tid_raw;  // -1: never matches a column below
@@ -161,7 +177,7 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
     int64_t nlrow = lrow;
     if (has_next) {
       int64_t nt, nq;
-      map_row(a, qn, nlrow, nt, nq);
+      map_row(a, perm_row(qn, nrows), nlrow, nt, nq);
     }
     const auto rn = row_rsrc(lg + nlrow * a.ld, has_next ? row_bytes : 0);
     if (a.write_grad) {

@@ -12,6 +12,7 @@ VARIANTS = {
     "ld_nt_st_def": {"PRL_LOAD_AUX": "2", "PRL_STORE_AUX": "0"},
     "ld_def_st_def": {"PRL_LOAD_AUX": "0", "PRL_STORE_AUX": "0"},
     "copy_ceiling": {"PRL_COPY_CEILING": "1"},
+    "row_sequential": {"PRL_ROW_PERMUTE": "0"},
     "attn_fwd_1wave": {"PRL_ATTN_FWD_MINB": "1"},
     "attn_serial": {"PRL_ATTN_INTERLEAVE": "0"},
 }
