@@ -191,44 +191,83 @@ __global__ __launch_bounds__(256) void rmsnorm_dw_stage2(const float* __restrict
 // SwiGLU: h = bf16(bf16(silu(g)) * u)
 __device__ __forceinline__ float silu(float g) { return g / (1.0f + expf(-g)); }
 
+// SWIGLU_UNROLL vectors per thread per iteration, all loads issued before any math: with one
+// vector per thread a CU had ~64 KB of loads in flight, short of the ~60-100 KB per CU the HBM
+// latency needs at 5 TB/s (the kernels ran at 4.4 / 4.7 TB/s).
+#ifndef SWIGLU_UNROLL
+#define SWIGLU_UNROLL 4
+#endif
+__device__ __forceinline__ u32x4 swiglu_vec(u32x4 gv, u32x4 uv) {
+  u32x4 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    o[j] = pack(r16(silu(lo(gv[j]))) * lo(uv[j]), r16(silu(hi(gv[j]))) * hi(uv[j]));
+  return o;
+}
 __global__ __launch_bounds__(256) void swiglu_fwd(const u32x4* __restrict__ g, const u32x4* __restrict__ u,
                                                   u32x4* __restrict__ h, int64_t n8) {
+  constexpr int U = SWIGLU_UNROLL;
   const int64_t stride = (int64_t)gridDim.x * 256;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += stride) {
-    const u32x4 gv = __builtin_nontemporal_load(g + i), uv = __builtin_nontemporal_load(u + i);
-    u32x4 o;
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  for (; i + (U - 1) * stride < n8; i += U * stride) {
+    u32x4 gv[U], uv[U];
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      o[j] = pack(r16(silu(lo(gv[j]))) * lo(uv[j]), r16(silu(hi(gv[j]))) * hi(uv[j]));
-    __builtin_nontemporal_store(o, h + i);
+    for (int k = 0; k < U; ++k) {
+      gv[k] = __builtin_nontemporal_load(g + i + k * stride);
+      uv[k] = __builtin_nontemporal_load(u + i + k * stride);
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) __builtin_nontemporal_store(swiglu_vec(gv[k], uv[k]), h + i + k * stride);
   }
+  for (; i < n8; i += stride)
+    __builtin_nontemporal_store(swiglu_vec(__builtin_nontemporal_load(g + i), __builtin_nontemporal_load(u + i)), h + i);
 }
 
 // du = bf16(dh * s), s = bf16(silu(g));  dg = bf16(bf16(dh * u) * sig (1 + g (1 - sig)))
+__device__ __forceinline__ void swiglu_bwd_vec(u32x4 dv, u32x4 gv, u32x4 uv, u32x4& og, u32x4& ou) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float dgr[2], dur[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const float gg = e ? hi(gv[j]) : lo(gv[j]);
+      const float uu = e ? hi(uv[j]) : lo(uv[j]);
+      const float dd = e ? hi(dv[j]) : lo(dv[j]);
+      const float sig = 1.0f / (1.0f + expf(-gg));
+      dur[e] = dd * r16(silu(gg));  // the saved bf16 activation, as the eager chain keeps it
+      const float ds = r16(dd * uu);
+      dgr[e] = ds * (sig * (1.0f + gg * (1.0f - sig)));
+    }
+    og[j] = pack(dgr[0], dgr[1]);
+    ou[j] = pack(dur[0], dur[1]);
+  }
+}
 __global__ __launch_bounds__(256) void swiglu_bwd(const u32x4* __restrict__ dh, const u32x4* __restrict__ g,
                                                   const u32x4* __restrict__ u, u32x4* __restrict__ dg,
                                                   u32x4* __restrict__ du, int64_t n8) {
+  constexpr int U = SWIGLU_UNROLL > 2 ? 2 : SWIGLU_UNROLL;  // 3 loads per vector: 2 is enough in flight
   const int64_t stride = (int64_t)gridDim.x * 256;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += stride) {
-    const u32x4 dv = __builtin_nontemporal_load(dh + i), gv = __builtin_nontemporal_load(g + i),
-                uv = __builtin_nontemporal_load(u + i);
-    u32x4 og, ou;
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  for (; i + (U - 1) * stride < n8; i += U * stride) {
+    u32x4 dv[U], gv[U], uv[U];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float dgr[2], dur[2];
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const float gg = e ? hi(gv[j]) : lo(gv[j]);
-        const float uu = e ? hi(uv[j]) : lo(uv[j]);
-        const float dd = e ? hi(dv[j]) : lo(dv[j]);
-        const float sig = 1.0f / (1.0f + expf(-gg));
-        dur[e] = dd * r16(silu(gg));  // the saved bf16 activation, as the eager chain keeps it
-        const float ds = r16(dd * uu);
-        dgr[e] = ds * (sig * (1.0f + gg * (1.0f - sig)));
-      }
-      og[j] = pack(dgr[0], dgr[1]);
-      ou[j] = pack(dur[0], dur[1]);
+    for (int k = 0; k < U; ++k) {
+      dv[k] = __builtin_nontemporal_load(dh + i + k * stride);
+      gv[k] = __builtin_nontemporal_load(g + i + k * stride);
+      uv[k] = __builtin_nontemporal_load(u + i + k * stride);
     }
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      u32x4 og, ou;
+      swiglu_bwd_vec(dv[k], gv[k], uv[k], og, ou);
+      __builtin_nontemporal_store(og, dg + i + k * stride);
+      __builtin_nontemporal_store(ou, du + i + k * stride);
+    }
+  }
+  for (; i < n8; i += stride) {
+    u32x4 og, ou;
+    swiglu_bwd_vec(__builtin_nontemporal_load(dh + i), __builtin_nontemporal_load(g + i), __builtin_nontemporal_load(u + i),
+                   og, ou);
     __builtin_nontemporal_store(og, dg + i);
     __builtin_nontemporal_store(ou, du + i);
   }

@@ -13,6 +13,8 @@ VARIANTS = {
     "ld_def_st_def": {"PRL_LOAD_AUX": "0", "PRL_STORE_AUX": "0"},
     "copy_ceiling": {"PRL_COPY_CEILING": "1"},
     "row_sequential": {"PRL_ROW_PERMUTE": "0"},
+    "swiglu_u1": {"SWIGLU_UNROLL": "1"},
+    "swiglu_u2": {"SWIGLU_UNROLL": "2"},
     "attn_fwd_1wave": {"PRL_ATTN_FWD_MINB": "1"},
     "attn_serial": {"PRL_ATTN_INTERLEAVE": "0"},
 }
