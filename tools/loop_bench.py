@@ -32,7 +32,9 @@ sys.path[:0] = [str(ROOT / "pipelinerl-swe_amd")]
 EOS = 151643  # Qwen2.5 <|endoftext|>
 
 
-def make_rollouts(n: int, group: int, mean_len: int, prompt: int, vocab: int, seed: int):
+def make_rollouts(n: int, group: int, mean_len: int, prompt: int, vocab: int, seed: int, dist: str = "uniform"):
+    """dist "uniform": length U[mean/2, 3 mean/2) with a fixed prompt; "c3": BASELINE configs[2]'s
+    math rollouts, prompt U{64..512} + completion U{256..8192} (max_tokens 8192)."""
     import numpy as np
 
     from pipelinerl_amd.finetune.rl import RLConfig, populate_rl_data, prepare_rl_fields
@@ -40,7 +42,11 @@ def make_rollouts(n: int, group: int, mean_len: int, prompt: int, vocab: int, se
     rng = np.random.default_rng(seed)
     data = []
     for i in range(n):
-        L = int(rng.integers(mean_len // 2, mean_len * 3 // 2))
+        if dist == "c3":
+            prompt = int(rng.integers(64, 513))
+            L = prompt + int(rng.integers(256, 8193))
+        else:
+            L = int(rng.integers(mean_len // 2, mean_len * 3 // 2))
         c = L - prompt
         ids = rng.integers(0, EOS, L).tolist()
         if rng.random() < 0.75:
@@ -62,6 +68,8 @@ def main():
     ap.add_argument("--mean-len", type=int, default=2048)
     ap.add_argument("--prompt", type=int, default=256)
     ap.add_argument("--fused-lm-head", action="store_true")
+    ap.add_argument("--dist", choices=["uniform", "c3"], default="uniform",
+                    help="rollout lengths: uniform around --mean-len, or configs[2]'s U{64..512} + U{256..8192}")
     ap.add_argument("--eager-ops", action="store_true", help="HF element-wise chains instead of the HIP model ops")
     ap.add_argument("--workdir", default=None)
     a = ap.parse_args()
@@ -82,7 +90,7 @@ def main():
 
     t0 = time.time()
     n = a.samples_per_step * a.steps
-    data = make_rollouts(n, 8, a.mean_len, a.prompt, QWEN[a.model]["vocab_size"], 0)
+    data = make_rollouts(n, 8, a.mean_len, a.prompt, QWEN[a.model]["vocab_size"], 0, a.dist)
     reset_streams_backend()
     set_streams_backend("files")
     packer = MicroBatchPacker(1, a.seq_length, a.samples_per_step, types.SimpleNamespace(eos_token_id=EOS))
@@ -132,7 +140,7 @@ def main():
     # wall time between the logs of step 1 and step N: data, stats, optimizer, scheduler included
     sec = stamps[-1] - stamps[0] if len(stamps) > 1 else loop_s
     out = {"tool": "loop_bench", "model": f"Qwen2.5-{a.model} shapes (random init, bf16)",
-           "seq_length": a.seq_length, "samples_per_step": a.samples_per_step, "mean_rollout_len": a.mean_len,
+           "seq_length": a.seq_length, "samples_per_step": a.samples_per_step, "mean_rollout_len": a.mean_len, "length_dist": a.dist,
            "fused_lm_head": a.fused_lm_head, "fused_model_ops": not a.eager_ops, "steps": m.completed_steps,
            "micro_batches_per_step": [x["throughput/micro_batches_per_step"] for x in lines],
            "tokens_per_step": [x["throughput/tokens_per_step"] for x in lines],
