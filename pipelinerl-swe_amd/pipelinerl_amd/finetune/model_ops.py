@@ -133,8 +133,9 @@ class PrlLinearFn(torch.autograd.Function):
     Backward (dX = dY W, dW = dY^T X) always: 1.3-2.9x faster weight gradients and 1.05-1.15x
     faster input gradients than torch's bundled library with the library heuristic alone
     (tools/gemm_sweep.py, profiles/r01_gemm_sweep.jsonl), more with the swept solutions of
-    gemm_solutions.json.  Forward only where a swept solution exists for the shape (bias in the
-    GEMM epilogue); elsewhere torch's F.linear, which the heuristic does not beat.  bf16 only."""
+    gemm_solutions.json.  Forward only where gemm_solutions.json routes the shape (a swept solution,
+    or the heuristic where it measured faster than torch; bias in the GEMM epilogue); elsewhere
+    torch's F.linear, which the heuristic does not generally beat.  bf16 only."""
 
     @staticmethod
     def forward(ctx, x, w, b):
@@ -142,7 +143,7 @@ class PrlLinearFn(torch.autograd.Function):
         ctx.has_bias = b is not None
         T = x.numel() // x.shape[-1]
         sol = gemm.solution_for("fwd", T, w.shape[0], w.shape[1])
-        if sol >= 0 and (b is None or (b.dtype == torch.bfloat16 and b.is_contiguous())):
+        if sol is not None and (b is None or (b.dtype == torch.bfloat16 and b.is_contiguous())):
             return gemm.linear_fwd(x, w, b, solution=sol)
         return torch.nn.functional.linear(x, w, b)
 

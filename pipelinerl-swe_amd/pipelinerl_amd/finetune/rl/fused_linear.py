@@ -93,7 +93,7 @@ class LinearGrpoLossFn(torch.autograd.Function):
                 qc = qsel[a:a + step].contiguous()
                 hc = h2.index_select(0, idx)
                 # [c, V] contiguous
-                lg = gemm.linear_fwd(hc, w) if use_prl and gemm.solution_for("fwd", hc.shape[0], V, Hd) >= 0 \
+                lg = gemm.linear_fwd(hc, w) if use_prl and gemm.solution_for("fwd", hc.shape[0], V, Hd) is not None \
                     else torch.mm(hc, w.t())
                 cb = _c_batch(lg.data_ptr(), lg.dtype, B, L, V, V, fields)
                 co = _native.PrlGrpoOutputs(*[rows[i].data_ptr() for i in range(8)], None,

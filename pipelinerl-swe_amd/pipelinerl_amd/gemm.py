@@ -86,14 +86,16 @@ def solutions() -> dict:
     return _solutions
 
 
-def solution_for(pas: str, T: int, N: int, K: int, d_dtype: int = BF16, accumulate: bool = False) -> int:
-    """Tuned solution index for the nearest tuned token count (log scale) within 2x of T, else -1
-    (the library heuristic): a solution tuned for 65 536 rows is not trusted at 4 096."""
+def solution_for(pas: str, T: int, N: int, K: int, d_dtype: int = BF16, accumulate: bool = False) -> int | None:
+    """Routing entry for the nearest tuned token count (log scale) within 2x of T: a solution
+    index (>= 0), -1 = the library heuristic (entries measured faster than torch's matmul with
+    it, forward only), or None when no entry covers T (forward: torch's F.linear; backward: the
+    heuristic).  A solution tuned for 65 536 rows is not trusted at 4 096."""
     entries = solutions().get(f"{pas}:{N}:{K}:{'f32' if d_dtype == F32 else 'bf16'}:{int(accumulate)}")
     if not entries or T <= 0:
-        return -1
+        return None
     best = min(entries, key=lambda e: abs(math.log(T) - math.log(e["T"])))
-    return int(best["index"]) if abs(math.log(T) - math.log(best["T"])) <= math.log(2.0) + 1e-9 else -1
+    return int(best["index"]) if abs(math.log(T) - math.log(best["T"])) <= math.log(2.0) + 1e-9 else None
 
 
 def gemm(op_a: int, op_b: int, m: int, n: int, k: int, a: torch.Tensor, lda: int, b: torch.Tensor, ldb: int,
@@ -123,7 +125,7 @@ def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = Non
     N = w.shape[0]
     y = torch.empty((T, N), dtype=x.dtype, device=x.device)
     sol = solution_for("fwd", T, N, K) if solution is None else solution
-    gemm(T_, N_, N, T, K, w, K, x2, K, y, N, solution=sol, bias=bias)
+    gemm(T_, N_, N, T, K, w, K, x2, K, y, N, solution=-1 if sol is None else sol, bias=bias)
     return y.view(*x.shape[:-1], N)
 
 
@@ -133,7 +135,8 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     T, N = d2.shape
     K = w.shape[1]
     dx = torch.empty((T, K), dtype=dy.dtype, device=dy.device)
-    gemm(N_, N_, K, T, N, w, K, d2, N, dx, K, solution=solution_for("dgrad", T, N, K))
+    sol = solution_for("dgrad", T, N, K)
+    gemm(N_, N_, K, T, N, w, K, d2, N, dx, K, solution=-1 if sol is None else sol)
     return dx.view(*dy.shape[:-1], K)
 
 
@@ -148,8 +151,8 @@ def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = N
     if out.shape != (N, K) or not out.is_contiguous():
         raise GemmError("linear_wgrad: out must be a contiguous [N, K] tensor")
     dd = F32 if out.dtype == torch.float32 else BF16
-    gemm(N_, T_, K, N, T, x2, K, d2, N, out, K, beta=1.0 if accumulate else 0.0,
-         solution=solution_for("wgrad", T, N, K, dd, accumulate))
+    sol = solution_for("wgrad", T, N, K, dd, accumulate)
+    gemm(N_, T_, K, N, T, x2, K, d2, N, out, K, beta=1.0 if accumulate else 0.0, solution=-1 if sol is None else sol)
     return out
 
 

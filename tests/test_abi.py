@@ -98,8 +98,8 @@ def test_gemm_solution_window(monkeypatch):
     monkeypatch.setattr(gemm, "_solutions", {"wgrad:8:16:bf16:0": [{"T": 1000, "index": 7}, {"T": 8000, "index": 9}]})
     assert gemm.solution_for("wgrad", 1000, 8, 16) == 7
     assert gemm.solution_for("wgrad", 1900, 8, 16) == 7
-    assert gemm.solution_for("wgrad", 3000, 8, 16) == -1  # 3x from 1000, 2.7x from 8000
+    assert gemm.solution_for("wgrad", 3000, 8, 16) is None  # 3x from 1000, 2.7x from 8000
     assert gemm.solution_for("wgrad", 16000, 8, 16) == 9
-    assert gemm.solution_for("wgrad", 17000, 8, 16) == -1
-    assert gemm.solution_for("fwd", 1000, 8, 16) == -1 and gemm.solution_for("wgrad", 0, 8, 16) == -1
-    assert gemm.solution_for("wgrad", 1000, 8, 16, gemm.F32, True) == -1
+    assert gemm.solution_for("wgrad", 17000, 8, 16) is None
+    assert gemm.solution_for("fwd", 1000, 8, 16) is None and gemm.solution_for("wgrad", 0, 8, 16) is None
+    assert gemm.solution_for("wgrad", 1000, 8, 16, gemm.F32, True) is None

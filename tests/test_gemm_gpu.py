@@ -52,6 +52,8 @@ def test_tuned_solutions_match_fp32():
         N, K = int(N), int(K)
         for e in entries:
             T = e["T"]
+            if e["index"] < 0:  # a routing entry (library heuristic): covered by the pass tests
+                continue
             g = torch.Generator(device=DEV).manual_seed(T % 1000 + N)
             x, w = _rand((T, K), g), _rand((N, K), g, 0.05)
             if pas == "fwd":  # with and without the bias epilogue (q/k/v carry a bias)
