@@ -26,7 +26,8 @@ At N > 1, last, BASELINE.json configs[3] (C4) is measured under "split_pipeline"
 [0, N/2) train Qwen2.5-7B shapes data-parallel while ranks [N/2, N) act as actors; trainer rank 0
 broadcasts each step's weights to them (WeightUpdateManager -> WorkerExtension) while the
 trainers run the next step.  The trainers' step time with and without the broadcast in flight
-gives hidden_frac (1.0 = the broadcast latency is fully overlapped).
+gives hidden_frac (1.0 = the broadcast latency is fully overlapped).  At N >= 4, "fsdp_32b":
+BASELINE.json configs[4] (C5), Qwen2.5-32B shapes sharded with FSDP2 over all ranks, KL on.
 
 Prints ONE JSON line (rank 0).  roofline.achieved = algorithmic bytes per launch
 (T*V*2 read + T*V*2 dlogits write + 37*T side data) / the average duration
@@ -125,6 +126,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-comm-probe", action="store_true", help="N > 1: skip the all-reduce / broadcast probes")
     ap.add_argument("--no-trainer-step", action="store_true", help="skip the full trainer-step probe")
+    ap.add_argument("--no-fsdp", action="store_true", help="N >= 4: skip the configs[4] FSDP 32B probe")
     ap.add_argument("--no-split-pipeline", action="store_true",
                     help="N > 1: skip the split trainer/actor probe (configs[3]: 7B, overlapped weight broadcast)")
     args = ap.parse_args()
@@ -236,6 +238,15 @@ def main():
         split["model"] = "Qwen2.5-7b shapes (random init, bf16), 2 x 16384-token micro-batches per trainer rank"
         torch.cuda.empty_cache()
 
+    fsdp = None
+    if world >= 4 and not args.no_fsdp:
+        # configs[4] (C5): Qwen2.5-32B shapes, FSDP2 over every rank, KL-to-reference on
+        from pipelinerl_amd.trainer_probe import fsdp_step_probe
+
+        torch.cuda.empty_cache()
+        fsdp = fsdp_step_probe("32b", tokens=4096, micro_batches=1, steps=2, warmup=1, device=dev, kl_coef=0.001)
+        torch.cuda.empty_cache()
+
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
         tokens_total = T * world * args.steps
@@ -279,6 +290,8 @@ def main():
             out["trainer_step"] = trainer
         if split is not None:
             out["split_pipeline"] = split
+        if fsdp is not None:
+            out["fsdp_32b"] = fsdp
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -23,15 +23,19 @@ QWEN = {  # published Qwen2.5 shapes (config.json of each checkpoint)
                  num_key_value_heads=2, vocab_size=151936, tie_word_embeddings=True),
     "7b": dict(hidden_size=3584, intermediate_size=18944, num_hidden_layers=28, num_attention_heads=28,
                num_key_value_heads=4, vocab_size=152064, tie_word_embeddings=False),
+    "32b": dict(hidden_size=5120, intermediate_size=27648, num_hidden_layers=64, num_attention_heads=40,
+                num_key_value_heads=8, vocab_size=152064, tie_word_embeddings=False),
 }
 
 
-def qwen2_model(name: str, device: torch.device, grad_ckpt: bool = False, fused_ops: bool = True):
+def qwen2_model(name: str, device: torch.device, grad_ckpt: bool = False, fused_ops: bool = True,
+                layers: int | None = None):
     from transformers import AutoModelForCausalLM, Qwen2Config
 
     from .finetune.attention import register
 
-    cfg = Qwen2Config(max_position_embeddings=32768, rope_theta=1e6, rms_norm_eps=1e-6, **QWEN[name])
+    shapes = dict(QWEN[name], **({"num_hidden_layers": layers} if layers else {}))
+    cfg = Qwen2Config(max_position_embeddings=32768, rope_theta=1e6, rms_norm_eps=1e-6, **shapes)
     torch.manual_seed(0)
     with torch.device(device):  # initialise on the GPU (a CPU init of 1.5B+ params takes minutes)
         model = AutoModelForCausalLM.from_config(cfg, dtype=torch.bfloat16, attn_implementation=register())
@@ -45,8 +49,9 @@ def qwen2_model(name: str, device: torch.device, grad_ckpt: bool = False, fused_
     return model
 
 
-def packed_batch(T: int, seq: int, prompt: int, V: int, device, seed: int = 0):
-    """One packed micro-batch: T // seq rollouts of ``seq`` tokens (``prompt`` of them prompt)."""
+def packed_batch(T: int, seq: int, prompt: int, V: int, device, seed: int = 0, ref_noise: bool = False):
+    """One packed micro-batch: T // seq rollouts of ``seq`` tokens (``prompt`` of them prompt);
+    ``ref_noise``: reference log-probs = old + N(0, 0.05^2) on label tokens."""
     from .finetune.types import PipelineBatchEncoding
 
     g = torch.Generator().manual_seed(seed)
@@ -57,9 +62,10 @@ def packed_batch(T: int, seq: int, prompt: int, V: int, device, seed: int = 0):
     rewards = torch.repeat_interleave(torch.randint(0, 2, (nseq,), generator=g).float(), seq)[None]
     lab = (labels != -100).float()
     old = (torch.randn((1, T), generator=g) - 12.0) * lab
+    ref = old + 0.05 * torch.randn((1, T), generator=g) * lab if ref_noise else old.clone()
     b = PipelineBatchEncoding(
         input_ids=ids, labels=labels, attention_mask=torch.ones_like(ids), position_ids=pos[None],
-        rewards=rewards, advantages=rewards - rewards.mean(), ref_logprobs=old.clone(), old_logprobs=old,
+        rewards=rewards, advantages=rewards - rewards.mean(), ref_logprobs=ref, old_logprobs=old,
         group_tokens=torch.full((1, T), float(seq)), num_labels=torch.full((1, T), float(seq - prompt)),
         overflow=torch.zeros((1, T)), seq_boundaries=torch.arange(0, T + 1, seq, dtype=torch.int32),
         model_version=0, is_packed=True)
@@ -69,12 +75,13 @@ def packed_batch(T: int, seq: int, prompt: int, V: int, device, seed: int = 0):
     return b
 
 
-def rl_config(samples_per_step: int, fused_head: bool = False):
+def rl_config(samples_per_step: int, fused_head: bool = False, kl_coef: float = 0.0):
     from .finetune.rl import RLConfig
 
-    # GRPO defaults (conf/finetune/base.yaml + grpo.yaml): ppo, eps 4, kl 0, C 5
-    return RLConfig(policy_loss="ppo", epsilon=4.0, kl_coef=0.0, final_kl_coef=0.0, clamp_log_ratio_ref_new_value=5,
-                    batch_size=samples_per_step, fused_lm_head=fused_head)
+    # GRPO defaults (conf/finetune/base.yaml + grpo.yaml): ppo, eps 4, kl 0, C 5; C5 turns KL on
+    # (kl_coef 0.001, conf/deepscaler15b.yaml:34)
+    return RLConfig(policy_loss="ppo", epsilon=4.0, kl_coef=kl_coef, final_kl_coef=kl_coef,
+                    clamp_log_ratio_ref_new_value=5, batch_size=samples_per_step, fused_lm_head=fused_head)
 
 
 def _sync(device) -> None:
@@ -93,30 +100,41 @@ class TrainerStep:
 
     def __init__(self, name: str = "1.5b", tokens: int = 16384, seq: int = 2048, prompt: int = 256,
                  micro_batches: int = 4, device=None, fused_head: bool = False, grad_ckpt: bool = False,
-                 fused_ops: bool = True, group=None, model=None, step_fn=None, vocab: int | None = None):
+                 fused_ops: bool = True, group=None, model=None, step_fn=None, vocab: int | None = None,
+                 fsdp: bool = False, kl_coef: float = 0.0, layers: int | None = None):
         from .finetune.grad_sync import GradBuckets
         from .finetune.optim import get_optimizer
+        from .finetune.sharding import shard_model
 
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.group = group
         world = dist.get_world_size(group) if dist.is_initialized() else 1
         rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.world, self.tokens, self.micro_batches = world, tokens, micro_batches
-        self.model = model if model is not None else qwen2_model(name, self.device, grad_ckpt, fused_ops)
+        self.model = model if model is not None else qwen2_model(name, self.device, grad_ckpt, fused_ops, layers)
+        self.fsdp = fsdp
+        if fsdp:  # FSDP2 over the default group (finetune/sharding.py): it reduce-scatters the grads
+            if group is not None:
+                raise ValueError("fsdp shards over the default process group")
+            self.model = shard_model(self.model)
         if step_fn is None:
             from .finetune.rl import rl_step as step_fn
         self.step_fn = step_fn
         self.opt = get_optimizer("adamw_torch", self.model, 1e-6, 0.01)
-        self.grads = GradBuckets(list(self.model.parameters()), group=group) if world > 1 else None
+        self.grads = GradBuckets(list(self.model.parameters()), group=group) if world > 1 and not fsdp else None
         V = vocab or QWEN[name]["vocab_size"]
-        self.batches = [packed_batch(tokens, seq, prompt, V, self.device, seed=rank * 97 + i)
+        self.batches = [packed_batch(tokens, seq, prompt, V, self.device, seed=rank * 97 + i, ref_noise=kl_coef > 0)
                         for i in range(micro_batches)]
-        self.cfg = rl_config(micro_batches * (tokens // seq) * world, fused_head)
+        self.cfg = rl_config(micro_batches * (tokens // seq) * world, fused_head, kl_coef)
 
     def step(self, wum=None, version: int = 0) -> None:
+        from .finetune.sharding import set_gradient_sync
+
         for i, b in enumerate(self.batches):
             if self.grads is not None and i == len(self.batches) - 1:
                 self.grads.arm()
+            if self.fsdp:  # reduce-scatter on the boundary micro-batch only (the reference's no_sync)
+                set_gradient_sync(self.model, i == len(self.batches) - 1)
             loss, _ = self.step_fn(self.model, b, 0, 100, self.cfg)
             loss.backward()
         if self.grads is not None:
@@ -178,6 +196,28 @@ def trainer_step_probe(name: str = "1.5b", tokens: int = 16384, seq: int = 2048,
             "ms_per_optimizer_step": round(sec * 1e3, 2),
             "tokens_per_s": round(total / sec, 1), "tokens_per_s_per_gpu": round(total / sec / world, 1),
             "peak_mem_gb": round(peak, 2), "steps": steps, "warmup": warmup}
+
+
+def fsdp_step_probe(name: str = "32b", tokens: int = 4096, seq: int = 2048, prompt: int = 256,
+                    micro_batches: int = 1, steps: int = 2, warmup: int = 1, device=None, kl_coef: float = 0.001,
+                    layers: int | None = None) -> dict:
+    """BASELINE.json configs[4] (C5): Qwen2.5-32B shapes sharded with FSDP2 over every rank (RCCL
+    all-gather / reduce-scatter), KL-to-reference on, packed micro-batches; the whole optimizer
+    step as the trainer runs it with ``sharding: fsdp``.  Collective over the default group."""
+    device = device or torch.device("cuda", torch.cuda.current_device())
+    torch.cuda.reset_peak_memory_stats(device)
+    ts = TrainerStep(name, tokens, seq, prompt, micro_batches, device, fsdp=True, kl_coef=kl_coef, layers=layers)
+    sec = ts.timed(steps, warmup)
+    world = ts.world
+    peak = torch.cuda.max_memory_allocated(device) / 1e9
+    ts.close()
+    total = tokens * micro_batches * world
+    n_layers = layers or QWEN[name]["num_hidden_layers"]
+    return {"model": f"Qwen2.5-{name} shapes ({n_layers} layers, random init, bf16), FSDP2 over {world} ranks",
+            "kl_coef": kl_coef, "tokens_per_micro_batch": tokens, "micro_batches_per_step": micro_batches,
+            "seq_len": seq, "ms_per_optimizer_step": round(sec * 1e3, 2), "tokens_per_s": round(total / sec, 1),
+            "tokens_per_s_per_gpu": round(total / sec / world, 1), "peak_mem_gb": round(peak, 2),
+            "steps": steps, "warmup": warmup}
 
 
 def split_pipeline_probe(actors: int, steps: int = 2, warmup: int = 1, device=None, transport: str = "bucketed",

@@ -75,3 +75,33 @@ def test_split_pipeline_gloo(tmp_path, world, actors):
     for r in range(1, n_tr):  # DP replicas stay identical
         for n, p in got[0]["params"].items():
             assert torch.equal(got[r]["params"][n], p), (r, n)
+
+
+def _fsdp_run(rank, port, world, out):
+    sys.path[:0] = [str(ROOT), str(ROOT / "pipelinerl-swe_amd"), str(ROOT / "tests")]
+    os.environ["OMP_NUM_THREADS"] = "1"
+    import torch.distributed as dist
+    from cpu_rl_step import cpu_rl_step
+    from pipelinerl_amd.trainer_probe import TrainerStep
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    ts = TrainerStep(tokens=64, seq=32, prompt=8, micro_batches=2, device=torch.device("cpu"), model=_tiny().float(),
+                     step_fn=cpu_rl_step, vocab=96, fsdp=True, kl_coef=0.001)
+    assert ts.cfg.kl_coef == 0.001 and ts.grads is None
+    assert not torch.equal(ts.batches[0].ref_logprobs, ts.batches[0].old_logprobs)  # KL term is live
+    sec = ts.timed(2, 1)
+    full = {n: p.detach().full_tensor().clone() for n, p in ts.model.named_parameters()}
+    torch.save({"sec": sec, "params": full}, Path(out) / f"f{rank}.pt")
+    dist.destroy_process_group()
+
+
+def test_fsdp_trainer_step_gloo(tmp_path):
+    """The configs[4] probe's step (TrainerStep(fsdp=True), KL on) on gloo world 2: runs, and the
+    gathered parameters agree on both ranks after three optimizer steps."""
+    from test_weight_update_cpu import free_port
+
+    mp.spawn(_fsdp_run, args=(free_port(), 2, str(tmp_path)), nprocs=2, join=True)
+    a, b = (torch.load(tmp_path / f"f{r}.pt") for r in range(2))
+    assert a["sec"] > 0 and b["sec"] > 0
+    for n, p in a["params"].items():
+        assert torch.equal(p, b["params"][n]), n
