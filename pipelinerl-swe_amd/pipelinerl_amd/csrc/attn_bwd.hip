@@ -416,6 +416,24 @@ __device__ __forceinline__ void attn_bwd_dq(const __bf16* __restrict__ q, const 
     }
 }
 
+#ifndef PRL_ATTN_XCD
+#define PRL_ATTN_XCD 1  // A/B (tools/build_variants.py attn_xcd_off): fwd 28/4 heads 0.343 -> 0.318 ms at 8 x 2048
+#endif
+// XCD-aware order of the query-block workgroups (forward, dQ role).  Workgroups are dealt round-
+// robin over the 8 XCDs (blocks b and b + 8 share an L2), so the `rep` query heads of one kv group
+// (consecutive logical blocks, reading the same K / V stages) would land on `rep` different L2s.
+// Remap: physical block b (x = b % 8, s = b / 8) runs logical group j = (s / G) * 8 + x, member
+// s % G, so a group's G blocks share an XCD while consecutive groups still go to different XCDs
+// (the heaviest-first item order is kept across the chip).  Bijective on [0, N - N % (8 G));
+// the tail keeps the identity.
+__device__ __forceinline__ int xcd_group_remap(int b, int n, int G) {
+  if (!PRL_ATTN_XCD || G <= 1) return b;
+  const int main = n - n % (8 * G);
+  if (b >= main) return b;
+  const int x = b & 7, sl = b >> 3;
+  return ((sl / G) * 8 + x) * G + sl % G;
+}
+
 // One launch for both roles: workgroups [0, n_kv * Hkv) compute dK/dV of a (key block, kv head),
 // the rest dQ of a (query block, query head), so the lighter dQ workgroups fill the causal tail.
 __global__ __launch_bounds__(256) void attn_bwd_fused(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
@@ -431,9 +449,10 @@ __global__ __launch_bounds__(256) void attn_bwd_fused(const __bf16* __restrict__
   if (b < n_kv * Hkv)
     attn_bwd_dkdv(q, k, v, dout, lse2, delta, kv_items, dk, dv, T, H, Hkv, c2, scale, b / Hkv, b % Hkv, s0, s1, sL,
                   sDl);
-  else
-    attn_bwd_dq(q, k, v, dout, lse2, delta, q_items, dq, T, H, Hkv, c2, scale, (b - n_kv * Hkv) / H,
-                (b - n_kv * Hkv) % H, s0, s1);
+  else {
+    const int lq = xcd_group_remap(b - n_kv * Hkv, (int)gridDim.x - n_kv * Hkv, H / Hkv);
+    attn_bwd_dq(q, k, v, dout, lse2, delta, q_items, dq, T, H, Hkv, c2, scale, lq / H, lq % H, s0, s1);
+  }
 }
 
 // Forward (same structure as the dQ role): one workgroup = 128 queries of one query head, each
@@ -496,7 +515,8 @@ __global__ __launch_bounds__(256, PRL_ATTN_FWD_MINB) void attn_fwd(const __bf16*
                                                 int Hkv, float c2) {
   __shared__ __attribute__((aligned(16))) char sK[STAGE * D * 2], sV[STAGE * D * 2];
   const int tid = threadIdx.x;
-  const int it = blockIdx.x / H, h = blockIdx.x % H;
+  const int lb = xcd_group_remap(blockIdx.x, gridDim.x, H / Hkv);
+  const int it = lb / H, h = lb % H;
   const int s0 = items[3 * it], s1 = items[3 * it + 1], qb = items[3 * it + 2];
   const int lane = tid & 63, w = tid >> 6, hi = lane >> 5, l32 = lane & 31;
   const int64_t rs = (int64_t)H * D, rsk = (int64_t)Hkv * D;

@@ -14,6 +14,7 @@ VARIANTS = {
     "copy_ceiling": {"PRL_COPY_CEILING": "1"},
     "row_sequential": {"PRL_ROW_PERMUTE": "0"},
     "swiglu_u1": {"SWIGLU_UNROLL": "1"},
+    "attn_xcd_off": {"PRL_ATTN_XCD": "0"},
     "swiglu_u2": {"SWIGLU_UNROLL": "2"},
     "attn_fwd_1wave": {"PRL_ATTN_FWD_MINB": "1"},
     "attn_serial": {"PRL_ATTN_INTERLEAVE": "0"},
