@@ -66,7 +66,7 @@ def shard_model(model, fsdp_cfg=None, grad_reduce: str = "mean", reshard_after_f
     for m in [*layers, model]:
         if grad_reduce == "sum":
             m.set_gradient_divide_factor(1.0)
-        if dist.get_backend() == "gloo":  # gloo has no PREMUL_SUM / AVG: plain SUM + a scale
+        if "nccl" not in str(dist.get_backend()):  # gloo has no PREMUL_SUM / AVG: plain SUM + a scale
             m.set_force_sum_reduction_for_comms(True)
     logger.info(f"FSDP: {len(layers)} decoder layers + root sharded over {dist.get_world_size()} ranks "
                 f"(param_dtype {mp.param_dtype}, reduce_dtype {mp.reduce_dtype})")
