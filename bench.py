@@ -142,8 +142,8 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        if rehearse:
-            dist.init_process_group("gloo")
+        if rehearse:  # gloo for CUDA tensors too (FSDP's device mesh would open RCCL groups)
+            dist.init_process_group("cpu:gloo,cuda:gloo")
         else:
             dist.init_process_group("nccl", device_id=dev)
 
@@ -230,12 +230,13 @@ def main():
         logits = fields = None
         torch.cuda.empty_cache()
         actors = world // 2
+        split_model = "1.5b" if rehearse else "7b"  # every rehearsal rank shares one GPU's memory
         split = split_pipeline_probe(
             actors, steps=2, warmup=1, device=dev,
-            make_trainer=lambda g: TrainerStep("7b", tokens=16384, micro_batches=2, device=dev, group=g),
-            make_actor_module=lambda: comm_probe.ShapedModule(comm_probe.qwen2_param_shapes("7b"), device=dev,
+            make_trainer=lambda g: TrainerStep(split_model, tokens=16384, micro_batches=2, device=dev, group=g),
+            make_actor_module=lambda: comm_probe.ShapedModule(comm_probe.qwen2_param_shapes(split_model), device=dev,
                                                               fill=0.0))
-        split["model"] = "Qwen2.5-7b shapes (random init, bf16), 2 x 16384-token micro-batches per trainer rank"
+        split["model"] = f"Qwen2.5-{split_model} shapes (random init, bf16), 2 x 16384-token micro-batches per trainer rank"
         torch.cuda.empty_cache()
 
     fsdp = None
@@ -244,7 +245,8 @@ def main():
         from pipelinerl_amd.trainer_probe import fsdp_step_probe
 
         torch.cuda.empty_cache()
-        fsdp = fsdp_step_probe("32b", tokens=4096, micro_batches=1, steps=2, warmup=1, device=dev, kl_coef=0.001)
+        fsdp = fsdp_step_probe("32b", tokens=4096, micro_batches=1, steps=2, warmup=1, device=dev, kl_coef=0.001,
+                               layers=2 if rehearse else None)
         torch.cuda.empty_cache()
 
     if rank == 0:
