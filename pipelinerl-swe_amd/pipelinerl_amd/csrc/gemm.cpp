@@ -228,6 +228,17 @@ bool from_index(hipblasLtHandle_t h, const Key& k, Plan* p) {
   return true;
 }
 
+void destroy(Plan& p) {
+  if (p.desc) g_api.desc_destroy(p.desc);
+  if (p.la) g_api.layout_destroy(p.la);
+  if (p.lb) g_api.layout_destroy(p.lb);
+  if (p.ld) g_api.layout_destroy(p.ld);
+}
+
+// Packed micro-batches have a different token count almost every time, so the cache is bounded:
+// past kMaxPlans entries it is emptied (a plan costs one heuristic query, ~0.1 ms of host time).
+constexpr size_t kMaxPlans = 4096;
+
 int plan_for(int dev, hipblasLtHandle_t h, const Key& k, Plan** out) {
   auto key = std::make_pair(dev, k);
   auto it = g_plans.find(key);
@@ -235,14 +246,15 @@ int plan_for(int dev, hipblasLtHandle_t h, const Key& k, Plan** out) {
     *out = &it->second;
     return 0;
   }
+  if (g_plans.size() >= kMaxPlans) {  // callers hold no Plan pointer across calls (one lock scope)
+    for (auto& kv : g_plans) destroy(kv.second);
+    g_plans.clear();
+  }
   Plan p;
   int rc = make_layouts(k, &p);
   if (!rc && !(k.solution >= 0 && from_index(h, k, &p))) rc = heuristic(h, &p);
   if (rc) {
-    if (p.desc) g_api.desc_destroy(p.desc);
-    if (p.la) g_api.layout_destroy(p.la);
-    if (p.lb) g_api.layout_destroy(p.lb);
-    if (p.ld) g_api.layout_destroy(p.ld);
+    destroy(p);
     return rc;
   }
   *out = &(g_plans[key] = p);
