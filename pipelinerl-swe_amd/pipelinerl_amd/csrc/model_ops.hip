@@ -90,8 +90,10 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd(const uint16_t* __restrict__ 
 
 // dx_i = r g_i - (r^3 / H) x_i sum_j g_j x_j with g = bf16(dy * w);  dw partial per block:
 // sum over the block's rows of bf16(dy * bf16(x r)) (the eager chain's weight-grad product).
+// dx_i = r g_i - (r^3 / H) x_i sum_j g_j x_j with g = bf16(dy * w);  dw partial per block:
+// sum over the block's rows of bf16(dy * bf16(x r)) (the eager chain's weight-grad product).
 template <int NV>
-__global__ __launch_bounds__(256) void rmsnorm_bwd(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
+__global__ __launch_bounds__(256) void rmsnorm_bwd_narrow(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
                                                    const uint16_t* __restrict__ w, const float* __restrict__ rstd,
                                                    uint16_t* __restrict__ dx, float* __restrict__ partial,
                                                    int64_t rows, int H) {
@@ -155,6 +157,116 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd(const uint16_t* __restrict__ 
   __syncthreads();
   for (int i = threadIdx.x; i < H; i += 256)
     partial[(int64_t)blockIdx.x * H + i] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+}
+
+// Wide rows (NV > 4, e.g. H = 3584): the dw partials of the 4 waves fold through ONE LDS row, in
+// wave order, so the block needs H floats of LDS instead of 4 H, and w / x / dy stay packed
+// between uses: 0.254 -> 0.217 ms at 16384 x 3584 (tools/ew_bench.py).  Narrow rows keep the
+// 4-row fold (rmsnorm_bwd_narrow), which measured faster at H = 1536 (0.179 vs 0.193 ms).
+template <int NV>
+__global__ __launch_bounds__(256) void rmsnorm_bwd_wide(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
+                                                   const uint16_t* __restrict__ w, const float* __restrict__ rstd,
+                                                   uint16_t* __restrict__ dx, float* __restrict__ partial,
+                                                   int64_t rows, int H) {
+  __shared__ float red[64 * 8 * NV];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t wave = (int64_t)blockIdx.x * 4 + wid;
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
+  const int nv8 = H >> 3;
+  const float invH = 1.0f / (float)H;
+  u32x4 wv[NV];
+  float acc[NV][8];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int c = k * 64 + lane;
+    wv[k] = c < nv8 ? reinterpret_cast<const u32x4*>(w)[c] : u32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[k][j] = 0.f;
+  }
+  u32x4 xv[NV], gv[NV];
+  auto load_row = [&](int64_t r, u32x4* xo, u32x4* go) {
+    const u32x4* xr = reinterpret_cast<const u32x4*>(x + r * H);
+    const u32x4* gr = reinterpret_cast<const u32x4*>(dy + r * H);
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = k * 64 + lane;
+      xo[k] = c < nv8 ? __builtin_nontemporal_load(xr + c) : u32x4{0, 0, 0, 0};
+      go[k] = c < nv8 ? __builtin_nontemporal_load(gr + c) : u32x4{0, 0, 0, 0};
+    }
+  };
+  if (wave < rows) load_row(wave, xv, gv);
+  float rs = wave < rows ? rstd[wave] : 0.f;
+  for (int64_t r = wave; r < rows; r += nwaves) {
+    constexpr bool kPrefetch = false;  // measured: no gain at H = 1536, registers better spent on occupancy
+    u32x4 xn[kPrefetch ? NV : 1], gn[kPrefetch ? NV : 1];
+    const int64_t rn = r + nwaves;
+    float rsn = 0.f;
+    if (kPrefetch && rn < rows) {  // in flight during this row's math
+      load_row(rn, xn, gn);
+      rsn = rstd[rn];
+    }
+    // register pressure: keep w packed (no hoisted unpacked copy across the loop) so the kernel
+    // runs more than one wave per SIMD
+#pragma unroll
+    for (int k = 0; k < NV; ++k) asm volatile("" : "+v"(wv[k]));
+    float dot = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float g0 = r16(lo(gv[k][j]) * lo(wv[k][j])), g1 = r16(hi(gv[k][j]) * hi(wv[k][j]));
+        dot = __builtin_fmaf(g0, lo(xv[k][j]), __builtin_fmaf(g1, hi(xv[k][j]), dot));
+        const float t0 = r16(lo(xv[k][j]) * rs), t1 = r16(hi(xv[k][j]) * rs);
+        acc[k][2 * j] += r16(lo(gv[k][j]) * t0);
+        acc[k][2 * j + 1] += r16(hi(gv[k][j]) * t1);
+      }
+    }
+    dot = wave_sum(dot);
+    const float cfac = rs * rs * rs * invH * dot;
+    u32x4* dr = reinterpret_cast<u32x4*>(dx + r * H);
+#pragma unroll
+    for (int k = 0; k < NV; ++k) asm volatile("" : "+v"(xv[k]), "+v"(gv[k]), "+v"(wv[k]));  // re-unpack below
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = k * 64 + lane;
+      if (c < nv8) {
+        u32x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float g0 = r16(lo(gv[k][j]) * lo(wv[k][j])), g1 = r16(hi(gv[k][j]) * hi(wv[k][j]));
+          o[j] = pack(rs * g0 - cfac * lo(xv[k][j]), rs * g1 - cfac * hi(xv[k][j]));
+        }
+        __builtin_nontemporal_store(o, dr + c);
+      }
+    }
+    if (rn < rows) {
+      if constexpr (kPrefetch) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+          xv[k] = xn[k];
+          gv[k] = gn[k];
+        }
+        rs = rsn;
+      } else {
+        load_row(rn, xv, gv);
+        rs = rstd[rn];
+      }
+    }
+  }
+  // block partial of dw: the 4 waves fold into one LDS row in wave order (deterministic)
+  for (int wi = 0; wi < 4; ++wi) {
+    if (wid == wi) {
+#pragma unroll
+      for (int k = 0; k < NV; ++k)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float& cell = red[(k * 64 + lane) * 8 + j];
+          cell = wi ? cell + acc[k][j] : acc[k][j];
+        }
+    }
+    __syncthreads();
+  }
+  for (int i = threadIdx.x; i < H; i += 256) partial[(int64_t)blockIdx.x * H + i] = red[i];
 }
 
 // dw = sum over the bwd kernel's block partials, deterministic, two levels:
@@ -337,7 +449,8 @@ hipError_t launch_norm_fwd(const void* x, const void* w, void* y, float* rstd, i
 template <int NV>
 hipError_t launch_norm_bwd(const void* dy, const void* x, const void* w, const float* rstd, void* dx, float* partial,
                            int64_t rows, int H, int grid, hipStream_t s) {
-  hipLaunchKernelGGL(rmsnorm_bwd<NV>, dim3(grid), dim3(256), 0, s, (const uint16_t*)dy, (const uint16_t*)x,
+  hipLaunchKernelGGL((NV <= 4 ? rmsnorm_bwd_narrow<NV> : rmsnorm_bwd_wide<NV>), dim3(grid), dim3(256), 0, s,
+                     (const uint16_t*)dy, (const uint16_t*)x,
                      (const uint16_t*)w, rstd, (uint16_t*)dx, partial, rows, H);
   return hipGetLastError();
 }

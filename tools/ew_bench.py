@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--tokens", type=int, default=65536)
     ap.add_argument("--inter", type=int, default=8960)
     ap.add_argument("--hidden", type=int, default=1536)
+    ap.add_argument("--rows7b", type=int, default=16384)
     a = ap.parse_args()
     lib = _native.load()
     st = torch.cuda.current_stream().cuda_stream
@@ -51,6 +52,20 @@ def main():
     ms = timed(lambda: lib.prl_swiglu_backward(dh.data_ptr(), g.data_ptr(), u.data_ptr(), dg.data_ptr(), du.data_ptr(), n,
                                                st))
     out["swiglu_bwd"] = {"ms": round(ms, 4), "TBps": round(10 * n / ms / 1e9, 3)}
+    del g, u, dh, h, dg, du
+    from pipelinerl_amd.finetune.model_ops import RMSNormFn
+
+    for rows, hid in ((T, H), (a.rows7b, 3584)):
+        x = torch.randn((rows, hid), device="cuda").to(torch.bfloat16).requires_grad_()
+        w = torch.ones(hid, device="cuda", dtype=torch.bfloat16).requires_grad_()
+        dy = torch.randn((rows, hid), device="cuda").to(torch.bfloat16)
+        y = RMSNormFn.apply(x, w, 1e-6)
+        ms_f = timed(lambda: RMSNormFn.apply(x.detach(), w.detach(), 1e-6))
+        ms_b = timed(lambda: torch.autograd.grad(y, (x, w), dy, retain_graph=True))
+        nb = rows * hid * 2
+        out[f"rmsnorm_{rows}x{hid}"] = {"fwd_ms": round(ms_f, 4), "fwd_TBps": round(2 * nb / ms_f / 1e9, 3),
+                                        "bwd_ms": round(ms_b, 4), "bwd_TBps": round(3 * nb / ms_b / 1e9, 3)}
+        del x, w, dy, y
     print(json.dumps(out), flush=True)
 
 
