@@ -293,9 +293,19 @@ __device__ __forceinline__ void grad_vec(const float (&x)[VEC], float (&d)[VEC],
   }
 }
 
-template <typename T, int VEC>
-__global__ __launch_bounds__(256) void grpo_fwd_stream(KArgs a) {
-  constexpr int BLOCK = 256, NW = BLOCK / 64;
+#ifndef PRL_STREAM_F32_U
+#define PRL_STREAM_F32_U 4
+#endif
+#ifndef PRL_STREAM_F32_WG_PER_CU
+#define PRL_STREAM_F32_WG_PER_CU 1
+#endif
+// BLOCK threads per row, U vectors per thread in flight per loop step.  The fp32 form (rows of
+// 594 KiB do not fit the register file) runs 1024-thread workgroups, one per CU, 4 vectors per
+// thread: 64 KiB of loads in flight per CU, and only ~#CUs rows (~150 MB) between a row's first
+// read and its re-read, so the gradient pass's re-read is served by the 256 MiB Infinity Cache.
+template <typename T, int VEC, int BLOCK = 256, int U = 1>
+__global__ __launch_bounds__(BLOCK) void grpo_fwd_stream(KArgs a) {
+  constexpr int NW = BLOCK / 64;
   __shared__ float red[2][NW][3];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int64_t nrows = fwd_rows(a);
@@ -314,7 +324,15 @@ __global__ __launch_bounds__(256) void grpo_fwd_stream(KArgs a) {
     const int64_t tgt = bad_id ? -1 : tid_raw;
     const float xt = bad_id ? __builtin_nanf("") : scalar_logit<T>(row, tgt);
     Lse st = lse_empty();
-    for (int64_t gv = tid; gv < nvec; gv += BLOCK) {
+    int64_t gv = tid;
+    for (; gv + (U - 1) * BLOCK < nvec; gv += U * BLOCK) {
+      float x[U][VEC];
+#pragma unroll
+      for (int u = 0; u < U; ++u) RowIO<T, VEC>::load(row, gv + u * BLOCK, x[u]);
+#pragma unroll
+      for (int u = 0; u < U; ++u) lse_add<VEC>(st, x[u], c);
+    }
+    for (; gv < nvec; gv += BLOCK) {
       float x[VEC];
       RowIO<T, VEC>::load(row, gv, x);
       lse_add<VEC>(st, x, c);
@@ -339,17 +357,36 @@ __global__ __launch_bounds__(256) void grpo_fwd_stream(KArgs a) {
       const float beta = -core.g_h * kLn2 * inv_t;
       const float gadd = core.g_lp * inv_t;
       const bool zero_row = (core.g_lp == 0.f && core.g_h == 0.f);
-      for (int64_t gv = tid; gv < nvec; gv += BLOCK) {
+      int64_t g2 = tid;
+      for (; g2 + (U - 1) * BLOCK < nvec; g2 += U * BLOCK) {
+        float d[U][VEC];
+        if (zero_row) {
+#pragma unroll
+          for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int j = 0; j < VEC; ++j) d[u][j] = 0.f;
+        } else {
+          float x[U][VEC];
+#pragma unroll
+          for (int u = 0; u < U; ++u) RowIO<T, VEC>::load(row, g2 + u * BLOCK, x[u]);
+#pragma unroll
+          for (int u = 0; u < U; ++u)
+            grad_vec<VEC>(x[u], d[u], c, M, l2s, alpha, beta, (g2 + u * BLOCK) * VEC, tgt, gadd);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) RowIO<T, VEC>::store(drow, g2 + u * BLOCK, d[u]);
+      }
+      for (; g2 < nvec; g2 += BLOCK) {
         float d[VEC];
         if (zero_row) {
 #pragma unroll
           for (int j = 0; j < VEC; ++j) d[j] = 0.f;
         } else {
           float x[VEC];
-          RowIO<T, VEC>::load(row, gv, x);
-          grad_vec<VEC>(x, d, c, M, l2s, alpha, beta, gv * VEC, tgt, gadd);
+          RowIO<T, VEC>::load(row, g2, x);
+          grad_vec<VEC>(x, d, c, M, l2s, alpha, beta, g2 * VEC, tgt, gadd);
         }
-        RowIO<T, VEC>::store(drow, gv, d);
+        RowIO<T, VEC>::store(drow, g2, d);
       }
     }
   }
@@ -634,7 +671,9 @@ static hipError_t launch_rows(const KArgs& a, const PrlGrpoBatch* b, const PrlGr
     hipLaunchKernelGGL((grpo_fwd_stream<uint16_t, 1>), dim3(grid), dim3(256), 0, s, a);
   } else if (b->V % 4 == 0 && b->ld % 4 == 0 && aligned16(b->logits) &&
              (!p->write_grad || aligned16(out->dlogits))) {
-    hipLaunchKernelGGL((grpo_fwd_stream<float, 4>), dim3(grid), dim3(256), 0, s, a);
+    const int64_t want1 = (int64_t)cus * PRL_STREAM_F32_WG_PER_CU;  // 1024-thread workgroups
+    const int g1 = (int)(nrows < want1 ? nrows : want1);
+    hipLaunchKernelGGL((grpo_fwd_stream<float, 4, 1024, PRL_STREAM_F32_U>), dim3(g1), dim3(1024), 0, s, a);
   } else {
     hipLaunchKernelGGL((grpo_fwd_stream<float, 1>), dim3(grid), dim3(256), 0, s, a);
   }

@@ -15,6 +15,8 @@ VARIANTS = {
     "row_sequential": {"PRL_ROW_PERMUTE": "0"},
     "swiglu_u1": {"SWIGLU_UNROLL": "1"},
     "attn_xcd_off": {"PRL_ATTN_XCD": "0"},
+    "f32_u2": {"PRL_STREAM_F32_U": "2"},
+    "f32_wg2": {"PRL_STREAM_F32_WG_PER_CU": "2"},
     "swiglu_u2": {"SWIGLU_UNROLL": "2"},
     "attn_fwd_1wave": {"PRL_ATTN_FWD_MINB": "1"},
     "attn_serial": {"PRL_ATTN_INTERLEAVE": "0"},
