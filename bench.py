@@ -197,27 +197,44 @@ def main():
         dist.all_reduce(k_max, op=dist.ReduceOp.MAX)
     elapsed = float(t_max)
     kern_ms = float(k_max)
+    # The probes below are reported beside `value`, never in it.  A probe that raises (on every rank
+    # alike: they are collective) is reported as an error and the later probes are skipped, so the
+    # bench line is still printed.
+    failed: list[str] = []
+
+    def optional(name: str, fn):
+        if failed:
+            return {"skipped": f"after the {failed[0]} probe failed"}
+        try:
+            return fn()
+        except Exception as e:  # noqa: BLE001
+            failed.append(name)
+            torch.cuda.empty_cache()
+            return {"error": f"{type(e).__name__}: {e}"[:400]}
+
+    logits = fields = None
+    torch.cuda.empty_cache()
     comm = None
     if world > 1 and not args.no_comm_probe:
         # the trainer's two exchange steps on the C2 model's parameter set, measured after the
-        # timed region (not part of `value`): DP gradient all-reduce, trainer -> actors broadcast
+        # timed region: DP gradient all-reduce, trainer -> actors broadcast
         from pipelinerl_amd import comm_probe
 
-        logits = fields = None
-        torch.cuda.empty_cache()
-        shapes = comm_probe.qwen2_param_shapes("1.5b")
-        comm = {"model": "Qwen2.5-1.5B parameter shapes, bf16",
-                "grad_allreduce": comm_probe.grad_allreduce_probe(shapes, dev, iters=5),
-                "weight_broadcast": comm_probe.broadcast_probe(shapes, dev, iters=3)}
+        def exchange():
+            shapes = comm_probe.qwen2_param_shapes("1.5b")
+            return {"model": "Qwen2.5-1.5B parameter shapes, bf16",
+                    "grad_allreduce": comm_probe.grad_allreduce_probe(shapes, dev, iters=5),
+                    "weight_broadcast": comm_probe.broadcast_probe(shapes, dev, iters=3)}
+
+        comm = optional("exchange", exchange)
     trainer = None
     if not args.no_trainer_step:
-        # the whole optimizer step the loss head sits in (reported beside `value`, not in it)
+        # the whole optimizer step the loss head sits in
         from pipelinerl_amd.trainer_probe import trainer_step_probe
 
-        logits = fields = None
         torch.cuda.empty_cache()
-        trainer = trainer_step_probe("1.5b", tokens=T, micro_batches=2, steps=2, warmup=1, device=dev,
-                                     fused_head=True)
+        trainer = optional("trainer_step", lambda: trainer_step_probe("1.5b", tokens=T, micro_batches=2, steps=2,
+                                                                      warmup=1, device=dev, fused_head=True))
 
     split = None
     if world > 1 and not args.no_split_pipeline:
@@ -227,16 +244,19 @@ def main():
         from pipelinerl_amd import comm_probe
         from pipelinerl_amd.trainer_probe import TrainerStep, split_pipeline_probe
 
-        logits = fields = None
         torch.cuda.empty_cache()
-        actors = world // 2
         split_model = "1.5b" if rehearse else "7b"  # every rehearsal rank shares one GPU's memory
-        split = split_pipeline_probe(
-            actors, steps=2, warmup=1, device=dev,
-            make_trainer=lambda g: TrainerStep(split_model, tokens=16384, micro_batches=2, device=dev, group=g),
-            make_actor_module=lambda: comm_probe.ShapedModule(comm_probe.qwen2_param_shapes(split_model), device=dev,
-                                                              fill=0.0))
-        split["model"] = f"Qwen2.5-{split_model} shapes (random init, bf16), 2 x 16384-token micro-batches per trainer rank"
+
+        def split_run():
+            r = split_pipeline_probe(
+                world // 2, steps=2, warmup=1, device=dev,
+                make_trainer=lambda g: TrainerStep(split_model, tokens=16384, micro_batches=2, device=dev, group=g),
+                make_actor_module=lambda: comm_probe.ShapedModule(comm_probe.qwen2_param_shapes(split_model),
+                                                                  device=dev, fill=0.0))
+            r["model"] = f"Qwen2.5-{split_model} shapes (random init, bf16), 2 x 16384-token micro-batches per trainer rank"
+            return r
+
+        split = optional("split_pipeline", split_run)
         torch.cuda.empty_cache()
 
     fsdp = None
@@ -245,8 +265,9 @@ def main():
         from pipelinerl_amd.trainer_probe import fsdp_step_probe
 
         torch.cuda.empty_cache()
-        fsdp = fsdp_step_probe("32b", tokens=4096, micro_batches=1, steps=2, warmup=1, device=dev, kl_coef=0.001,
-                               layers=2 if rehearse else None)
+        fsdp = optional("fsdp_32b", lambda: fsdp_step_probe("32b", tokens=4096, micro_batches=1, steps=2, warmup=1,
+                                                             device=dev, kl_coef=0.001,
+                                                             layers=2 if rehearse else None))
         torch.cuda.empty_cache()
 
     if rank == 0:
