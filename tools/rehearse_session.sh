@@ -1,5 +1,6 @@
-# one-GPU rehearsal of bench.py's N > 1 control flow (gloo, every rank on cuda:0) + GEMM A/B
+# One-GPU rehearsal of bench.py's N > 1 control flow: every rank on cuda:0 over gloo
+# (PRL_BENCH_REHEARSE=gloo; small split / FSDP shapes).  Timings are meaningless; it checks that
+# every probe of the N = 2 and N = 4 bench lines completes and verifies its result.
 bash tools/gpu_session.sh \
- "rehearse2:420:PRL_BENCH_REHEARSE=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2 --tokens 16384 --no-trainer-step" \
- "gemm_base:200:python tools/gemm_shapes_bench.py 65536 1.5b" \
- "gemm_tuned:200:PYTORCH_TUNABLEOP_ENABLED=1 PYTORCH_TUNABLEOP_TUNING=0 PYTORCH_TUNABLEOP_FILENAME=tools/tunableop.csv python tools/gemm_shapes_bench.py 65536 1.5b"
+ "rehearse2:600:PRL_BENCH_REHEARSE=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2 --tokens 16384" \
+ "rehearse4:900:PRL_BENCH_REHEARSE=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 4 --steps 5 --warmup 2 --tokens 16384"
