@@ -441,9 +441,8 @@ __global__ __launch_bounds__(256) void grpo_bwd_stream(KArgs a, const float* max
 // Statistics (rl/__init__.py:315-375) and value-head gradient from the per-row outputs.
 // Block b owns rows [b*chunk, (b+1)*chunk); each thread folds its rows in a fixed order,
 // then the block folds threads in index order: deterministic for a given row count.
-constexpr int kStatThreads = 256;
+constexpr int kStatThreads = 64;  // one wave per block: no LDS, several blocks per CU
 __global__ __launch_bounds__(kStatThreads) void grpo_stats_partial(KArgs a, int64_t chunk) {
-  __shared__ double sh[kStatThreads][PRL_NSTAT + 1];
   const int tid = threadIdx.x;
   const int64_t nrows = a.B * (a.L - 1);
   double acc[PRL_NSTAT];
@@ -514,33 +513,51 @@ __global__ __launch_bounds__(kStatThreads) void grpo_stats_partial(KArgs a, int6
 #pragma unroll
     for (int i = 0; i < PRL_NSTAT; ++i) acc[i] = stat_fold(i, acc[i], (double)c[i]);
   }
+  // block (= wave) fold per statistic: a fixed xor tree across the lanes — deterministic (both
+  // partners of a tree step compute the same commutative fold).  Was 256-thread blocks folded by
+  // one thread per statistic walking all 256 threads serially: 93 us per launch at C2, now ~10x less.
+  // fully unrolled so acc[] stays in registers (a dynamic index would put it in scratch)
+  static_assert(PRL_NSTAT == 39, "unroll count below");
+#pragma unroll 39
+  for (int i = 0; i < PRL_NSTAT; ++i) {
+    double r = acc[i];
 #pragma unroll
-  for (int i = 0; i < PRL_NSTAT; ++i) sh[tid][i] = acc[i];
-  __syncthreads();
-  if (tid < PRL_NSTAT) {
-    double r = stat_identity(tid);
-    for (int t = 0; t < kStatThreads; ++t) r = stat_fold(tid, r, sh[t][tid]);
-    a.partials[(int64_t)blockIdx.x * PRL_NSTAT + tid] = r;
+    for (int o = 32; o > 0; o >>= 1) r = stat_fold(i, r, __shfl_xor(r, o, 64));
+    if (tid == 0) a.partials[(int64_t)i * gridDim.x + blockIdx.x] = r;  // stat-major: finalize reads coalesced
   }
 }
 
-// Fold the per-block partials: kFinLanes threads per statistic fold a strided subset in order,
-// then lane 0 folds those kFinLanes results in order (deterministic for a given block count).
-constexpr int kFinLanes = 16;
-__global__ __launch_bounds__(1024) void grpo_finalize(const double* __restrict__ partials, int nblocks,
-                                                      double* __restrict__ stats) {
-  __shared__ double sh[PRL_NSTAT][kFinLanes];
-  const int i = threadIdx.x / kFinLanes, j = threadIdx.x % kFinLanes;
-  if (i < PRL_NSTAT) {
-    double acc = stat_identity(i);
-    for (int b = j; b < nblocks; b += kFinLanes) acc = stat_fold(i, acc, partials[(int64_t)b * PRL_NSTAT + i]);
-    sh[i][j] = acc;
+// Fold the per-block partials (stat-major, partials[i * nblocks + b]): one workgroup per
+// statistic; thread t folds blocks t, t + 256, ... in order (4 loads in flight), each wave folds
+// its lanes with a fixed xor tree, then thread 0 folds the 4 waves in index order: deterministic
+// for a given block count.  One launch latency for all 39 statistics (was one 1024-thread
+// workgroup looping over them: 11-28 us).
+constexpr int kFinThreads = 256;
+__global__ __launch_bounds__(kFinThreads) void grpo_finalize(const double* __restrict__ partials, int nblocks,
+                                                             double* __restrict__ stats) {
+  __shared__ double wsum[kFinThreads / 64];
+  const int i = blockIdx.x, t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const double* p = partials + (int64_t)i * nblocks;
+  double acc = stat_identity(i);
+  for (int b0 = 0; b0 < nblocks; b0 += kFinThreads * 4) {
+    double v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int b = b0 + t + kFinThreads * k;
+      v[k] = b < nblocks ? p[b] : stat_identity(i);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc = stat_fold(i, acc, v[k]);
   }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc = stat_fold(i, acc, __shfl_xor(acc, o, 64));
+  if (lane == 0) wsum[wid] = acc;
   __syncthreads();
-  if (i < PRL_NSTAT && j == 0) {
-    double acc = stat_identity(i);
-    for (int k = 0; k < kFinLanes; ++k) acc = stat_fold(i, acc, sh[i][k]);
-    stats[i] = acc;
+  if (t == 0) {
+    double r = wsum[0];
+#pragma unroll
+    for (int w = 1; w < kFinThreads / 64; ++w) r = stat_fold(i, r, wsum[w]);
+    stats[i] = r;
   }
 }
 
@@ -684,7 +701,7 @@ static hipError_t launch_rows(const KArgs& a, const PrlGrpoBatch* b, const PrlGr
 static hipError_t launch_stats(const KArgs& a, int64_t nrows, double* stats, hipStream_t s) {
   int sblocks = 0;
   if (nrows > 0) {
-    // ~256 rows per 256-thread block: one row per thread, enough blocks to fill the chip
+    // >= 64 rows per one-wave block (one row per thread at C2), at most kMaxGrid blocks
     int64_t chunk = (nrows + kMaxGrid - 1) / kMaxGrid;
     if (chunk < kStatThreads) chunk = kStatThreads;
     sblocks = (int)((nrows + chunk - 1) / chunk);
@@ -692,7 +709,7 @@ static hipError_t launch_stats(const KArgs& a, int64_t nrows, double* stats, hip
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(grpo_finalize, dim3(1), dim3(PRL_NSTAT * kFinLanes), 0, s, a.partials, sblocks, stats);
+  hipLaunchKernelGGL(grpo_finalize, dim3(PRL_NSTAT), dim3(kFinThreads), 0, s, a.partials, sblocks, stats);
   return hipGetLastError();
 }
 
