@@ -218,6 +218,15 @@ int prl_rmsnorm_workspace_bytes(int64_t H, size_t* bytes);
 int prl_rmsnorm_backward(const void* dy, const void* x, const void* w, const float* rstd, void* dx,
                          void* dw, void* workspace, size_t workspace_bytes, int64_t rows, int64_t H,
                          void* stream);
+/* The decoder's residual add fused with the norm that reads its result (transformers
+ * Qwen2DecoderLayer.forward: `hidden = residual + hidden; ... norm(hidden)`): h = bf16(residual
+ * + x) written to h, y = rmsnorm(h).  Backward: dx = bf16(bf16(rmsnorm'(dy)) + dh), the gradient
+ * of both residual and x (dh = gradient reaching h through the residual stream). */
+int prl_add_rmsnorm_forward(const void* residual, const void* x, const void* w, void* h, void* y,
+                            float* rstd, int64_t rows, int64_t H, float eps, void* stream);
+int prl_add_rmsnorm_backward(const void* dy, const void* dh, const void* h, const void* w,
+                             const float* rstd, void* dx, void* dw, void* workspace,
+                             size_t workspace_bytes, int64_t rows, int64_t H, void* stream);
 /* out = bf16(bf16(silu(gate)) * up) over n elements; backward gives dgate, dup. */
 int prl_swiglu_forward(const void* gate, const void* up, void* out, int64_t n, void* stream);
 int prl_swiglu_backward(const void* dout, const void* gate, const void* up, void* dgate, void* dup,

@@ -85,6 +85,10 @@ _SIGNATURES = {
     "prl_rmsnorm_workspace_bytes": (c_int, [c_int64, POINTER(c_size_t)]),
     "prl_rmsnorm_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
                                      c_int64, c_int64, c_void_p]),
+    "prl_add_rmsnorm_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64,
+                                        c_float, c_void_p]),
+    "prl_add_rmsnorm_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                         c_void_p, c_size_t, c_int64, c_int64, c_void_p]),
     "prl_swiglu_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     "prl_swiglu_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     "prl_rope_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32,

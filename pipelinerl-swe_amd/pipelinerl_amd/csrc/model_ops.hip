@@ -7,6 +7,7 @@
 // exactly (same intermediate casts), so patched and unpatched models agree bit for bit in
 // the forward pass.
 //   rmsnorm   y = bf16(w * bf16(x * rsqrt(mean(x^2) + eps)))         (fp32 statistics)
+//   add_rmsnorm  h = bf16(residual + x), y = rmsnorm(h)            (decoder residual add fused)
 //   swiglu    h = bf16(bf16(silu(g)) * u)
 //   rope      q' = bf16(bf16(q * cos) + bf16(rotate_half(q) * sin))  (q and k in one launch)
 // HBM-bound: 16-B vector loads/stores, one wave per row for the norms.
@@ -40,10 +41,13 @@ __device__ __forceinline__ float wave_sum(float v) {
 
 // ---------------------------------------------------------------------------------------
 // RMSNorm.  One wave per row; the row (H <= 64 * 8 * NV bf16) stays in registers.
-template <int NV>
+// ADD: x is the sublayer output and the row normalised is h = bf16(res + x) (the decoder's
+// residual add, eager `residual + hidden_states`), also written to `hout`.
+template <int NV, bool ADD>
 __global__ __launch_bounds__(256) void rmsnorm_fwd(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
                                                    uint16_t* __restrict__ y, float* __restrict__ rstd,
-                                                   int64_t rows, int H, float eps) {
+                                                   int64_t rows, int H, float eps, const uint16_t* __restrict__ res,
+                                                   uint16_t* __restrict__ hout) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t nwaves = (int64_t)gridDim.x * 4;
@@ -62,6 +66,14 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd(const uint16_t* __restrict__ 
     for (int k = 0; k < NV; ++k) {
       const int c = k * 64 + lane;
       xv[k] = c < nv8 ? __builtin_nontemporal_load(xr + c) : u32x4{0, 0, 0, 0};
+      if constexpr (ADD) {
+        if (c < nv8) {
+          const u32x4 rv = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(res + r * H) + c);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) xv[k][j] = pack(lo(rv[j]) + lo(xv[k][j]), hi(rv[j]) + hi(xv[k][j]));
+          __builtin_nontemporal_store(xv[k], reinterpret_cast<u32x4*>(hout + r * H) + c);
+        }
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const float a = lo(xv[k][j]), b = hi(xv[k][j]);
@@ -92,11 +104,11 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd(const uint16_t* __restrict__ 
 // sum over the block's rows of bf16(dy * bf16(x r)) (the eager chain's weight-grad product).
 // dx_i = r g_i - (r^3 / H) x_i sum_j g_j x_j with g = bf16(dy * w);  dw partial per block:
 // sum over the block's rows of bf16(dy * bf16(x r)) (the eager chain's weight-grad product).
-template <int NV>
+template <int NV, bool ADD>
 __global__ __launch_bounds__(256) void rmsnorm_bwd_narrow(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
                                                    const uint16_t* __restrict__ w, const float* __restrict__ rstd,
                                                    uint16_t* __restrict__ dx, float* __restrict__ partial,
-                                                   int64_t rows, int H) {
+                                                   int64_t rows, int H, const uint16_t* __restrict__ dres) {
   __shared__ float red[4][64 * 8 * NV];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int64_t wave = (int64_t)blockIdx.x * 4 + wid;
@@ -116,8 +128,19 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_narrow(const uint16_t* __rest
     const u32x4* xr = reinterpret_cast<const u32x4*>(x + r * H);
     const u32x4* gr = reinterpret_cast<const u32x4*>(dy + r * H);
     const float rs = rstd[r];
-    u32x4 xv[NV], gv[NV];
+    u32x4 xv[NV], gv[NV], dv[ADD ? NV : 1];
     float dot = 0.f;
+    // keep w packed across the row loop (no hoisted unpacked copy): registers go to occupancy
+#pragma unroll
+    for (int k = 0; k < NV; ++k) asm volatile("" : "+v"(wv[k]));
+    if constexpr (ADD) {  // issued with the row's other loads: in flight across the reduction
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const int c = k * 64 + lane;
+        dv[k] = c < nv8 ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(dres + r * H) + c)
+                        : u32x4{0, 0, 0, 0};
+      }
+    }
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
       const int c = k * 64 + lane;
@@ -136,6 +159,8 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_narrow(const uint16_t* __rest
     const float cfac = rs * rs * rs * invH * dot;
     u32x4* dr = reinterpret_cast<u32x4*>(dx + r * H);
 #pragma unroll
+    for (int k = 0; k < NV; ++k) asm volatile("" : "+v"(xv[k]), "+v"(gv[k]), "+v"(wv[k]));  // re-unpack below
+#pragma unroll
     for (int k = 0; k < NV; ++k) {
       const int c = k * 64 + lane;
       if (c < nv8) {
@@ -144,6 +169,10 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_narrow(const uint16_t* __rest
         for (int j = 0; j < 4; ++j) {
           const float g0 = r16(lo(gv[k][j]) * lo(wv[k][j])), g1 = r16(hi(gv[k][j]) * hi(wv[k][j]));
           o[j] = pack(rs * g0 - cfac * lo(xv[k][j]), rs * g1 - cfac * hi(xv[k][j]));
+        }
+        if constexpr (ADD) {  // + the residual branch's gradient, summed as autograd would (bf16 + bf16)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = pack(lo(o[j]) + lo(dv[k][j]), hi(o[j]) + hi(dv[k][j]));
         }
         __builtin_nontemporal_store(o, dr + c);
       }
@@ -163,11 +192,11 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_narrow(const uint16_t* __rest
 // wave order, so the block needs H floats of LDS instead of 4 H, and w / x / dy stay packed
 // between uses: 0.254 -> 0.217 ms at 16384 x 3584 (tools/ew_bench.py).  Narrow rows keep the
 // 4-row fold (rmsnorm_bwd_narrow), which measured faster at H = 1536 (0.179 vs 0.193 ms).
-template <int NV>
+template <int NV, bool ADD>
 __global__ __launch_bounds__(256) void rmsnorm_bwd_wide(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
                                                    const uint16_t* __restrict__ w, const float* __restrict__ rstd,
                                                    uint16_t* __restrict__ dx, float* __restrict__ partial,
-                                                   int64_t rows, int H) {
+                                                   int64_t rows, int H, const uint16_t* __restrict__ dres) {
   __shared__ float red[64 * 8 * NV];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int64_t wave = (int64_t)blockIdx.x * 4 + wid;
@@ -235,6 +264,11 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_wide(const uint16_t* __restri
         for (int j = 0; j < 4; ++j) {
           const float g0 = r16(lo(gv[k][j]) * lo(wv[k][j])), g1 = r16(hi(gv[k][j]) * hi(wv[k][j]));
           o[j] = pack(rs * g0 - cfac * lo(xv[k][j]), rs * g1 - cfac * hi(xv[k][j]));
+        }
+        if constexpr (ADD) {  // + the residual branch's gradient, summed as autograd would (bf16 + bf16)
+          const u32x4 dv = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(dres + r * H) + c);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = pack(lo(o[j]) + lo(dv[j]), hi(o[j]) + hi(dv[j]));
         }
         __builtin_nontemporal_store(o, dr + c);
       }
@@ -441,32 +475,44 @@ constexpr int kMaxNVBwd = 10;  // backward keeps 8 x NV fp32 dw accumulators per
 
 template <int NV>
 hipError_t launch_norm_fwd(const void* x, const void* w, void* y, float* rstd, int64_t rows, int H, float eps,
-                           int grid, hipStream_t s) {
-  hipLaunchKernelGGL(rmsnorm_fwd<NV>, dim3(grid), dim3(256), 0, s, (const uint16_t*)x, (const uint16_t*)w,
-                     (uint16_t*)y, rstd, rows, H, eps);
+                           int grid, hipStream_t s, const void* res, void* hout) {
+  if (res)
+    hipLaunchKernelGGL((rmsnorm_fwd<NV, true>), dim3(grid), dim3(256), 0, s, (const uint16_t*)x, (const uint16_t*)w,
+                       (uint16_t*)y, rstd, rows, H, eps, (const uint16_t*)res, (uint16_t*)hout);
+  else
+    hipLaunchKernelGGL((rmsnorm_fwd<NV, false>), dim3(grid), dim3(256), 0, s, (const uint16_t*)x, (const uint16_t*)w,
+                       (uint16_t*)y, rstd, rows, H, eps, (const uint16_t*)nullptr, (uint16_t*)nullptr);
+  return hipGetLastError();
+}
+template <int NV, bool ADD>
+hipError_t launch_norm_bwd_t(const void* dy, const void* x, const void* w, const float* rstd, void* dx, float* partial,
+                             int64_t rows, int H, int grid, hipStream_t s, const void* dres) {
+  hipLaunchKernelGGL((NV <= 4 ? rmsnorm_bwd_narrow<NV, ADD> : rmsnorm_bwd_wide<NV, ADD>), dim3(grid), dim3(256), 0, s,
+                     (const uint16_t*)dy, (const uint16_t*)x, (const uint16_t*)w, rstd, (uint16_t*)dx, partial, rows, H,
+                     (const uint16_t*)dres);
   return hipGetLastError();
 }
 template <int NV>
 hipError_t launch_norm_bwd(const void* dy, const void* x, const void* w, const float* rstd, void* dx, float* partial,
-                           int64_t rows, int H, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((NV <= 4 ? rmsnorm_bwd_narrow<NV> : rmsnorm_bwd_wide<NV>), dim3(grid), dim3(256), 0, s,
-                     (const uint16_t*)dy, (const uint16_t*)x,
-                     (const uint16_t*)w, rstd, (uint16_t*)dx, partial, rows, H);
-  return hipGetLastError();
+                           int64_t rows, int H, int grid, hipStream_t s, const void* dres) {
+  return dres ? launch_norm_bwd_t<NV, true>(dy, x, w, rstd, dx, partial, rows, H, grid, s, dres)
+              : launch_norm_bwd_t<NV, false>(dy, x, w, rstd, dx, partial, rows, H, grid, s, nullptr);
 }
 template <int... N>
 hipError_t norm_fwd_table(int nv, const void* x, const void* w, void* y, float* rstd, int64_t rows, int H, float eps,
-                          int grid, hipStream_t s, std::integer_sequence<int, N...>) {
+                          int grid, hipStream_t s, const void* res, void* hout, std::integer_sequence<int, N...>) {
   hipError_t e = hipErrorInvalidValue;
-  ((nv == N + 1 ? (e = launch_norm_fwd<N + 1>(x, w, y, rstd, rows, H, eps, grid, s), true) : false) || ...);
+  (void)((nv == N + 1 ? (e = launch_norm_fwd<N + 1>(x, w, y, rstd, rows, H, eps, grid, s, res, hout), true) : false) ||
+         ...);
   return e;
 }
 template <int... N>
 hipError_t norm_bwd_table(int nv, const void* dy, const void* x, const void* w, const float* rstd, void* dx,
-                          float* partial, int64_t rows, int H, int grid, hipStream_t s,
+                          float* partial, int64_t rows, int H, int grid, hipStream_t s, const void* dres,
                           std::integer_sequence<int, N...>) {
   hipError_t e = hipErrorInvalidValue;
-  ((nv == N + 1 ? (e = launch_norm_bwd<N + 1>(dy, x, w, rstd, dx, partial, rows, H, grid, s), true) : false) || ...);
+  (void)((nv == N + 1 ? (e = launch_norm_bwd<N + 1>(dy, x, w, rstd, dx, partial, rows, H, grid, s, dres), true) : false) ||
+         ...);
   return e;
 }
 
@@ -490,29 +536,32 @@ int prl_rmsnorm_workspace_bytes(int64_t H, size_t* bytes) {
   return PRL_OK;
 }
 
-int prl_rmsnorm_forward(const void* x, const void* w, void* y, float* rstd, int64_t rows, int64_t H, float eps,
-                        void* stream) {
+static int norm_forward(const void* x, const void* w, void* y, float* rstd, int64_t rows, int64_t H, float eps,
+                        void* stream, const void* res, void* hout) {
   if (!x || !w || !y || !rstd || rows < 0 || H <= 0) return PRL_E_INVALID;
   if (H % 8 || H > 64 * 8 * kMaxNV || !a16(x) || !a16(w) || !a16(y)) return PRL_E_UNSUPPORTED;
+  if (res && (!a16(res) || !a16(hout))) return PRL_E_UNSUPPORTED;
   if (rows == 0) return PRL_OK;
   const int nv = (int)((H / 8 + 63) / 64);
   const int64_t g = (rows + 3) / 4;
   const int grid = (int)(g < 2048 ? g : 2048);
-  return (int)norm_fwd_table(nv, x, w, y, rstd, rows, (int)H, eps, grid, static_cast<hipStream_t>(stream),
+  return (int)norm_fwd_table(nv, x, w, y, rstd, rows, (int)H, eps, grid, static_cast<hipStream_t>(stream), res, hout,
                              std::make_integer_sequence<int, kMaxNV>{});
 }
 
-int prl_rmsnorm_backward(const void* dy, const void* x, const void* w, const float* rstd, void* dx, void* dw,
-                         void* workspace, size_t workspace_bytes, int64_t rows, int64_t H, void* stream) {
+static int norm_backward(const void* dy, const void* x, const void* w, const float* rstd, void* dx, void* dw,
+                         void* workspace, size_t workspace_bytes, int64_t rows, int64_t H, void* stream,
+                         const void* dres) {
   if (!dy || !x || !w || !rstd || !dx || !dw || !workspace || rows < 0 || H <= 0) return PRL_E_INVALID;
   if (H % 8 || H > 64 * 8 * kMaxNVBwd || !a16(x) || !a16(w) || !a16(dy) || !a16(dx)) return PRL_E_UNSUPPORTED;
+  if (dres && !a16(dres)) return PRL_E_UNSUPPORTED;
   if (workspace_bytes < sizeof(float) * (size_t)(kNormBlocks + kDwSlices) * (size_t)H) return PRL_E_WORKSPACE;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int nv = (int)((H / 8 + 63) / 64);
   const int64_t g = (rows + 3) / 4;
   const int grid = (int)(g < kNormBlocks ? (g > 0 ? g : 1) : kNormBlocks);
   float* partial = static_cast<float*>(workspace);
-  hipError_t e = norm_bwd_table(nv, dy, x, w, rstd, dx, partial, rows, (int)H, grid, s,
+  hipError_t e = norm_bwd_table(nv, dy, x, w, rstd, dx, partial, rows, (int)H, grid, s, dres,
                                 std::make_integer_sequence<int, kMaxNVBwd>{});
   if (e != hipSuccess) return (int)e;
   float* mid = partial + (size_t)kNormBlocks * (size_t)H;
@@ -521,6 +570,28 @@ int prl_rmsnorm_backward(const void* dy, const void* x, const void* w, const flo
   hipLaunchKernelGGL(rmsnorm_dw_stage2, dim3((unsigned)((H + 255) / 256)), dim3(256), 0, s, mid, (int)H,
                      (uint16_t*)dw);
   return (int)hipGetLastError();
+}
+
+int prl_rmsnorm_forward(const void* x, const void* w, void* y, float* rstd, int64_t rows, int64_t H, float eps,
+                        void* stream) {
+  return norm_forward(x, w, y, rstd, rows, H, eps, stream, nullptr, nullptr);
+}
+
+int prl_add_rmsnorm_forward(const void* residual, const void* x, const void* w, void* h, void* y, float* rstd,
+                            int64_t rows, int64_t H, float eps, void* stream) {
+  if (!residual || !h) return PRL_E_INVALID;
+  return norm_forward(x, w, y, rstd, rows, H, eps, stream, residual, h);
+}
+
+int prl_rmsnorm_backward(const void* dy, const void* x, const void* w, const float* rstd, void* dx, void* dw,
+                         void* workspace, size_t workspace_bytes, int64_t rows, int64_t H, void* stream) {
+  return norm_backward(dy, x, w, rstd, dx, dw, workspace, workspace_bytes, rows, H, stream, nullptr);
+}
+
+int prl_add_rmsnorm_backward(const void* dy, const void* dh, const void* h, const void* w, const float* rstd, void* dx,
+                             void* dw, void* workspace, size_t workspace_bytes, int64_t rows, int64_t H, void* stream) {
+  if (!dh) return PRL_E_INVALID;
+  return norm_backward(dy, h, w, rstd, dx, dw, workspace, workspace_bytes, rows, H, stream, dh);
 }
 
 int prl_swiglu_forward(const void* gate, const void* up, void* out, int64_t n, void* stream) {

@@ -65,16 +65,66 @@ class RMSNormFn(torch.autograd.Function):
         dx = torch.empty_like(x2)
         dw = torch.empty_like(w)
         lib = _native.load()
-        key = (x2.device.index or 0, H)
-        ws = _WS.get(key)
-        if ws is None:
-            n = ctypes.c_size_t(0)
-            _native.check(lib.prl_rmsnorm_workspace_bytes(H, ctypes.byref(n)), "prl_rmsnorm_workspace_bytes")
-            ws = _WS[key] = torch.empty(n.value, dtype=torch.uint8, device=x2.device)
+        ws = _norm_ws(x2.device, H)
         _native.check(lib.prl_rmsnorm_backward(dy2.data_ptr(), x2.data_ptr(), w.data_ptr(), rstd.data_ptr(),
                                                dx.data_ptr(), dw.data_ptr(), ws.data_ptr(), ws.numel(), x2.shape[0],
                                                H, _stream(x2)), "prl_rmsnorm_backward")
         return dx.view(ctx.shape), dw, None
+
+
+def _norm_ws(dev: torch.device, H: int) -> torch.Tensor:
+    key = (dev.index or 0, H)
+    ws = _WS.get(key)
+    if ws is None:
+        n = ctypes.c_size_t(0)
+        _native.check(_native.load().prl_rmsnorm_workspace_bytes(H, ctypes.byref(n)), "prl_rmsnorm_workspace_bytes")
+        ws = _WS[key] = torch.empty(n.value, dtype=torch.uint8, device=dev)
+    return ws
+
+
+class AddRMSNormFn(torch.autograd.Function):
+    """h = residual + x and y = rmsnorm(h) in one pass (the decoder's residual add fused with the
+    norm that reads it); returns (h, y).  Backward: the gradient reaching h through the residual
+    stream is added inside the norm's backward kernel, so no separate add runs in either
+    direction.  Forward bit-identical to the eager `residual + x` then Qwen2RMSNorm."""
+
+    @staticmethod
+    def forward(ctx, residual, x, w, eps: float):
+        H = x.shape[-1]
+        x2, r2 = x.reshape(-1, H), residual.reshape(-1, H)
+        rows = x2.shape[0]
+        h, y = torch.empty_like(x2), torch.empty_like(x2)
+        rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
+        _native.check(_native.load().prl_add_rmsnorm_forward(r2.data_ptr(), x2.data_ptr(), w.data_ptr(), h.data_ptr(),
+                                                             y.data_ptr(), rstd.data_ptr(), rows, H, float(eps),
+                                                             _stream(x)), "prl_add_rmsnorm_forward")
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(h, w, rstd)
+        ctx.shape = x.shape
+        return h.view(x.shape), y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dh, dy):
+        h, w, rstd = ctx.saved_tensors
+        H = h.shape[1]
+        if dy is None:
+            return dh, dh, None, None
+        dy2 = dy.reshape(-1, H).contiguous()
+        dx = torch.empty_like(h)
+        dw = torch.empty_like(w)
+        ws = _norm_ws(h.device, H)
+        lib = _native.load()
+        if dh is None:
+            rc = lib.prl_rmsnorm_backward(dy2.data_ptr(), h.data_ptr(), w.data_ptr(), rstd.data_ptr(), dx.data_ptr(),
+                                          dw.data_ptr(), ws.data_ptr(), ws.numel(), h.shape[0], H, _stream(h))
+        else:
+            dh2 = dh.reshape(-1, H).contiguous()
+            rc = lib.prl_add_rmsnorm_backward(dy2.data_ptr(), dh2.data_ptr(), h.data_ptr(), w.data_ptr(),
+                                              rstd.data_ptr(), dx.data_ptr(), dw.data_ptr(), ws.data_ptr(), ws.numel(),
+                                              h.shape[0], H, _stream(h))
+        _native.check(rc, "prl_add_rmsnorm_backward")
+        dx = dx.view(ctx.shape)
+        return dx, dx, dw, None
 
 
 class SwiGLUFn(torch.autograd.Function):
@@ -141,11 +191,7 @@ class PrlLinearFn(torch.autograd.Function):
     def forward(ctx, x, w, b):
         ctx.save_for_backward(x, w)
         ctx.has_bias = b is not None
-        T = x.numel() // x.shape[-1]
-        sol = gemm.solution_for("fwd", T, w.shape[0], w.shape[1])
-        if sol is not None and (b is None or (b.dtype == torch.bfloat16 and b.is_contiguous())):
-            return gemm.linear_fwd(x, w, b, solution=sol)
-        return torch.nn.functional.linear(x, w, b)
+        return _fwd_gemm(x, w, b)
 
     @staticmethod
     def backward(ctx, dy):
@@ -159,12 +205,85 @@ class PrlLinearFn(torch.autograd.Function):
         return dx, dw, db
 
 
+class SharedInputLinearFn(torch.autograd.Function):
+    """Several linear layers on ONE input (q/k/v, gate/up): each forward as PrlLinearFn's; in the
+    backward the input gradients are summed in the dgrad GEMMs' epilogue (dX = dY0 W0, then
+    dX += dYi Wi with beta = 1) instead of by autograd's separate bf16 add kernels (one
+    [T, K] read-read-write per extra layer).  Arguments: x, w0, b0, w1, b1, ..."""
+
+    @staticmethod
+    def forward(ctx, x, *wb):
+        ws, bs = wb[0::2], wb[1::2]
+        ctx.set_materialize_grads(False)  # an unused output's gradient stays None: no GEMMs for it
+        ctx.save_for_backward(x, *ws)
+        ctx.has_bias = tuple(b is not None for b in bs)
+        return tuple(_fwd_gemm(x, w, b) for w, b in zip(ws, bs))
+
+    @staticmethod
+    def backward(ctx, *dys):
+        x, *ws = ctx.saved_tensors
+        grads = [None]
+        dx = None
+        for i, (dy, w) in enumerate(zip(dys, ws)):
+            if dy is None:
+                grads += [None, None]
+                continue
+            dy = dy if dy.is_contiguous() else dy.contiguous()
+            if ctx.needs_input_grad[0]:
+                dx = gemm.linear_dgrad(dy, w) if dx is None else gemm.linear_dgrad(dy, w, out=dx, accumulate=True)
+            dw = gemm.linear_wgrad(dy, x) if ctx.needs_input_grad[1 + 2 * i] else None
+            db = None
+            if ctx.has_bias[i] and ctx.needs_input_grad[2 + 2 * i]:
+                db = dy.reshape(-1, dy.shape[-1]).sum(0, dtype=torch.float32).to(dy.dtype)
+            grads += [dw, db]
+        grads[0] = dx
+        return tuple(grads)
+
+
+def _fwd_gemm(x, w, b):
+    T = x.numel() // x.shape[-1]
+    sol = gemm.solution_for("fwd", T, w.shape[0], w.shape[1])
+    if sol is not None and (b is None or (b.dtype == torch.bfloat16 and b.is_contiguous())):
+        return gemm.linear_fwd(x, w, b, solution=sol)
+    return torch.nn.functional.linear(x, w, b)
+
+
+class _Group:
+    """Linear layers that read the same input (an attention's q/k/v): the first call with an
+    input computes all of them in one SharedInputLinearFn and hands the others their outputs
+    when they are called with that same tensor."""
+
+    def __init__(self, mods):
+        self.mods = list(mods)
+        self.x = None
+        self.out: dict[int, torch.Tensor] = {}
+
+    def __call__(self, lin, x):
+        if self.x is x and id(lin) in self.out:
+            y = self.out.pop(id(lin))
+            if not self.out:
+                self.x = None
+            return y
+        if not all(_linear_ok(x, m.weight) for m in self.mods):
+            return None
+        wb = [t for m in self.mods for t in (m.weight, m.bias)]
+        ys = SharedInputLinearFn.apply(x, *wb)
+        self.x = x
+        self.out = {id(m): y for m, y in zip(self.mods, ys) if m is not lin}
+        return ys[self.mods.index(lin)]
+
+
 def _linear_ok(x, w) -> bool:
     return (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and w.is_contiguous()
             and x.dim() >= 2 and x.shape[-1] % 8 == 0 and w.shape[0] % 8 == 0)
 
 
 def _prl_linear_forward(self, x):
+    grp = self.__dict__.get("_prl_group")
+    if grp is not None:
+        y = grp(self, x)
+        if y is not None:
+            return y
     if _linear_ok(x, self.weight):
         return PrlLinearFn.apply(x, self.weight, self.bias)
     return torch.nn.functional.linear(x, self.weight, self.bias)
@@ -174,6 +293,11 @@ def _prl_linear_forward(self, x):
 # patching
 
 def _rmsnorm_forward(self, hidden_states):
+    pend = self.__dict__.get("_prl_pending")
+    if pend is not None:  # the previous decoder layer already normalised this tensor (fused add)
+        self.__dict__["_prl_pending"] = None
+        if pend[0] is hidden_states:
+            return pend[1]
     w = self.weight
     H = hidden_states.shape[-1]
     if _ok(hidden_states, w) and H % 8 == 0 and H <= 5120:
@@ -182,10 +306,54 @@ def _rmsnorm_forward(self, hidden_states):
 
 
 def _mlp_forward(self, x):
-    g, u = self.gate_proj(x), self.up_proj(x)
+    gp, up = self.gate_proj, self.up_proj
+    if getattr(gp, "_prl_linear", False) and getattr(up, "_prl_linear", False) and _linear_ok(x, gp.weight) \
+            and _linear_ok(x, up.weight):
+        g, u = SharedInputLinearFn.apply(x, gp.weight, gp.bias, up.weight, up.bias)
+    else:
+        g, u = gp(x), up(x)
     if _ok(g, u) and g.numel() % 8 == 0:
         return self.down_proj(SwiGLUFn.apply(g, u))
     return self.down_proj(self.act_fn(g) * u)
+
+
+def _add_norm_ok(norm, residual, x) -> bool:
+    w = getattr(norm, "weight", None)
+    H = x.shape[-1]
+    return (getattr(norm, "_prl_orig_forward", None) is not None and w is not None
+            and not hasattr(w, "_local_tensor") and _ok(residual, x, w) and residual.shape == x.shape
+            and H % 8 == 0 and H <= 5120)
+
+
+def _add_norm(norm, residual, x):
+    """(residual + x, norm(residual + x)) through AddRMSNormFn, or the eager pair."""
+    if _add_norm_ok(norm, residual, x):
+        return AddRMSNormFn.apply(residual, x, norm.weight, norm.variance_epsilon)
+    h = residual + x
+    return h, norm(h)
+
+
+def _decoder_forward(self, hidden_states, attention_mask=None, position_ids=None, past_key_values=None,
+                     use_cache=False, position_embeddings=None, **kwargs):
+    """transformers Qwen2DecoderLayer.forward with both residual adds fused into the norms that
+    read their results: `residual + attn` into post_attention_layernorm, and `residual + mlp`
+    into the NEXT layer's input_layernorm (or the final norm), whose output is handed over via
+    that norm module (`_prl_pending`, consumed by the next call with this very tensor).  The
+    cross-layer hand-over is skipped under gradient checkpointing and for sharded (FSDP) norm
+    weights, which the next layer only gathers in its own forward."""
+    n1 = self.input_layernorm(hidden_states)
+    a, _ = self.self_attn(hidden_states=n1, attention_mask=attention_mask, position_ids=position_ids,
+                          past_key_values=past_key_values, use_cache=use_cache,
+                          position_embeddings=position_embeddings, **kwargs)
+    h1, n2 = _add_norm(self.post_attention_layernorm, hidden_states, a)
+    m = self.mlp(n2)
+    nxt = self.__dict__.get("_prl_next_norm")
+    if nxt is not None and not (self.training and getattr(self, "gradient_checkpointing", False)) \
+            and _add_norm_ok(nxt, h1, m):
+        h2, n_next = AddRMSNormFn.apply(h1, m, nxt.weight, nxt.variance_epsilon)
+        nxt.__dict__["_prl_pending"] = (h2, n_next)
+        return h2
+    return h1 + m
 
 
 def _rope_ok(q, k, cos, sin) -> bool:
@@ -238,6 +406,35 @@ def patch_model(model) -> dict:
                 lin.forward = types.MethodType(_prl_linear_forward, lin)
                 lin._prl_linear = True
             n_linear += 1
+    # q/k/v of each attention share their input: one SharedInputLinearFn (dgrads summed in the
+    # GEMM epilogue).  PRL_QKV_GROUP=0 keeps them separate (A/B measurements)
+    n_group = 0
+    if n_linear and os.environ.get("PRL_QKV_GROUP", "1") != "0":
+        for m in model.modules():
+            lins = [getattr(m, a, None) for a in ("q_proj", "k_proj", "v_proj")]
+            if type(m).__name__.endswith("Attention") and all(getattr(l, "_prl_linear", False) for l in lins):
+                if "_prl_group" not in lins[0].__dict__:
+                    g = _Group(lins)
+                    for l in lins:
+                        l.__dict__["_prl_group"] = g
+                n_group += 1
+    # decoder layers (input_layernorm / self_attn / post_attention_layernorm / mlp, Qwen2 / Llama
+    # style): residual adds fused into the norms.  PRL_ADD_NORM=0 keeps the eager adds (A/B)
+    n_addnorm = 0
+    if os.environ.get("PRL_ADD_NORM", "1") != "0":
+        inner = getattr(model, "model", model)
+        layers = list(getattr(inner, "layers", []))
+        final = getattr(inner, "norm", None)
+        if layers and all(type(l).__name__.endswith("DecoderLayer") and all(
+                hasattr(l, a) for a in ("input_layernorm", "self_attn", "post_attention_layernorm", "mlp"))
+                and hasattr(l.post_attention_layernorm, "_prl_orig_forward") for l in layers):
+            for i, l in enumerate(layers):
+                nxt = layers[i + 1].input_layernorm if i + 1 < len(layers) else final
+                l.__dict__["_prl_next_norm"] = nxt if hasattr(nxt, "_prl_orig_forward") else None
+                if "_prl_orig_forward" not in l.__dict__:
+                    l.__dict__["_prl_orig_forward"] = l.forward
+                    l.forward = types.MethodType(_decoder_forward, l)
+                n_addnorm += 1
     n_rope = 0
     for modname in mods:
         mod = sys.modules.get(modname)
@@ -246,6 +443,7 @@ def patch_model(model) -> dict:
             mod.apply_rotary_pos_emb = _make_rope(f)
         if f is not None:
             n_rope += 1
-    counts = {"rmsnorm": n_norm, "swiglu_mlp": n_mlp, "rope_modules": n_rope, "prl_linear": n_linear}
+    counts = {"rmsnorm": n_norm, "swiglu_mlp": n_mlp, "rope_modules": n_rope, "prl_linear": n_linear,
+              "qkv_groups": n_group, "add_norm_layers": n_addnorm}
     logger.info(f"fused model ops patched: {counts}")
     return counts

@@ -129,15 +129,25 @@ def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = Non
     return y.view(*x.shape[:-1], N)
 
 
-def linear_dgrad(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    """dX = dY W, dY [..., N], W [N, K]."""
+def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None,
+                 accumulate: bool = False) -> torch.Tensor:
+    """dX = dY W, dY [..., N], W [N, K]; with ``out`` (bf16, [..., K] contiguous) and
+    accumulate=True the GEMM adds into it (beta = 1): the input gradient of layers sharing one
+    input (q/k/v, gate/up) summed in the epilogue instead of by separate add kernels."""
     d2 = _rows(dy)
     T, N = d2.shape
     K = w.shape[1]
-    dx = torch.empty((T, K), dtype=dy.dtype, device=dy.device)
-    sol = solution_for("dgrad", T, N, K)
-    gemm(N_, N_, K, T, N, w, K, d2, N, dx, K, solution=-1 if sol is None else sol)
-    return dx.view(*dy.shape[:-1], K)
+    if out is None:
+        if accumulate:
+            raise GemmError("linear_dgrad: accumulate needs out")
+        out = torch.empty((T, K), dtype=dy.dtype, device=dy.device)
+    if out.numel() != T * K or out.dtype != dy.dtype or not out.is_contiguous():
+        raise GemmError("linear_dgrad: out must be a contiguous bf16 tensor of T x K elements")
+    sol = solution_for("dgrad", T, N, K, BF16, accumulate)
+    if sol is None and accumulate:  # a swept beta = 0 solution; prl_gemm checks it supports beta = 1
+        sol = solution_for("dgrad", T, N, K)
+    gemm(N_, N_, K, T, N, w, K, d2, N, out, K, beta=1.0 if accumulate else 0.0, solution=-1 if sol is None else sol)
+    return out.view(*dy.shape[:-1], K)
 
 
 def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = None,

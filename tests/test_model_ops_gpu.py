@@ -129,6 +129,79 @@ def test_prl_linear(shape):
             assert float((got.reshape(ref.shape).float() - ref).abs().max()) <= tol, (i, shape)
 
 
+@pytest.mark.parametrize("H", [256, 1536, 3584])
+def test_add_rmsnorm(H):
+    """AddRMSNormFn: h and y bit-identical to eager `residual + x` then Qwen2RMSNorm; gradients
+    of residual, x and w vs eager autograd (which sums the residual-stream and norm gradients
+    in a separate bf16 add), with and without a gradient reaching h directly."""
+    from transformers.models.qwen2.modeling_qwen2 import Qwen2RMSNorm
+
+    from pipelinerl_amd.finetune.model_ops import AddRMSNormFn, RMSNormFn
+
+    T = 777
+    g = torch.Generator(device=DEV).manual_seed(11)
+    r = torch.randn((1, T, H), generator=g, device=DEV).to(torch.bfloat16)
+    x = torch.randn((1, T, H), generator=g, device=DEV).to(torch.bfloat16)
+    norm = Qwen2RMSNorm(H, eps=1e-6).to(DEV, torch.bfloat16)
+    with torch.no_grad():
+        norm.weight.copy_(1 + 0.1 * torch.randn(H, generator=g, device=DEV))
+    dh = torch.randn((1, T, H), generator=g, device=DEV).to(torch.bfloat16)
+    dy = torch.randn((1, T, H), generator=g, device=DEV).to(torch.bfloat16)
+    for with_dh in (True, False):
+        ra, xa, wa = (t.detach().clone().requires_grad_() for t in (r, x, norm.weight))
+        rb, xb, wb = (t.detach().clone().requires_grad_() for t in (r, x, norm.weight))
+        ha = ra + xa
+        ya = Qwen2RMSNorm.forward(type("N", (), {"weight": wa, "variance_epsilon": 1e-6})(), ha)  # eager, weight wa
+        hb, yb = AddRMSNormFn.apply(rb, xb, wb, 1e-6)
+        assert torch.equal(ha, hb)
+        # y: the same kernel as RMSNormFn on h (bit-identical to it); vs eager up to a last-bit
+        # rstd flip (test_rmsnorm)
+        assert torch.equal(yb, RMSNormFn.apply(hb.detach(), wb.detach(), 1e-6))
+        assert (ya.float() != yb.float()).float().mean().item() < 1e-3 and _close(yb, ya, 1.6e-2)[0]
+        outs_a, outs_b = ([ha, ya], [dh, dy]), ([hb, yb], [dh, dy])
+        if not with_dh:
+            outs_a, outs_b = ([ya], [dy]), ([yb], [dy])
+        torch.autograd.backward(*outs_a)
+        torch.autograd.backward(*outs_b)
+        for ga, gb in ((ra.grad, rb.grad), (xa.grad, xb.grad), (wa.grad, wb.grad)):
+            err = float((ga.float() - gb.float()).abs().max())
+            assert err <= 2e-2 * float(ga.float().abs().max()) + 1e-6, (H, with_dh, err)
+
+
+@pytest.mark.parametrize("bias", [True, False])
+def test_shared_input_linear(bias):
+    """SharedInputLinearFn (q/k/v-shaped: 3 layers on one input, dgrads summed in the GEMM
+    epilogue with beta = 1): outputs equal separate linears, gradients within bf16 rounding of
+    the fp32 products; a layer whose output is unused contributes nothing."""
+    from pipelinerl_amd.finetune.model_ops import SharedInputLinearFn
+
+    T, K, Ns = 1000, 512, (512, 128, 128)
+    g = torch.Generator(device=DEV).manual_seed(7)
+    x = torch.randn((1, T, K), generator=g, device=DEV).to(torch.bfloat16)
+    ws = [(torch.randn((n, K), generator=g, device=DEV) * 0.05).to(torch.bfloat16) for n in Ns]
+    bs = [torch.randn(n, generator=g, device=DEV).to(torch.bfloat16) if bias else None for n in Ns]
+    dys = [torch.randn((1, T, n), generator=g, device=DEV).to(torch.bfloat16) for n in Ns]
+    for used in ((0, 1, 2), (0, 2)):
+        xa = x.clone().requires_grad_()
+        wa = [w.clone().requires_grad_() for w in ws]
+        ba = [b.clone().requires_grad_() if b is not None else None for b in bs]
+        ys = SharedInputLinearFn.apply(xa, *[t for p in zip(wa, ba) for t in p])
+        for i, y in enumerate(ys):
+            assert torch.equal(y, torch.nn.functional.linear(x, ws[i], bs[i]))
+        torch.autograd.backward([ys[i] for i in used], [dys[i] for i in used])
+        dx = sum(dys[i][0].float() @ ws[i].float() for i in used)
+        assert float((xa.grad[0].float() - dx).abs().max()) <= 1e-2 * float(dx.abs().max())
+        for i in range(3):
+            if i not in used:
+                assert wa[i].grad is None
+                continue
+            ref = dys[i][0].float().t() @ x[0].float()
+            assert float((wa[i].grad.float() - ref).abs().max()) <= 1e-2 * float(ref.abs().max())
+            if bias:
+                ref = dys[i][0].float().sum(0)
+                assert float((ba[i].grad.float() - ref).abs().max()) <= 1e-2 * float(ref.abs().max())
+
+
 def test_patched_qwen2_matches_eager(tmp_path):
     from loop_helpers import tiny_model_dir
     from transformers import AutoConfig, AutoModelForCausalLM
@@ -154,6 +227,8 @@ def test_patched_qwen2_matches_eager(tmp_path):
                 assert counts["rmsnorm"] == 2 * cfg.num_hidden_layers + 1
                 assert counts["swiglu_mlp"] == cfg.num_hidden_layers and counts["rope_modules"] == 1
                 assert counts["prl_linear"] == 7 * cfg.num_hidden_layers + 1  # + lm_head
+                assert counts["qkv_groups"] == cfg.num_hidden_layers
+                assert counts["add_norm_layers"] == cfg.num_hidden_layers
             lg = m(input_ids=ids, position_ids=pos, **kw).logits
             lg.float().pow(2).mean().backward()
             outs.append(lg.detach())

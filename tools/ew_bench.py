@@ -65,7 +65,18 @@ def main():
         nb = rows * hid * 2
         out[f"rmsnorm_{rows}x{hid}"] = {"fwd_ms": round(ms_f, 4), "fwd_TBps": round(2 * nb / ms_f / 1e9, 3),
                                         "bwd_ms": round(ms_b, 4), "bwd_TBps": round(3 * nb / ms_b / 1e9, 3)}
-        del x, w, dy, y
+        # residual add fused into the norm (AddRMSNormFn): fwd reads res + x, writes h + y; bwd
+        # reads dy, h, dh, writes dx
+        from pipelinerl_amd.finetune.model_ops import AddRMSNormFn
+
+        res = torch.randn((rows, hid), device="cuda").to(torch.bfloat16).requires_grad_()
+        dh = torch.randn((rows, hid), device="cuda").to(torch.bfloat16)
+        hh, yy = AddRMSNormFn.apply(res, x, w, 1e-6)
+        ms_f = timed(lambda: AddRMSNormFn.apply(res.detach(), x.detach(), w.detach(), 1e-6))
+        ms_b = timed(lambda: torch.autograd.grad((hh, yy), (x, w), (dh, dy), retain_graph=True))
+        out[f"add_rmsnorm_{rows}x{hid}"] = {"fwd_ms": round(ms_f, 4), "fwd_TBps": round(4 * nb / ms_f / 1e9, 3),
+                                            "bwd_ms": round(ms_b, 4), "bwd_TBps": round(4 * nb / ms_b / 1e9, 3)}
+        del x, w, dy, y, res, dh, hh, yy
     print(json.dumps(out), flush=True)
 
 
