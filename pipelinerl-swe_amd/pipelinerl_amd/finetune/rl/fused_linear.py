@@ -12,8 +12,8 @@ final hidden states and the ``lm_head`` weight and, for the label rows only, in 
   dh_c      = dlogits_c @ W                  (GEMM, prl_gemm for bf16)
   dW       += dlogits_c^T @ h_c              (GEMM, fp32 accumulator, prl_gemm for bf16)
 
-then one ``prl_grpo_stats`` pass over all rows.  Peak extra memory is one [c, V] chunk plus an
-fp32 [V, H] accumulator instead of two [T, V] tensors, and the three lm_head GEMMs and the
+then one ``prl_grpo_stats`` pass over all rows.  Peak extra memory is one [c, V] chunk (plus an
+fp32 [V, H] accumulator when there are several) instead of two [T, V] tensors, and the three lm_head GEMMs and the
 loss kernel skip the prompt rows.  The backward scales the saved dh / dW by the upstream
 gradient on device.
 
@@ -78,7 +78,7 @@ class LinearGrpoLossFn(torch.autograd.Function):
         rows = torch.zeros((8, max(Q, 1)), dtype=torch.float32, device=dev)
         stats = torch.empty(NSTAT, dtype=torch.float64, device=dev)
         dh = torch.zeros((B * L, Hd), dtype=h2.dtype, device=dev) if write_grad else None
-        dw = torch.zeros((V, Hd), dtype=torch.float32, device=dev) if write_grad else None
+        dw = None
         stream = torch.cuda.current_stream(dev).cuda_stream
         cp = params.to_c(write_grad)
         if Q > 0:
@@ -88,6 +88,12 @@ class LinearGrpoLossFn(torch.autograd.Function):
             R = int(qsel.numel())
             step = max(1, int(chunk_rows))
             use_prl = w.dtype == torch.bfloat16 and w.is_contiguous() and Hd % 8 == 0 and V % 8 == 0
+            # one chunk: dW straight from one bf16-output GEMM over all label rows (the
+            # reference's own rounding; 1.3x faster than the fp32-accumulating form at 1.5B
+            # shapes).  Several chunks: an fp32 accumulator across them.
+            single = R <= step and use_prl
+            if write_grad and not single:
+                dw = torch.zeros((V, Hd), dtype=torch.float32, device=dev)
             for a in range(0, R, step):
                 idx = hrow[a:a + step]
                 qc = qsel[a:a + step].contiguous()
@@ -103,7 +109,10 @@ class LinearGrpoLossFn(torch.autograd.Function):
                               "prl_grpo_forward_rows")
                 if write_grad and use_prl:  # ROCm hipBLASLt (include/prl_gemm.h)
                     dh.index_copy_(0, idx, gemm.linear_dgrad(lg, w))
-                    gemm.linear_wgrad(lg, hc, out=dw, accumulate=True)
+                    if single:
+                        dw = gemm.linear_wgrad(lg, hc)
+                    else:
+                        gemm.linear_wgrad(lg, hc, out=dw, accumulate=True)
                 elif write_grad:
                     dh.index_copy_(0, idx, torch.mm(lg, w))
                     _accumulate_dw(dw, lg, hc)
@@ -115,6 +124,8 @@ class LinearGrpoLossFn(torch.autograd.Function):
                                          ws.numel(), stream), "prl_grpo_stats")
         loss = (-stats[0]).to(torch.float32)
         ctx.mark_non_differentiable(stats, rows)
+        if write_grad and dw is None:  # no label rows: zero weight gradient
+            dw = torch.zeros((V, Hd), dtype=torch.float32, device=dev)
         ctx.dh, ctx.dw = dh, dw
         ctx.shape = (B, L, Hd)
         ctx.h_dtype, ctx.w_dtype = hidden.dtype, weight.dtype
@@ -128,7 +139,7 @@ class LinearGrpoLossFn(torch.autograd.Function):
             if ctx.needs_input_grad[0]:
                 d_hidden = (ctx.dh.view(ctx.shape) * g.to(ctx.dh.dtype)).to(ctx.h_dtype)
             if ctx.needs_input_grad[1]:
-                d_weight = (ctx.dw * g).to(ctx.w_dtype)
+                d_weight = (ctx.dw.float() * g).to(ctx.w_dtype)  # g applied in fp32 (not rounded to bf16)
         ctx.dh = ctx.dw = None
         return d_hidden, d_weight, None, None, None
 

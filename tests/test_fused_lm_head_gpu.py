@@ -90,15 +90,17 @@ def test_fp32_matches_oracle(chunk):
     assert ok, err
 
 
-def test_bf16_resident_rows_and_upstream_scale():
-    """Qwen vocab (register-resident kernel with a row map), bf16 GEMMs, upstream 0.5."""
+@pytest.mark.parametrize("chunk", [3, 4096])
+def test_bf16_resident_rows_and_upstream_scale(chunk):
+    """Qwen vocab (register-resident kernel with a row map), bf16 GEMMs, upstream 0.5; several
+    chunks (fp32 dW accumulator) and one chunk (dW from one bf16-output GEMM)."""
     V, Hd = 151936, 64
     lens, prompts = [6, 5], [2, 3]
     b = _batch(lens, prompts, V, seed=2)
     g = torch.Generator().manual_seed(2)
     h = (torch.randn((1, sum(lens), Hd), generator=g)).to(torch.bfloat16).to(DEV)
     w = (torch.randn((V, Hd), generator=g) * 0.3).to(torch.bfloat16).to(DEV)
-    loss, stats, rows, dh, dw = _run_fused(h, w, b, CFG, chunk=3, scale=0.5)
+    loss, stats, rows, dh, dw = _run_fused(h, w, b, CFG, chunk=chunk, scale=0.5)
     # oracle on the bf16-rounded logits the GEMM produced
     logits = (h[0].float() @ w.float().t()).to(torch.bfloat16).float().cpu().numpy()[None]
     o = grpo_oracle.rl_step_oracle(logits, b, CFG, 0, 10)
