@@ -8,7 +8,7 @@
 // Problems are given in torch's row-major terms: pass fwd  Y[T,N]  = X[T,K] W[N,K]^T
 //                                               pass dgrad dX[T,K] = dY[T,N] W[N,K]
 //                                               pass wgrad dW[N,K] = dY[T,N]^T X[T,K]
-//   hipblaslt_probe <pass> <T> <N> <K> [<pass> <T> <N> <K> ...]
+//   hipblaslt_probe [--heuristic-only | --top K] <pass> <T> <N> <K> [<pass> <T> <N> <K> ...]
 // Build: hipcc -O2 --offload-arch=gfx950 tools/hipblaslt_probe.cpp -lhipblaslt -o tools/hipblaslt_probe.bin
 //
 // CAUTION: a full sweep runs every solution the library reports as supporting the problem, and
@@ -73,6 +73,14 @@ int main(int argc, char** argv) {
   if (heur_only) {
     --argc;
     ++argv;
+  }
+  // --top K: time only the heuristic's K ranked candidates (the library's own picks for the
+  // problem, not every solution of the catalog: the lower-risk sweep)
+  int top = 0;
+  if (argc > 2 && !strcmp(argv[1], "--top")) {
+    top = atoi(argv[2]);
+    argc -= 2;
+    argv += 2;
   }
   if (argc < 5 || (argc - 1) % 4) {
     fprintf(stderr, "usage: %s <fwd|dgrad|wgrad> T N K [...]\n", argv[0]);
@@ -157,7 +165,12 @@ int main(int argc, char** argv) {
     int heur_idx = nh ? hipblaslt_ext::getIndexFromAlgo(heur[0].algo) : -1;
 
     std::vector<hipblasLtMatmulHeuristicResult_t> all;
-    if (!heur_only)
+    if (top > 0) {
+      all.resize(top);
+      int nt = 0;
+      CK(hipblasLtMatmulAlgoGetHeuristic(h, desc, la, lb, lc, lc, pref, top, all.data(), &nt));
+      all.resize(nt);
+    } else if (!heur_only)
       CK(hipblaslt_ext::getAllAlgos(h, hipblaslt_ext::GemmType::HIPBLASLT_GEMM, p.opA, p.opB, HIP_R_16BF, HIP_R_16BF,
                                   dt, dt, HIPBLAS_COMPUTE_32F, all));
     std::vector<std::pair<float, int>> res;
