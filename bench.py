@@ -103,6 +103,20 @@ def cpu_baseline(rows: int, V: int, threads: int, min_seconds: float = 10.0, max
                       f"{dt:.2f} s"}
 
 
+def host_cpu() -> dict:
+    """The host the CPU baseline ran on (record nproc and the CPU model)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"cpu_model": model, "nproc": os.cpu_count()}
+
+
 def load_traffic(T: int, V: int) -> tuple[float | None, str | None]:
     """HBM bytes per launch from the committed rocprofv3 PMC summary, if one exists for this shape."""
     for p in sorted((ROOT / "profiles").glob("*pmc_traffic.json"), reverse=True):
@@ -284,6 +298,7 @@ def main():
             from oracle import cpu_trainer
 
             cpu["trainer_step"] = cpu_trainer.cpu_trainer_step(threads=threads)
+            cpu["host"] = host_cpu()
         out = {
             "metric": "trainer tokens/s (packed GRPO) at 1/2/4/8 MI355X; loss-kernel HBM GB/s",
             "value": round(tokens_total / elapsed, 1),
