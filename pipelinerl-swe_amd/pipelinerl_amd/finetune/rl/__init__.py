@@ -57,7 +57,7 @@ class RLConfig(BaseModel):
     # build-only keys (absent from the reference; ignored there):
     # lm_head + loss over the label rows only, in row chunks (fused_linear.py)
     fused_lm_head: bool = Field(default=False)
-    lm_head_chunk_rows: int = Field(default=16384)
+    lm_head_chunk_rows: int = Field(default=65536)
 
 
 def linear_decay_coef(current_step: int, max_step: int, initial_coef: float, final_coef: float) -> float:

@@ -145,7 +145,7 @@ class LinearGrpoLossFn(torch.autograd.Function):
 
 
 def linear_grpo_loss(hidden: torch.Tensor, weight: torch.Tensor, fields: dict, params: GrpoParams,
-                     chunk_rows: int = 16384):
+                     chunk_rows: int = 65536):
     """(loss, stats [NSTAT] f64 device, rows [8, B*(L-1)]) of lm_head(hidden) -> GRPO loss head,
     scoring only the label rows.  ``weight``: the lm_head weight [V, H] (no bias)."""
     return LinearGrpoLossFn.apply(hidden, weight, fields, params, chunk_rows)

@@ -37,7 +37,7 @@ def timed(fn, steps, warmup):
     return (time.perf_counter() - t0) / steps
 
 
-def rl_cfg(fused_head: bool = False, chunk: int = 16384):
+def rl_cfg(fused_head: bool = False, chunk: int = 65536):
     from pipelinerl_amd.finetune.rl import RLConfig
 
     return RLConfig(policy_loss="ppo", epsilon=4.0, kl_coef=0.0, final_kl_coef=0.0, clamp_log_ratio_ref_new_value=5,
@@ -131,6 +131,6 @@ if __name__ == "__main__":
     ap.add_argument("--loss", default="fused,aten")
     ap.add_argument("--grad-ckpt", action="store_true")
     ap.add_argument("--eager-ops", action="store_true", help="HF eager RMSNorm / SwiGLU / RoPE (no model_ops patch)")
-    ap.add_argument("--chunk", type=int, default=16384, help="lm_head_chunk_rows for --loss fused_head")
+    ap.add_argument("--chunk", type=int, default=65536, help="lm_head_chunk_rows for --loss fused_head")
     a = ap.parse_args()
     mode_loss(a) if a.mode == "loss" else mode_trainer(a)
