@@ -80,9 +80,10 @@ def _stream(t: torch.Tensor) -> int:
 
 def solutions() -> dict:
     global _solutions
-    if _solutions is None:  # PRL_GEMM_SOLUTIONS=off: library heuristic only (A/B measurements)
-        off = os.environ.get("PRL_GEMM_SOLUTIONS", "") == "off"
-        _solutions = json.loads(SOLUTIONS_PATH.read_text()) if SOLUTIONS_PATH.exists() and not off else {}
+    if _solutions is None:  # PRL_GEMM_SOLUTIONS=off: library heuristic only; =<file>: another table (A/B)
+        env = os.environ.get("PRL_GEMM_SOLUTIONS", "")
+        path = Path(env) if env not in ("", "off") else SOLUTIONS_PATH
+        _solutions = json.loads(path.read_text()) if env != "off" and path.exists() else {}
     return _solutions
 
 
