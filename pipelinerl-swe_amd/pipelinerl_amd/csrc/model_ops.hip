@@ -523,6 +523,13 @@ int ew_grid(int64_t n8) {
   return (int)(g < 4096 ? (g > 0 ? g : 1) : 4096);
 }
 constexpr int kNormBlocks = 2048;  // rmsnorm backward blocks (4 waves each): enough waves in flight
+// Backward grid cap (<= kNormBlocks, the workspace's partial rows): one resident round, 3 blocks of 4
+// waves per CU on 256 CUs at the kernels' 3 waves per SIMD, so no partial last round of blocks
+// (A/B vs 2048: 0.187 -> 0.178 ms at 65536 x 1536, 0.213 -> 0.196 at 16384 x 3584;
+// profiles/r01_norm_grid_ab.jsonl)
+#ifndef PRL_NORM_GRID
+#define PRL_NORM_GRID 768
+#endif
 
 }  // namespace prl_ops
 
@@ -559,7 +566,7 @@ static int norm_backward(const void* dy, const void* x, const void* w, const flo
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int nv = (int)((H / 8 + 63) / 64);
   const int64_t g = (rows + 3) / 4;
-  const int grid = (int)(g < kNormBlocks ? (g > 0 ? g : 1) : kNormBlocks);
+  const int grid = (int)(g < PRL_NORM_GRID ? (g > 0 ? g : 1) : PRL_NORM_GRID);
   float* partial = static_cast<float*>(workspace);
   hipError_t e = norm_bwd_table(nv, dy, x, w, rstd, dx, partial, rows, (int)H, grid, s, dres,
                                 std::make_integer_sequence<int, kMaxNVBwd>{});

@@ -20,6 +20,7 @@ VARIANTS = {
     "swiglu_u2": {"SWIGLU_UNROLL": "2"},
     "attn_fwd_1wave": {"PRL_ATTN_FWD_MINB": "1"},
     "attn_serial": {"PRL_ATTN_INTERLEAVE": "0"},
+    "norm_grid2048": {"PRL_NORM_GRID": "2048"},
 }
 
 if __name__ == "__main__":
