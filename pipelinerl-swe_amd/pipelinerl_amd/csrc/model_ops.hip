@@ -527,6 +527,12 @@ constexpr int kNormBlocks = 2048;  // rmsnorm backward blocks (4 waves each): en
 // waves per CU on 256 CUs at the kernels' 3 waves per SIMD, so no partial last round of blocks
 // (A/B vs 2048: 0.187 -> 0.178 ms at 65536 x 1536, 0.213 -> 0.196 at 16384 x 3584;
 // profiles/r01_norm_grid_ab.jsonl)
+// Forward grid cap: one resident round (6 blocks of 4 waves per CU on 256 CUs; the add form runs
+// 6 waves per SIMD): 0.078 -> 0.073 ms at 65536 x 1536, add form 0.152 -> 0.145 ms, vs 2048
+// (profiles/r01_norm_grid_ab.jsonl)
+#ifndef PRL_NORM_FWD_GRID
+#define PRL_NORM_FWD_GRID 1536
+#endif
 #ifndef PRL_NORM_GRID
 #define PRL_NORM_GRID 768
 #endif
@@ -551,7 +557,7 @@ static int norm_forward(const void* x, const void* w, void* y, float* rstd, int6
   if (rows == 0) return PRL_OK;
   const int nv = (int)((H / 8 + 63) / 64);
   const int64_t g = (rows + 3) / 4;
-  const int grid = (int)(g < 2048 ? g : 2048);
+  const int grid = (int)(g < PRL_NORM_FWD_GRID ? g : PRL_NORM_FWD_GRID);
   return (int)norm_fwd_table(nv, x, w, y, rstd, rows, (int)H, eps, grid, static_cast<hipStream_t>(stream), res, hout,
                              std::make_integer_sequence<int, kMaxNV>{});
 }

@@ -21,6 +21,7 @@ VARIANTS = {
     "attn_fwd_1wave": {"PRL_ATTN_FWD_MINB": "1"},
     "attn_serial": {"PRL_ATTN_INTERLEAVE": "0"},
     "norm_grid2048": {"PRL_NORM_GRID": "2048"},
+    "norm_fwd2048": {"PRL_NORM_FWD_GRID": "2048"},
 }
 
 if __name__ == "__main__":
