@@ -244,6 +244,51 @@ def test_patched_qwen2_matches_eager(tmp_path):
         assert err <= 5e-2 * float(p.grad.float().abs().max()) + 1e-6, (n, err)
 
 
+@pytest.mark.parametrize("reentrant", [False, True])
+def test_patched_qwen2_gradient_checkpointing(tmp_path, reentrant):
+    """The decoder fusions under HF gradient checkpointing (the layer forward runs twice; the
+    cross-layer norm hand-over is skipped): patched + checkpointed == eager + checkpointed."""
+    from loop_helpers import tiny_model_dir
+    from transformers import AutoConfig, AutoModelForCausalLM
+
+    from pipelinerl_amd.finetune.attention import packed_kwargs, register
+    from pipelinerl_amd.finetune.model_ops import patch_model
+
+    cfg = AutoConfig.from_pretrained(tiny_model_dir(tmp_path, vocab=512))
+    cfg.hidden_size, cfg.intermediate_size, cfg.num_attention_heads, cfg.num_key_value_heads = 256, 512, 4, 2
+    torch.manual_seed(0)
+    eager = AutoModelForCausalLM.from_config(cfg, dtype=torch.bfloat16, attn_implementation=register()).to(DEV)
+    fused = copy.deepcopy(eager)
+    T = 96
+    ids = torch.randint(0, 512, (1, T), device=DEV)
+    pos = torch.cat([torch.arange(40), torch.arange(56)])[None].to(DEV)
+    batch = type("B", (), {"seq_boundaries": torch.tensor([0, 40, 96]), "position_ids": pos})()
+    kw = packed_kwargs(batch, DEV)
+    outs = []
+    try:
+        for m in (eager, fused):
+            if m is fused:
+                patch_model(fused)
+            m.train()
+            m.gradient_checkpointing_enable(gradient_checkpointing_kwargs={"use_reentrant": reentrant})
+            if reentrant:  # the reentrant form needs an input that requires grad to build a graph
+                m.enable_input_require_grads()
+            lg = m(input_ids=ids, position_ids=pos, use_cache=False, **kw).logits
+            lg.float().pow(2).mean().backward()
+            outs.append(lg.detach())
+    finally:
+        from transformers.models.qwen2 import modeling_qwen2 as mq
+
+        f = mq.apply_rotary_pos_emb
+        if getattr(f, "_prl_fused", False):
+            mq.apply_rotary_pos_emb = f._prl_orig
+    assert (outs[0].float() - outs[1].float()).abs().max() <= 5e-2 * outs[0].float().abs().max()
+    for (n, p), (_, q) in zip(eager.named_parameters(), fused.named_parameters()):
+        err = float((p.grad.float() - q.grad.float()).abs().max())
+        assert err <= 5e-2 * float(p.grad.float().abs().max()) + 1e-6, (n, err)
+    assert all(m.__dict__.get("_prl_pending") is None for m in fused.modules())
+
+
 def test_varlen_gqa_native_matches_repeated():
     """torch's varlen flash attention takes GQA (Hkv < Hq) directly: forward and gradients equal
     the repeated-k/v form the attention path used before (finetune/attention.py)."""
