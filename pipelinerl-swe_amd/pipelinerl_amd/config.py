@@ -2,9 +2,11 @@
 only uses to read a frozen YAML: launch.py writes exp/conf/exp_config.yaml and starts
 ``run_finetune.py --config-dir exp/conf --config-name exp_config +me.k=v ...``).
 
-Supports what that file needs: nested mappings, ``${a.b.c}`` absolute and ``${..x}`` relative
-interpolation (OmegaConf semantics: each leading dot beyond the first goes one level up),
-and Hydra-style ``key=value`` / ``+key=value`` overrides.
+Supports what that file needs: nested mappings, ``${a.b.c}`` absolute and ``${.x}`` / ``${..x}``
+relative interpolation (OmegaConf semantics: ``${.x}`` is a sibling of the key, in the node that
+holds it; each further leading dot goes one level up, so ``finetune.rl.final_kl_coef:
+${..rl.kl_coef}`` reads ``finetune.rl.kl_coef``, conf/finetune/base.yaml:96), and Hydra-style
+``key=value`` / ``+key=value`` overrides.
 """
 
 from __future__ import annotations
@@ -69,8 +71,10 @@ def _resolve_value(root: dict, here: list[str], value: Any, depth: int = 0) -> A
     def target(expr: str) -> Any:
         expr = expr.strip()
         if expr.startswith("."):
-            ndots = len(expr) - len(expr.lstrip("."))
-            base = here[:len(here) - ndots] if ndots <= len(here) else []
+            up = len(expr) - len(expr.lstrip(".")) - 1  # one dot = the containing node itself
+            if up > len(here):
+                raise KeyError(f"interpolation ${{{expr}}} at {'.'.join(here) or '<root>'} goes above the root")
+            base = here[:len(here) - up]
             path = base + [p for p in expr.lstrip(".").split(".") if p]
         else:
             path = expr.split(".")

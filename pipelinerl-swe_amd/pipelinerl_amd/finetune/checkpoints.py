@@ -102,7 +102,9 @@ def temporary_folder_and_move(output_dir: Path, group=None):
         os.rename(tmp, output_dir)
 
 
-def save_model_and_tokenizer(output_dir: Path, model, tokenizer, safe_serialization: bool = True, group=None):
+def save_model_and_tokenizer(output_dir: Path, model, tokenizer, *, safe_serialization: bool = False, group=None):
+    """checkpoints.py:280-300; ``safe_serialization`` is the config's ``use_safetensors``
+    (finetune_loop.py:805-811), ``group`` the CPU control group of the barriers (keyword-only)."""
     from .sharding import full_state_dict, is_sharded
 
     sd = full_state_dict(model) if is_sharded(model) else None  # collective: every rank
@@ -119,7 +121,7 @@ def save_model_and_tokenizer(output_dir: Path, model, tokenizer, safe_serializat
                 tokenizer.save_pretrained(tmp)
 
 
-def save_training_state(training_state_dir: Path, model, optimizer, lr_scheduler, extra: dict[str, Any],
+def save_training_state(training_state_dir: Path, model, optimizer, lr_scheduler, extra: dict[str, Any], *,
                         group=None):
     """training_state.pt (metrics, lr scheduler, optimizer); with FSDP the sharded optimizer
     state goes to ``optim/`` (torch.distributed.checkpoint, every rank writes its shard)."""

@@ -288,6 +288,7 @@ def rl_finetuning_worker(args, ctx: Dist, model, optimizer, lr_scheduler, grads:
     mb_sizes: list[int] = []
     waiting = 0.0
     sync_every = bool(args.get("fsdp_sync_every_micro_batch", False))
+    safe = bool(args.get("use_safetensors", False))  # checkpoints.py:285 default
 
     def next_batch():
         timeout = 0.1
@@ -398,18 +399,19 @@ def rl_finetuning_worker(args, ctx: Dist, model, optimizer, lr_scheduler, grads:
             wum.send_weight_update(metrics.samples)  # overlapped with the next step
             metrics.last_broadcasted_version = metrics.samples
         if time_to_save:
-            save_model_and_tokenizer(current_dir, model, tokenizer, ctx.ctrl)
-            save_training_state(state_dir, model, optimizer, lr_scheduler, asdict(metrics), ctx.ctrl)
+            save_model_and_tokenizer(current_dir, model, tokenizer, safe_serialization=safe, group=ctx.ctrl)
+            save_training_state(state_dir, model, optimizer, lr_scheduler, asdict(metrics), group=ctx.ctrl)
             if args.get("keep_intermediate_checkpoints", False):
-                save_model_and_tokenizer(inter_dir / str(metrics.completed_steps), model, tokenizer, ctx.ctrl)
+                save_model_and_tokenizer(inter_dir / str(metrics.completed_steps), model, tokenizer,
+                                         safe_serialization=safe, group=ctx.ctrl)
         if time_to_stop:
             break
 
     if wum is not None:
         wum.wait()
-    save_model_and_tokenizer(current_dir, model, tokenizer, ctx.ctrl)
+    save_model_and_tokenizer(current_dir, model, tokenizer, safe_serialization=safe, group=ctx.ctrl)
     if args.get("save_final_training_state", True):
-        save_training_state(state_dir, model, optimizer, lr_scheduler, asdict(metrics), ctx.ctrl)
+        save_training_state(state_dir, model, optimizer, lr_scheduler, asdict(metrics), group=ctx.ctrl)
     if ctx.is_main:
         (output_dir / "summary.json").write_text(json.dumps(asdict(metrics), indent=4, sort_keys=True))
         (output_dir / "rl_summary.json").write_text(json.dumps(dict(rl_metrics), indent=4, sort_keys=True))
