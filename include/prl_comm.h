@@ -53,6 +53,10 @@ int prl_comm_allreduce(void* comm, void* buf, size_t count, int dtype, int op, v
 int prl_comm_rank(void* comm, int* rank);
 int prl_comm_size(void* comm, int* world);
 int prl_comm_destroy(void* comm);
+/* Abort: frees the communicator without waiting for in-flight collectives, which return (no
+ * hang) — the trainer's way out when an actor died mid-broadcast (the reference
+ * blocks in NCCL until the process-group timeout, finetune_loop.py:155-172). */
+int prl_comm_abort(void* comm);
 
 #ifdef __cplusplus
 }

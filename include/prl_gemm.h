@@ -28,6 +28,7 @@ extern "C" {
 
 #define PRL_GEMM_E_INVALID 4001
 #define PRL_GEMM_E_LOAD 4002
+#define PRL_GEMM_E_REFUSED 4003
 #define PRL_GEMM_E_HIP 4100
 #define PRL_GEMM_E_BASE 4400
 
@@ -40,7 +41,9 @@ const char* prl_gemm_error_string(int code);
 /* D = op(A) op(B) (+ bias broadcast over D's columns) + beta * D.  `bias`: nullable, bf16, m
  * elements, bf16 D only (a linear layer's bias: m = output features).  `solution` >= 0 selects a
  * hipBLASLt solution index (falls back to the heuristic if it does not support the problem),
- * -1 = heuristic. */
+ * -1 = heuristic.  A solution index outside the set registered with prl_gemm_allow_solutions is
+ * refused (PRL_GEMM_E_REFUSED) before any device work: hipBLASLt's catalog holds solutions that
+ * fault the GPU on some shapes, and only the swept ones are trusted. */
 int prl_gemm_bf16(int op_a, int op_b, int64_t m, int64_t n, int64_t k, const void* A, int64_t lda,
                   const void* B, int64_t ldb, const void* bias, float beta, void* D, int64_t ldd, int d_dtype,
                   int solution, void* stream);
@@ -48,6 +51,10 @@ int prl_gemm_bf16(int op_a, int op_b, int64_t m, int64_t n, int64_t k, const voi
 /* Solution index prl_gemm_bf16 would use for this problem with solution = -1 (-1 if none). */
 int prl_gemm_heuristic_index(int op_a, int op_b, int64_t m, int64_t n, int64_t k, int64_t lda,
                              int64_t ldb, int64_t ldd, int d_dtype, float beta);
+
+/* Replace the set of solution indices prl_gemm_bf16 may run (n = 0: none, heuristic only).
+ * The binding registers the indices of its shipped solution table (gemm_solutions.json). */
+int prl_gemm_allow_solutions(const int32_t* indices, int n);
 
 /* Path and version of the hipBLASLt in use, NUL-terminated into buf (the load error if it could
  * not be opened).  Returns 0 or the load error code. */

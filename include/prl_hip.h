@@ -124,7 +124,7 @@ typedef struct PrlGrpoParams {
   float temperature;
   float batch_size;            /* token weight = 1 / batch_size unless group-normalised */
   float value_loss_coef;
-  float grad_scale;            /* upstream d(final_loss) assumed for dlogits / dvalues */
+  float grad_scale;            /* upstream d(final_loss) assumed for dlogits / dvalues (> 0, finite) */
 } PrlGrpoParams;
 
 /* Outputs.  Per-token arrays have B*(L-1) entries (row q = b*(L-1) + t). */
@@ -178,9 +178,10 @@ int prl_grpo_stats(const PrlGrpoBatch* batch, const PrlGrpoParams* params,
 /* Gradient pass from the per-row max / log2sum / entropy / g_lp / g_h saved by prl_grpo_forward (at
  * params->grad_scale), for an upstream gradient read ON DEVICE from *upstream (NULL = 1.0):
  *   dlogits = (*upstream) * d final / d logits.
- * If params->write_grad is set, dlogits already holds the gradient for upstream == 1 and
- * the kernel returns without touching memory when *upstream == 1 (no host sync needed to
- * decide).  Rows with zero coefficients are written as zeros without reading the logits. */
+ * If params->write_grad is set, dlogits already holds the gradient for upstream ==
+ * params->grad_scale (the caller's loss scale, e.g. DeepSpeed's 1/GAS) and the kernel returns
+ * without touching memory when *upstream equals it (no host sync needed to decide).  Rows with
+ * zero coefficients are written as zeros without reading the logits. */
 int prl_grpo_backward(const PrlGrpoBatch* batch, const PrlGrpoParams* params,
                       const float* row_max, const float* row_log2sum, const float* entropy,
                       const float* g_lp, const float* g_h, const float* upstream, void* dlogits,

@@ -64,6 +64,7 @@ def load():
         "prl_comm_rank": (c.c_int, [c.c_void_p, c.POINTER(c.c_int)]),
         "prl_comm_size": (c.c_int, [c.c_void_p, c.POINTER(c.c_int)]),
         "prl_comm_destroy": (c.c_int, [c.c_void_p]),
+        "prl_comm_abort": (c.c_int, [c.c_void_p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -133,6 +134,12 @@ class RcclComm:
         if self._h:
             _check(load().prl_comm_destroy(self._h), "prl_comm_destroy")
             self._h = None
+
+    def abort(self) -> None:
+        """Tear the communicator down without waiting for in-flight collectives (a peer died)."""
+        if self._h:
+            h, self._h = self._h, None
+            _check(load().prl_comm_abort(h), "prl_comm_abort")
 
 
 def broadcast(t: torch.Tensor, group, src: int = 0, async_op: bool = False):

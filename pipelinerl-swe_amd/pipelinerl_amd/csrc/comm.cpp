@@ -131,4 +131,12 @@ int prl_comm_destroy(void* comm) {
   return r;
 }
 
+int prl_comm_abort(void* comm) {
+  Comm* c = static_cast<Comm*>(comm);
+  if (!c) return PRL_COMM_E_INVALID;
+  const int r = rc(ncclCommAbort(c->comm));
+  delete c;
+  return r;
+}
+
 }  // extern "C"

@@ -85,6 +85,15 @@ std::mutex g_mu;
 std::map<int, hipblasLtHandle_t> g_handles;
 std::map<std::pair<int, hipStream_t>, void*> g_workspaces;
 std::map<std::pair<int, Key>, Plan> g_plans;
+// solution indices a caller may request (prl_gemm_allow_solutions): the set that ran clean in the
+// MI355X sweeps shipped with the library; anything else is refused before it reaches the GPU
+std::vector<int> g_allowed;
+std::mutex g_allow_mu;
+
+bool solution_allowed(int solution) {
+  std::lock_guard<std::mutex> lock(g_allow_mu);
+  return std::binary_search(g_allowed.begin(), g_allowed.end(), solution);
+}
 
 template <class F>
 bool sym(void* h, const char* name, F* out) {
@@ -271,11 +280,12 @@ Key make_key(int op_a, int op_b, int64_t m, int64_t n, int64_t k, int64_t lda, i
 
 extern "C" {
 
-int prl_gemm_abi_version(void) { return 2; }
+int prl_gemm_abi_version(void) { return 3; }
 
 const char* prl_gemm_error_string(int code) {
   if (code == 0) return "ok";
   if (code == PRL_GEMM_E_INVALID) return "invalid argument";
+  if (code == PRL_GEMM_E_REFUSED) return "solution index not in the allowed (swept) set";
   if (code == PRL_GEMM_E_LOAD) return g_api.error.empty() ? "hipBLASLt not loaded" : g_api.error.c_str();
   if (code >= PRL_GEMM_E_BASE) {
     switch (code - PRL_GEMM_E_BASE) {
@@ -297,6 +307,7 @@ int prl_gemm_bf16(int op_a, int op_b, int64_t m, int64_t n, int64_t k, const voi
   if (!valid(op_a, op_b, m, n, k, lda, ldb, ldd, d_dtype) || !A || !B || !D) return PRL_GEMM_E_INVALID;
   if (beta != 0.f && beta != 1.f) return PRL_GEMM_E_INVALID;
   if (bias && d_dtype != PRL_GEMM_BF16) return PRL_GEMM_E_INVALID;
+  if (solution >= 0 && !solution_allowed(solution)) return PRL_GEMM_E_REFUSED;
   int dev;
   RET(hp(hipGetDevice(&dev)));
   hipStream_t st = (hipStream_t)stream;
@@ -325,6 +336,18 @@ int prl_gemm_heuristic_index(int op_a, int op_b, int64_t m, int64_t n, int64_t k
   if (load_api() || handle_for(dev, &h) || plan_for(dev, h, make_key(op_a, op_b, m, n, k, lda, ldb, ldd, d_dtype, beta, -1), &p))
     return -1;
   return p->index;
+}
+
+int prl_gemm_allow_solutions(const int32_t* indices, int n) {
+  if (n < 0 || (n > 0 && !indices)) return PRL_GEMM_E_INVALID;
+  std::vector<int> v(indices, indices + n);
+  for (int i : v)
+    if (i < 0) return PRL_GEMM_E_INVALID;
+  std::sort(v.begin(), v.end());
+  v.erase(std::unique(v.begin(), v.end()), v.end());
+  std::lock_guard<std::mutex> lock(g_allow_mu);
+  g_allowed.swap(v);
+  return 0;
 }
 
 int prl_gemm_library(char* buf, int len) {

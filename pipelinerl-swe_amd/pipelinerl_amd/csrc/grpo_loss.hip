@@ -393,15 +393,18 @@ __global__ __launch_bounds__(BLOCK) void grpo_fwd_stream(KArgs a) {
 }
 
 // gradient pass from saved per-row coefficients for the upstream gradient *up (device);
-// skip_if_one: dlogits already holds the gradient for *up == 1 (fused forward)
+// skip_if_one: dlogits already holds the gradient for *up == grad_scale (fused forward)
 template <typename T, int VEC>
 __global__ __launch_bounds__(256) void grpo_bwd_stream(KArgs a, const float* max_in, const float* l2s_in,
                                                        const float* ent_in, const float* glp_in,
                                                        const float* gh_in, const float* up,
                                                        int skip_if_one) {
   constexpr int BLOCK = 256;
-  const float scale = up ? *up : 1.0f;
-  if (skip_if_one && scale == 1.0f) return;
+  // g_lp / g_h were saved at a.gscale (the loss scale the forward assumed): the upstream
+  // gradient is applied relative to it, and an upstream equal to it needs no pass at all
+  const float up_abs = up ? *up : 1.0f;
+  if (skip_if_one && up_abs == a.gscale) return;
+  const float scale = up_abs / a.gscale;
   const int tid = threadIdx.x;
   const int64_t nrows = a.B * (a.L - 1);
   const int64_t nvec = a.V / VEC;
@@ -588,6 +591,7 @@ static int fill_args(KArgs& a, const PrlGrpoBatch* b, const PrlGrpoParams* p, bo
     return PRL_E_INVALID;
   if (b->logits_dtype != PRL_BF16 && b->logits_dtype != PRL_F32) return PRL_E_UNSUPPORTED;
   if (p->policy_loss != PRL_PPO && p->policy_loss != PRL_REINFORCE) return PRL_E_INVALID;
+  if (!(p->grad_scale > 0.f && p->grad_scale < 3.0e38f)) return PRL_E_INVALID;  // finite, positive
   a = KArgs{};
   a.logits = b->logits;
   a.B = b->B;

@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import ctypes
 import logging
+import inspect
 import os
 import sys
 import types
@@ -333,18 +334,41 @@ def _add_norm(norm, residual, x):
     return h, norm(h)
 
 
-def _decoder_forward(self, hidden_states, attention_mask=None, position_ids=None, past_key_values=None,
-                     use_cache=False, position_embeddings=None, **kwargs):
+def _layer_call_args(layer, hidden_states, args, kwargs) -> tuple[dict, bool]:
+    """Map a decoder-layer call onto keyword arguments for its self_attn, under either
+    transformers layer contract: 5.x ``forward(hidden_states, attention_mask, position_ids,
+    past_key_values, use_cache, position_embeddings, **kw) -> Tensor`` or 4.x (the reference pins
+    4.51.1, pyproject.toml:20) ``forward(hidden_states, attention_mask, position_ids,
+    past_key_value, output_attentions, use_cache, cache_position, position_embeddings, **kw) ->
+    tuple`` (Qwen2Model takes ``layer_outputs[0]``; gradient checkpointing passes them
+    positionally).  Returns (self_attn kwargs, whether the layer returns a tuple)."""
+    sig = layer.__dict__.get("_prl_sig")
+    if sig is None:
+        sig = inspect.signature(layer.__dict__["_prl_orig_forward"])
+        layer.__dict__["_prl_sig"] = sig
+    bound = sig.bind(hidden_states, *args, **kwargs).arguments
+    attn_kw: dict = {}
+    for name, v in bound.items():
+        if name == "hidden_states":
+            continue
+        if sig.parameters[name].kind is inspect.Parameter.VAR_KEYWORD:
+            attn_kw.update(v)
+        else:
+            attn_kw[name] = v
+    return attn_kw, "output_attentions" in sig.parameters
+
+
+def _decoder_forward(self, hidden_states, *args, **kwargs):
     """transformers Qwen2DecoderLayer.forward with both residual adds fused into the norms that
     read their results: `residual + attn` into post_attention_layernorm, and `residual + mlp`
     into the NEXT layer's input_layernorm (or the final norm), whose output is handed over via
     that norm module (`_prl_pending`, consumed by the next call with this very tensor).  The
     cross-layer hand-over is skipped under gradient checkpointing and for sharded (FSDP) norm
-    weights, which the next layer only gathers in its own forward."""
+    weights, which the next layer only gathers in its own forward.  Returns what the installed
+    transformers' layer returns (a tensor on 5.x, a tuple on 4.x)."""
+    attn_kw, tuple_out = _layer_call_args(self, hidden_states, args, kwargs)
     n1 = self.input_layernorm(hidden_states)
-    a, _ = self.self_attn(hidden_states=n1, attention_mask=attention_mask, position_ids=position_ids,
-                          past_key_values=past_key_values, use_cache=use_cache,
-                          position_embeddings=position_embeddings, **kwargs)
+    a, attn_w = self.self_attn(hidden_states=n1, **attn_kw)
     h1, n2 = _add_norm(self.post_attention_layernorm, hidden_states, a)
     m = self.mlp(n2)
     nxt = self.__dict__.get("_prl_next_norm")
@@ -352,8 +376,11 @@ def _decoder_forward(self, hidden_states, attention_mask=None, position_ids=None
             and _add_norm_ok(nxt, h1, m):
         h2, n_next = AddRMSNormFn.apply(h1, m, nxt.weight, nxt.variance_epsilon)
         nxt.__dict__["_prl_pending"] = (h2, n_next)
+    else:
+        h2 = h1 + m
+    if not tuple_out:
         return h2
-    return h1 + m
+    return (h2, attn_w) if attn_kw.get("output_attentions") else (h2,)
 
 
 def _rope_ok(q, k, cos, sin) -> bool:

@@ -9,8 +9,12 @@ Drop-in surface (same names, arguments, return values and errors as the referenc
 
 rl_step runs the model forward WITHOUT ``labels`` (the reference passes them, which makes HF
 compute and discard a full fp32 cross-entropy over [T, V]; rl/__init__.py:183-197), then the
-fused HIP loss head (fused.py).  It syncs with the device once, to read the ~40 statistics
-(the reference issues ~30 ``.item()`` calls).
+fused HIP loss head (fused.py), by default over the label rows only with the lm_head fused in
+(fused_linear.py).  It reads the ~40 statistics back with ONE device->host copy (the reference
+issues ~30 ``.item()`` calls); with ``defer_stats=True`` (the trainer loop) that copy is only
+started, and the stats (and the reference's assertions) are materialised by
+``RLStats.resolve()`` after the caller has launched the backward, so the GPU queue never drains
+between a micro-batch's forward and backward.
 """
 
 from __future__ import annotations
@@ -55,8 +59,9 @@ class RLConfig(BaseModel):
     filter_zero_advantage_groups: bool = Field(default=False)
     value_loss_coef: float = Field(default=0.0)
     # build-only keys (absent from the reference; ignored there):
-    # lm_head + loss over the label rows only, in row chunks (fused_linear.py)
-    fused_lm_head: bool = Field(default=False)
+    # lm_head + loss over the label rows only, in row chunks (fused_linear.py); the prompt rows'
+    # logits are never formed, their hidden states are checked for finiteness instead
+    fused_lm_head: bool = Field(default=True)
     lm_head_chunk_rows: int = Field(default=65536)
 
 
@@ -72,9 +77,56 @@ def _num_sequences_device(batch: PipelineBatchEncoding) -> torch.Tensor | int:
     return int(batch.labels.shape[0])
 
 
+class RLStats:
+    """The statistics of one rl_step, still on their way to the host (``defer_stats=True``).
+    ``resolve()`` waits for the one D2H copy (not for the backward queued behind it), runs the
+    reference's assertions (rl/__init__.py:209, :237, :264, :313) and returns the dict."""
+
+    def __init__(self, dev: torch.Tensor, batch, params, kl_c: float, ent_c: float, nseq, has_value_head: bool,
+                 bad_hidden: torch.Tensor | None):
+        parts = [dev]
+        if isinstance(nseq, torch.Tensor):
+            parts.append(nseq.to(dev.device, torch.float64).reshape(1))
+        if bad_hidden is not None:
+            parts.append(bad_hidden.to(dev.device, torch.float64).reshape(1))
+        packed = torch.cat(parts) if len(parts) > 1 else dev
+        self._host = torch.empty(packed.shape, dtype=torch.float64, pin_memory=packed.is_cuda)
+        self._host.copy_(packed, non_blocking=True)
+        self._event = None
+        if packed.is_cuda:
+            self._event = torch.cuda.Event()
+            self._event.record(torch.cuda.current_stream(packed.device))
+        self._args = (batch, params, kl_c, ent_c, nseq, has_value_head, bad_hidden is not None)
+        self._value: dict[str, float] | None = None
+
+    def resolve(self) -> dict[str, float]:
+        if self._value is None:
+            if self._event is not None:
+                self._event.synchronize()
+            h = self._host.numpy()
+            batch, params, kl_c, ent_c, nseq, has_value_head, hidden_checked = self._args
+            n = len(h) - int(hidden_checked)
+            if hidden_checked and h[-1] > 0:  # a prompt row's logits cannot be finite (see below)
+                raise AssertionError("new_logprobs is not finite: non-finite hidden states on prompt rows")
+            if isinstance(nseq, torch.Tensor):
+                num_sequences, n = int(h[n - 1]), n - 1
+            else:
+                num_sequences = nseq
+            self._value = build_stats(h[:n], batch, params, kl_c, ent_c, num_sequences, has_value_head)
+            self._args = None
+        return self._value
+
+
 def rl_step(model, batch: PipelineBatchEncoding, current_step: int, max_step: int,
-            config: RLConfig) -> tuple[torch.Tensor, dict[str, float]]:
-    """One RL micro-batch: model forward + fused loss head.  Returns (loss, stats)."""
+            config: RLConfig, *, grad_scale: float = 1.0,
+            defer_stats: bool = False) -> tuple[torch.Tensor, dict[str, float] | RLStats]:
+    """One RL micro-batch: model forward + fused loss head.  Returns (loss, stats).
+
+    ``grad_scale``: the factor the caller will multiply the loss by before ``backward()``
+    (DeepSpeed's 1/gradient_accumulation_steps, finetune_loop.py:307-312): the fused kernels
+    then write their gradients at that scale in the forward pass, so the backward needs no
+    second pass over the logits.  Any other upstream gradient is still handled exactly.
+    ``defer_stats``: return an RLStats whose ``resolve()`` gives the dict (see module doc)."""
     if config.policy_loss not in ("ppo", "reinforce"):
         raise ValueError(f"Unknown algorithm {config.policy_loss}")
     has_value_head = hasattr(model, "value_head")
@@ -99,10 +151,16 @@ def rl_step(model, batch: PipelineBatchEncoding, current_step: int, max_step: in
     if getattr(getattr(model, "config", None), "use_cache", None) is not None:
         model_inputs["use_cache"] = False  # training: no KV cache (HF would concatenate k / v per layer)
     fused_head = config.fused_lm_head and _lm_head_of(model, has_value_head) is not None
+    bad_hidden = None
     if fused_head:
         hidden = _decoder_of(model)(**model_inputs).last_hidden_state
         logits = hidden
         values = None
+        # The reference asserts every row's new log-probs finite (rl/__init__.py:209), prompt rows
+        # included.  Label rows are checked by the kernel; a prompt row's logits h·Wᵀ are finite
+        # when its hidden state is (W is finite, or every label row's log-softmax reports it),
+        # barring bf16 overflow of a finite dot product.
+        bad_hidden = torch.logical_not(torch.isfinite(hidden[:, :-1]).all())
     else:
         outputs = model(**model_inputs)
         logits = outputs.logits
@@ -115,7 +173,8 @@ def rl_step(model, batch: PipelineBatchEncoding, current_step: int, max_step: in
         relu_log_p_weights=config.relu_log_p_weights, group_normalization=config.group_normalization,
         overlong_filtering=config.overlong_filtering, epsilon=config.epsilon, kl_coef=kl_c, entropy_coef=ent_c,
         clamp_log_ratio=float(config.clamp_log_ratio_ref_new_value), temperature=config.temperature,
-        batch_size=float(config.batch_size), value_loss_coef=config.value_loss_coef if has_value_head else 0.0)
+        batch_size=float(config.batch_size), value_loss_coef=config.value_loss_coef if has_value_head else 0.0,
+        grad_scale=float(grad_scale))
     fields = prepare_fields(batch, logits.device)
     if fused_head:
         loss, stats_dev, _ = linear_grpo_loss(hidden, _lm_head_of(model, False).weight, fields, params,
@@ -123,14 +182,8 @@ def rl_step(model, batch: PipelineBatchEncoding, current_step: int, max_step: in
     else:
         loss, stats_dev, _ = grpo_loss(logits, fields, params, values)
 
-    nseq = _num_sequences_device(batch)
-    if isinstance(nseq, torch.Tensor):
-        host = torch.cat([stats_dev, nseq.to(stats_dev.device, torch.float64).reshape(1)]).cpu().numpy()
-        num_sequences = int(host[-1])
-    else:
-        host = stats_dev.cpu().numpy()
-        num_sequences = nseq
-    return loss, build_stats(host, batch, params, kl_c, ent_c, num_sequences, has_value_head)
+    stats = RLStats(stats_dev, batch, params, kl_c, ent_c, _num_sequences_device(batch), has_value_head, bad_hidden)
+    return loss, (stats if defer_stats else stats.resolve())
 
 
 def _decoder_of(model):

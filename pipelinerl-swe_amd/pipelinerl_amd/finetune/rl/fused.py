@@ -7,8 +7,9 @@ autograd backward:
              statistics, and (when the logits require grad) writes dlogits for an upstream
              gradient of 1;
   backward — reads the upstream gradient on device; if it is 1 the precomputed dlogits are
-             returned untouched (no extra pass, no host sync); otherwise (sentinel batches
-             multiply the loss by 0, DeepSpeed scales by 1/GAS) dlogits are recomputed from
+             returned untouched (no extra pass, no host sync); the forward writes them for
+             ``params.grad_scale`` (DeepSpeed's 1/GAS loss scale, passed in by the loop); any
+             other upstream (sentinel batches multiply the loss by 0) recomputes dlogits from
              the logits with that scale.
 The statistics stay on device; the caller reads them back once.
 """
@@ -53,6 +54,8 @@ class GrpoParams:
     temperature: float = 1.0
     batch_size: float = 0.0
     value_loss_coef: float = 0.0
+    # the upstream gradient the forward writes dlogits / dvalues for (the caller's loss scale)
+    grad_scale: float = 1.0
 
     def to_c(self, write_grad: bool) -> _native.PrlGrpoParams:
         if self.policy_loss == "ppo":
@@ -64,7 +67,8 @@ class GrpoParams:
         return _native.PrlGrpoParams(
             kind, int(self.use_advantages), int(self.relu_log_p_weights), int(self.group_normalization),
             int(self.overlong_filtering), int(write_grad), self.epsilon, self.kl_coef, self.entropy_coef,
-            self.clamp_log_ratio, self.temperature, float(self.batch_size), self.value_loss_coef, 1.0)
+            self.clamp_log_ratio, self.temperature, float(self.batch_size), self.value_loss_coef,
+            float(self.grad_scale))
 
 
 FIELDS = ("input_ids", "labels", "rewards", "advantages", "ref_logprobs", "old_logprobs", "group_tokens",
@@ -153,6 +157,8 @@ class GrpoLossFn(torch.autograd.Function):
         d_logits = d_values = None
         if g_loss is None:
             return None, None, None, None
+        # absolute upstream: the kernel compares it with params.grad_scale (the scale the forward
+        # wrote dlogits at) and skips when they are equal
         g = g_loss.detach().to(torch.float32).reshape(1).contiguous()
         if ctx.dlogits is not None and ctx.needs_input_grad[0]:
             lib = _native.load()
@@ -165,9 +171,16 @@ class GrpoLossFn(torch.autograd.Function):
                                                 ctx.dlogits.data_ptr(), stream), "prl_grpo_backward")
             d_logits = ctx.dlogits if ctx.logits_dtype == ctx.dlogits.dtype else ctx.dlogits.to(ctx.logits_dtype)
         if ctx.dvalues is not None and ctx.needs_input_grad[1]:
-            d_values = ctx.dvalues * g
+            d_values = ctx.dvalues * _relative(g, ctx.params.grad_scale)
         ctx.dlogits = None
         return d_logits, d_values, None, None
+
+
+def _relative(g: torch.Tensor, scale: float) -> torch.Tensor:
+    """g / scale on device, exactly 1 where g == scale (gradients saved at ``scale``)."""
+    if scale == 1.0:
+        return g
+    return torch.where(g == scale, torch.ones_like(g), g / scale)
 
 
 def grpo_loss(logits: torch.Tensor, fields: dict, params: GrpoParams, values: torch.Tensor | None = None):

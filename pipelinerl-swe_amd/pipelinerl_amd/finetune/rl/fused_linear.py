@@ -15,11 +15,12 @@ final hidden states and the ``lm_head`` weight and, for the label rows only, in 
 then one ``prl_grpo_stats`` pass over all rows.  Peak extra memory is one [c, V] chunk (plus an
 fp32 [V, H] accumulator when there are several) instead of two [T, V] tensors, and the three lm_head GEMMs and the
 loss kernel skip the prompt rows.  The backward scales the saved dh / dW by the upstream
-gradient on device.
+gradient on device (relative to ``params.grad_scale``, the loss scale the forward formed them at).
 
 Semantics vs the reference: identical loss, statistics and gradients when the prompt rows'
 logits are finite.  Non-finite logits on a prompt row are not seen (the reference's finiteness
-assertion at :209 covers every row).  Opt-in: ``RLConfig.fused_lm_head``.
+assertion at :209 covers every row); rl_step checks the prompt rows' hidden states for
+finiteness instead.  ``RLConfig.fused_lm_head`` (default on).
 """
 
 from __future__ import annotations
@@ -30,7 +31,7 @@ import torch
 
 from ... import _native, gemm
 from ..._native import NSTAT, PRL_BF16, PRL_F32
-from .fused import GrpoParams, _workspace
+from .fused import GrpoParams, _relative, _workspace
 
 _ADDMM_F32: dict[str, bool] = {}
 
@@ -129,13 +130,14 @@ class LinearGrpoLossFn(torch.autograd.Function):
         ctx.dh, ctx.dw = dh, dw
         ctx.shape = (B, L, Hd)
         ctx.h_dtype, ctx.w_dtype = hidden.dtype, weight.dtype
+        ctx.grad_scale = float(params.grad_scale)
         return loss, stats, rows
 
     @staticmethod
     def backward(ctx, g_loss, g_stats, g_rows):
         d_hidden = d_weight = None
         if g_loss is not None and ctx.dh is not None:
-            g = g_loss.detach().to(torch.float32)
+            g = _relative(g_loss.detach().to(torch.float32), ctx.grad_scale)  # dh / dW formed at grad_scale
             if ctx.needs_input_grad[0]:
                 d_hidden = (ctx.dh.view(ctx.shape) * g.to(ctx.dh.dtype)).to(ctx.h_dtype)
             if ctx.needs_input_grad[1]:

@@ -43,7 +43,7 @@ from .finetune.checkpoints import (load_model, load_tokenizer, load_training_sta
                                    save_model_and_tokenizer, save_training_state)
 from .finetune.grad_sync import GradBuckets
 from .finetune.optim import get_optimizer
-from .finetune.rl import RLConfig, rl_step
+from .finetune.rl import RLConfig, RLStats, rl_step
 from .finetune.rl.utils import aggregate_rl_stats
 from .finetune.sharding import fsdp_requested, set_gradient_sync, shard_model
 from .finetune.types import PipelineBatchEncoding, TrainingMetrics
@@ -121,6 +121,8 @@ def run_data_loader(data_stream: SingleStreamSpec, batch_queue: Queue, device: t
                         if isinstance(v, torch.Tensor) and name != "seq_boundaries":  # host metadata
                             setattr(b, name, v.pin_memory().to(device, non_blocking=True))
                 batch_queue.put((b, ntok, nseq))
+        if stop is None or not stop.is_set():  # the reader went idle for `timeout` s: fail, not hang
+            batch_queue.put(TimeoutError(f"no training data on {data_stream} for {timeout} s"))
     except Exception as e:
         batch_queue.put(e)
 
@@ -172,6 +174,7 @@ def run_finetuning_loop(cfg, step_fn: Callable = rl_step, model=None, tokenizer=
     set_streams_backend(**cfg.streams)
     ctx = Dist(cfg.finetune.get("dist_backend"))
     args = cfg.finetune if "finetune" in cfg else cfg
+    grad_mode = grad_scale_convention(cfg)
     if args.gradient_accumulation_passes % ctx.world:
         raise ValueError("gradient_accumulation_passes must be divisible by num_processes")
     torch.manual_seed(args.seed)
@@ -236,7 +239,9 @@ def run_finetuning_loop(cfg, step_fn: Callable = rl_step, model=None, tokenizer=
         factory = weight_update_manager_factory or WeightUpdateManager
         wum = factory(urls, model, update_stream, actor_group, transport=args.get("weight_transport", "per_tensor"),
                       bucket_bytes=int(args.get("weight_bucket_mb", 256)) << 20,
-                      overlap=bool(args.get("overlap_weight_updates", True)), is_main=ctx.is_main)
+                      overlap=bool(args.get("overlap_weight_updates", True)), is_main=ctx.is_main,
+                      timeout_s=args.get("weight_update_timeout_s", 900.0),
+                      http_timeout_s=args.get("weight_update_http_timeout_s", 600.0))
         wum.send_weight_update(metrics.samples)
 
     batch_queue: Queue = Queue(maxsize=1)
@@ -248,7 +253,7 @@ def run_finetuning_loop(cfg, step_fn: Callable = rl_step, model=None, tokenizer=
     loader.start()
     try:
         return rl_finetuning_worker(args, ctx, model, optimizer, lr_scheduler, grads, wum, tokenizer, metrics,
-                                    batch_queue, update_stream, step_fn)
+                                    batch_queue, update_stream, step_fn, grad_scale_mode=grad_mode)
     finally:
         stop.set()
         if wum is not None:
@@ -260,9 +265,34 @@ def run_finetuning_loop(cfg, step_fn: Callable = rl_step, model=None, tokenizer=
                 dist.destroy_process_group(actor_group)
 
 
+def grad_scale_convention(cfg) -> str:
+    """Which engine's gradient-accumulation convention the run follows.  The reference's backend
+    is DeepSpeed ZeRO-3 by default (conf/base.yaml ``use_deepspeed: true``), whose
+    ``engine.backward`` divides every micro-batch loss by ``gradient_accumulation_steps``
+    (injected at finetune_loop.py:307-312); with Accelerate (FSDP or plain DDP, GAS 1) the
+    micro-batch gradients are summed.  ``finetune.grad_scale: accelerate | deepspeed`` overrides."""
+    args = cfg.finetune if "finetune" in cfg else cfg
+    mode = args.get("grad_scale")
+    if mode is None:
+        mode = "deepspeed" if cfg.get("use_deepspeed", False) and not cfg.get("use_fsdp", False) else "accelerate"
+    if mode not in ("accelerate", "deepspeed"):
+        raise ValueError(f"finetune.grad_scale must be 'accelerate' or 'deepspeed', got {mode!r}")
+    return mode
+
+
+def micro_batch_loss_scale(args, world: int, mode: str) -> float:
+    """1 / gradient_accumulation_steps under DeepSpeed, where GAS = seq_parallel *
+    gradient_accumulation_passes / num_processes (finetune_loop.py:306-310); 1 otherwise."""
+    if mode != "deepspeed":
+        return 1.0
+    gas = args.seq_parallel * (args.gradient_accumulation_passes // world)
+    return 1.0 / gas
+
+
 def rl_finetuning_worker(args, ctx: Dist, model, optimizer, lr_scheduler, grads: GradBuckets | None,
                          wum: WeightUpdateManager | None, tokenizer, metrics: TrainingMetrics, batch_queue: Queue,
-                         update_stream: SingleStreamSpec, step_fn: Callable = rl_step) -> TrainingMetrics:
+                         update_stream: SingleStreamSpec, step_fn: Callable = rl_step,
+                         grad_scale_mode: str = "accelerate") -> TrainingMetrics:
     """finetune_loop.py:488-867."""
     output_dir = Path(args.output_dir)
     current_dir, inter_dir, state_dir = output_dir / "current", output_dir / "intermediate", output_dir / "training_state"
@@ -289,6 +319,8 @@ def rl_finetuning_worker(args, ctx: Dist, model, optimizer, lr_scheduler, grads:
     waiting = 0.0
     sync_every = bool(args.get("fsdp_sync_every_micro_batch", False))
     safe = bool(args.get("use_safetensors", False))  # checkpoints.py:285 default
+    loss_scale = micro_batch_loss_scale(args, ctx.world, grad_scale_mode)
+    native_step = step_fn is rl_step
 
     def next_batch():
         timeout = 0.1
@@ -331,14 +363,22 @@ def rl_finetuning_worker(args, ctx: Dist, model, optimizer, lr_scheduler, grads:
         if do_step and grads is not None:
             grads.arm()
         set_gradient_sync(model, do_step or sync_every)  # FSDP: reduce-scatter on the boundary only
-        loss, stats = step_fn(model, batch, metrics.completed_steps, final_steps, rl_config)
+        if native_step:  # stats read back after the backward is queued; gradients at loss_scale
+            loss, stats = step_fn(model, batch, metrics.completed_steps, final_steps, rl_config,
+                                  grad_scale=loss_scale, defer_stats=True)
+        else:
+            loss, stats = step_fn(model, batch, metrics.completed_steps, final_steps, rl_config)
         if sentinel:
             loss = loss * 0.0
-        else:
+        elif loss_scale != 1.0:
+            loss = loss * loss_scale  # DeepSpeed's engine.backward: loss / gradient_accumulation_steps
+        loss.backward()
+        if isinstance(stats, RLStats):
+            stats = stats.resolve()  # also raises the reference's non-finite assertions
+        if not sentinel:
             for k, v in stats.items():
                 rl_metrics[k].append(v)
             metrics.lr = optimizer.param_groups[0]["lr"]
-        loss.backward()
         if not sentinel:
             passes_took.append(time.time() - t_pass)
         if ctx.is_main:
@@ -360,6 +400,7 @@ def rl_finetuning_worker(args, ctx: Dist, model, optimizer, lr_scheduler, grads:
         clip = args.get("gradient_clipping_threshold")
         gn = torch.nn.utils.clip_grad_norm_(model.parameters(), clip if clip else float("inf"))
         if wum is not None:
+            wum.poll()  # a failed update (actor error / timeout) ends training here
             wum.before_optimizer_step()
         optimizer.step()
         if grads is not None:

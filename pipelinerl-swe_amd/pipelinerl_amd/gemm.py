@@ -25,9 +25,10 @@ _PKG = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ["PRL_GEMM_LIB"]) if os.environ.get("PRL_GEMM_LIB") else _PKG / "libprl_gemm.so"
 HEADER_PATH = _PKG.parents[1] / "include" / "prl_gemm.h"
 SOLUTIONS_PATH = _PKG / "gemm_solutions.json"
-ABI_VERSION = 2
+ABI_VERSION = 3
 N_, T_ = 0, 1
 F32, BF16 = 0, 1
+PRL_GEMM_E_REFUSED = 4003
 
 _lib = None
 _solutions: dict | None = None
@@ -59,6 +60,7 @@ def load():
         "prl_gemm_heuristic_index": (c.c_int, [c.c_int, c.c_int, c.c_int64, c.c_int64, c.c_int64, c.c_int64,
                                                c.c_int64, c.c_int64, c.c_int, c.c_float]),
         "prl_gemm_library": (c.c_int, [c.c_char_p, c.c_int]),
+        "prl_gemm_allow_solutions": (c.c_int, [c.POINTER(c.c_int32), c.c_int]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -66,7 +68,15 @@ def load():
     if lib.prl_gemm_abi_version() != ABI_VERSION:
         raise GemmError("libprl_gemm.so ABI mismatch")
     _lib = lib
+    allow(sorted({int(e["index"]) for es in solutions().values() for e in es if int(e["index"]) >= 0}))
     return lib
+
+
+def allow(indices: list[int]) -> None:
+    """Register the solution indices prl_gemm may run (the shipped table's, swept clean on
+    MI355X); any other explicit index is refused by the library (PRL_GEMM_E_REFUSED)."""
+    arr = (ctypes.c_int32 * max(1, len(indices)))(*indices)
+    _check(load().prl_gemm_allow_solutions(arr, len(indices)), "prl_gemm_allow_solutions")
 
 
 def _check(rc: int, what: str):

@@ -25,6 +25,7 @@ What changes:
 from __future__ import annotations
 
 import ctypes
+import functools
 import logging
 import threading
 import time
@@ -143,24 +144,39 @@ def unwrap_model(model):
     return getattr(m, "pretrained_model", m)  # value-head wrapper: broadcast the LM only
 
 
-def http_post_request(url: str, message: BaseModel, timeout: float | None = None) -> None:
+class WeightUpdateError(RuntimeError):
+    """An actor refused or failed a weight update, or the update did not complete in time."""
+
+
+def http_post_request(url: str, message: BaseModel, timeout: float | None = 600.0) -> None:
+    """POST the request to one actor; raises WeightUpdateError on any HTTP error or timeout.
+    The reference logs and carries on (finetune_loop.py:157-166), after which its broadcast waits
+    in NCCL for an actor that will never join; here the error reaches the trainer."""
     import requests
 
     response = None
     try:
         response = requests.post(url + "/receive_weight_update", json=message.model_dump(), timeout=timeout)
         response.raise_for_status()
-    except requests.RequestException as e:  # logged, as the reference does (finetune_loop.py:157-166)
+    except requests.RequestException as e:
         logger.error(f"Error sending weight update request to {url}: {e}")
+        detail = f" - {response.status_code} {response.text[:200]}" if response is not None else ""
         if response is not None:
             logger.error(f"Response: {response.status_code} - {response.text}")
+        raise WeightUpdateError(f"weight update request to {url} failed: {e}{detail}") from e
 
 
 class WeightUpdateManager:
     def __init__(self, llm_urls: list[str], accelerated_model, update_stream, actor_update_group, *,
                  transport: str = "per_tensor", bucket_bytes: int = 256 << 20, overlap: bool = True,
-                 packer=None, post: Callable[[str, BaseModel], None] = http_post_request, is_main: bool = True,
-                 write_message: Callable[[Any, BaseModel], None] | None = None):
+                 packer=None, post: Callable[[str, BaseModel], None] | None = None, is_main: bool = True,
+                 write_message: Callable[[Any, BaseModel], None] | None = None, timeout_s: float | None = 900.0,
+                 http_timeout_s: float | None = 600.0):
+        """``timeout_s``: an update (every actor's HTTP answer and the whole broadcast) that has not
+        completed this long after its request raises WeightUpdateError from the next ``wait()`` /
+        ``send_weight_update()``; so does any actor's HTTP error, as soon as it arrives.  A failed
+        update aborts an RcclComm actor group (in-flight broadcasts return) — the trainer exits
+        instead of hanging in the collective (failure handling)."""
         self.llm_urls = list(llm_urls)
         self.model = accelerated_model
         self.update_stream = update_stream
@@ -169,7 +185,8 @@ class WeightUpdateManager:
         self.bucket_bytes = int(bucket_bytes)
         self.overlap = overlap
         self.packer = packer or HipFlatPacker()
-        self.post = post
+        self.post = post or functools.partial(http_post_request, timeout=http_timeout_s)
+        self.timeout_s = timeout_s
         self.is_main = is_main
         self.pool = ThreadPoolExecutor(max_workers=max(1, len(self.llm_urls)))
         self._write_message = write_message
@@ -263,19 +280,38 @@ class WeightUpdateManager:
 
         def finish():
             try:
-                if done is not None:
-                    done.synchronize()
-                else:  # gloo: wait() blocks this (waiter) thread only
-                    for w in works:
+                deadline = None if not self.timeout_s else t0 + float(self.timeout_s)
+                delay = 0.001
+                while True:  # an actor's HTTP error ends the wait at once, not the collective
+                    for url, f in zip(self.llm_urls, futures):
+                        if f.done() and f.exception() is not None:
+                            raise f.exception()
+                    comm_done = done.query() if done is not None else all(w.is_completed() for w in works)
+                    if comm_done and all(f.done() for f in futures):
+                        break
+                    if deadline is not None and time.time() > deadline:
+                        waiting = [u for u, f in zip(self.llm_urls, futures) if not f.done()]
+                        raise WeightUpdateError(
+                            f"weight update {version} not completed after {self.timeout_s:.0f} s "
+                            f"(broadcast {'done' if comm_done else 'in flight'}; actors not answered: {waiting})")
+                    time.sleep(delay)
+                    delay = min(delay * 2, 0.02)
+                if done is None:
+                    for w in works:  # gloo: surfaces a failed work's error
                         w.wait()
-                for f in futures:
-                    f.result()
                 self.last_latency_s = time.time() - t0
                 logger.info(f"Finished broadcasting weights for version {version} in {self.last_latency_s:.3f}s")
                 self._emit(WeightUpdateSuccess(version=version))
                 self.completed_versions.append(version)
             except BaseException as e:  # surfaced on the next wait()
+                logger.error(f"weight update {version} failed: {e}")
                 self._error = e
+                abort = getattr(self.group, "abort", None)
+                if callable(abort):  # RcclComm: in-flight broadcasts return instead of hanging
+                    try:
+                        abort()
+                    except Exception as ae:  # noqa: BLE001
+                        logger.error(f"aborting the actor group failed: {ae}")
 
         if self.overlap:
             self._inflight = threading.Thread(target=finish, name=f"weight-update-{version}", daemon=True)
@@ -294,6 +330,13 @@ class WeightUpdateManager:
     def wait(self) -> None:
         """Block until the in-flight update (if any) has been received by every actor."""
         if self._inflight is not None:
+            self._inflight.join()
+            self._inflight = None
+        self._raise()
+
+    def poll(self) -> None:
+        """Raise a failed in-flight update's error now, without waiting for a running one."""
+        if self._inflight is not None and not self._inflight.is_alive():
             self._inflight.join()
             self._inflight = None
         self._raise()

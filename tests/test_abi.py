@@ -2,6 +2,8 @@
 the Python binding's statistic table matches the header's enum."""
 
 import ctypes
+
+import pytest
 import re
 
 from conftest import ROOT
@@ -79,7 +81,7 @@ def test_gemm_library_exports_header_symbols():
     assert len(declared) >= 5
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.prl_gemm_abi_version() == gemm.ABI_VERSION == 2
+    assert lib.prl_gemm_abi_version() == gemm.ABI_VERSION == 3
     assert lib.prl_gemm_error_string(4001).decode() == "invalid argument"
     # m = 0, a bad op, null pointers, lda < m: all PRL_GEMM_E_INVALID
     assert lib.prl_gemm_bf16(0, 0, 0, 4, 4, 1, 4, 1, 4, None, 0.0, 1, 4, 1, -1, None) == 4001
@@ -89,6 +91,37 @@ def test_gemm_library_exports_header_symbols():
     assert lib.prl_gemm_bf16(0, 0, 4, 4, 4, 1, 4, 1, 4, None, 0.5, 1, 4, 1, -1, None) == 4001  # beta in {0, 1}
     assert lib.prl_gemm_bf16(0, 0, 4, 4, 4, 1, 4, 1, 4, 1, 0.0, 1, 4, 0, -1, None) == 4001  # bias needs bf16 D
     assert lib.prl_gemm_heuristic_index(0, 0, 0, 1, 1, 1, 1, 1, 1, 0.0) == -1
+
+
+def test_gemm_refuses_unswept_solution_indices():
+    """prl_gemm runs an explicit hipBLASLt solution index only if it is in the registered
+    (swept-clean) set: the binding registers gemm_solutions.json's indices at load, and any other
+    index is refused with PRL_GEMM_E_REFUSED before a device is touched (a catalog
+    solution outside the swept set faulted the GPU in a sweep).  The pointers below are never
+    dereferenced: the refusal comes first."""
+    import json
+
+    from pipelinerl_amd import gemm
+
+    lib = gemm.load()
+    shipped = sorted({int(e["index"]) for es in json.loads(gemm.SOLUTIONS_PATH.read_text()).values() for e in es
+                      if int(e["index"]) >= 0})
+    assert shipped
+    unswept = max(shipped) + 1
+    args = (0, 0, 4, 4, 4, 16, 4, 16, 4, None, 0.0, 16, 4, 1)
+    assert lib.prl_gemm_bf16(*args, unswept, None) == gemm.PRL_GEMM_E_REFUSED == 4003
+    assert b"allowed" in lib.prl_gemm_error_string(4003)
+    with pytest.raises(gemm.GemmError, match="allowed"):
+        gemm._check(lib.prl_gemm_bf16(*args, unswept, None), "prl_gemm_bf16")
+    # re-registering a smaller set refuses what was allowed before; an empty set allows none
+    try:
+        gemm.allow(shipped[1:])
+        assert lib.prl_gemm_bf16(*args, shipped[0], None) == 4003
+        gemm.allow([])
+        assert all(lib.prl_gemm_bf16(*args, i, None) == 4003 for i in shipped[:3])
+        assert lib.prl_gemm_allow_solutions(None, 2) == 4001
+    finally:
+        gemm.allow(shipped)
 
 
 def test_gemm_solution_window(monkeypatch):

@@ -116,3 +116,69 @@ def test_resume_from_training_state(tmp_path):
     assert m["steps"] == 1
     state = torch.load(exp / "finetune" / "training_state" / "training_state.pt", weights_only=True)
     assert state["completed_steps"] == 1 and "optimizer_state" in state
+
+
+def _grad_capture_main(rank, world, port, exp, steps, passes, extra):
+    """_rank_main with torch.nn.utils.clip_grad_norm_ wrapped to record the gradients just
+    before and just after clipping at every optimizer step."""
+    import torch.nn.utils as nnu
+
+    orig = nnu.clip_grad_norm_
+    rec = []
+
+    def clip(params, max_norm, *a, **k):
+        params = list(params)
+        before = torch.cat([p.grad.detach().reshape(-1).clone() for p in params if p.grad is not None])
+        n = orig(params, max_norm, *a, **k)
+        after = torch.cat([p.grad.detach().reshape(-1).clone() for p in params if p.grad is not None])
+        rec.append({"before": before, "after": after, "norm": float(n)})
+        return n
+
+    nnu.clip_grad_norm_ = clip
+    try:
+        _rank_main(rank, world, port, exp, steps, passes, extra)
+    finally:
+        nnu.clip_grad_norm_ = orig
+    torch.save(rec, Path(exp) / f"grads_r{rank}.pt")
+
+
+def test_deepspeed_grad_scale_convention(tmp_path):
+    """finetune.grad_scale: deepspeed divides every micro-batch loss by GAS =
+    seq_parallel * gradient_accumulation_passes / world (DeepSpeed's engine.backward with the
+    gradient_accumulation_steps the reference injects, finetune_loop.py:306-312); accelerate
+    (GAS 1) sums them.  The gradient the clip sees — and so the clip decision at 0.3 — differs
+    by exactly 1/GAS; after clipping both are the clipped form of their own gradient."""
+    world = 2
+    runs = {}
+    for mode in ("accelerate", "deepspeed"):
+        exp = tmp_path / mode
+        exp.mkdir()
+        per_step, _ = _setup(exp, world)
+        mp.spawn(_grad_capture_main, args=(world, free_port(), str(exp), 1, per_step, {"grad_scale": mode}),
+                 nprocs=world, join=True)
+        runs[mode] = torch.load(exp / "grads_r0.pt")
+    gas = per_step // world
+    assert gas > 1
+    acc, ds = runs["accelerate"][0], runs["deepspeed"][0]
+    rel = float((ds["before"] * gas - acc["before"]).abs().max() / acc["before"].abs().max())
+    assert rel < 1e-5, rel
+    assert abs(ds["norm"] * gas - acc["norm"]) <= 1e-5 * acc["norm"]
+    for r in (acc, ds):
+        want = r["before"] * min(1.0, 0.3 / (r["norm"] + 1e-6))
+        assert torch.allclose(r["after"], want, rtol=1e-5, atol=1e-9)
+
+
+def test_grad_scale_convention_follows_the_backend():
+    from pipelinerl_amd.config import Cfg
+    from pipelinerl_amd.finetune_loop import grad_scale_convention, micro_batch_loss_scale
+
+    assert grad_scale_convention(Cfg.wrap({"finetune": {}})) == "accelerate"
+    assert grad_scale_convention(Cfg.wrap({"use_deepspeed": True, "finetune": {}})) == "deepspeed"
+    assert grad_scale_convention(Cfg.wrap({"use_deepspeed": True, "use_fsdp": True, "finetune": {}})) == "accelerate"
+    assert grad_scale_convention(Cfg.wrap({"use_deepspeed": True, "finetune": {"grad_scale": "accelerate"}})) \
+        == "accelerate"
+    with pytest.raises(ValueError):
+        grad_scale_convention(Cfg.wrap({"finetune": {"grad_scale": "zero3"}}))
+    args = Cfg.wrap({"seq_parallel": 1, "gradient_accumulation_passes": 1024})
+    assert micro_batch_loss_scale(args, 4, "deepspeed") == 1 / 256
+    assert micro_batch_loss_scale(args, 4, "accelerate") == 1.0

@@ -33,3 +33,75 @@ def test_patched_cpu_model_equals_eager(tmp_path):
         assert torch.equal(p.grad, q.grad), name
     # no hand-over left pending on any norm after a full forward
     assert all(m.__dict__.get("_prl_pending") is None for m in patched.modules())
+
+
+def test_decoder_patch_keeps_the_installed_layer_contract(tmp_path):
+    """transformers 5.x layers return a tensor; 4.x layers (the reference pins 4.51.1,
+    pyproject.toml:20) return a tuple that Qwen2Model indexes with [0], and gradient
+    checkpointing passes their arguments positionally.  The patched forward must return what
+    the original returns, for either contract."""
+    import types
+
+    from pipelinerl_amd.finetune import model_ops
+
+    class Norm(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.weight = torch.nn.Parameter(torch.ones(8))
+            self.variance_epsilon = 1e-6
+
+        def forward(self, x):
+            return x * 2.0
+
+    class Attn(torch.nn.Module):
+        def forward(self, hidden_states, position_embeddings=None, attention_mask=None, past_key_value=None,
+                    cache_position=None, **kwargs):
+            self.seen = dict(kwargs, attention_mask=attention_mask, past_key_value=past_key_value,
+                             position_embeddings=position_embeddings)
+            return hidden_states + 1.0, "weights"
+
+    class Layer4x(torch.nn.Module):  # transformers 4.51 Qwen2DecoderLayer.forward contract
+        def __init__(self):
+            super().__init__()
+            self.input_layernorm, self.post_attention_layernorm = Norm(), Norm()
+            self.self_attn, self.mlp = Attn(), torch.nn.Identity()
+
+        def forward(self, hidden_states, attention_mask=None, position_ids=None, past_key_value=None,
+                    output_attentions=False, use_cache=False, cache_position=None, position_embeddings=None,
+                    **kwargs):
+            r = hidden_states
+            a, w = self.self_attn(hidden_states=self.input_layernorm(hidden_states), attention_mask=attention_mask,
+                                  position_ids=position_ids, past_key_value=past_key_value,
+                                  output_attentions=output_attentions, use_cache=use_cache,
+                                  cache_position=cache_position, position_embeddings=position_embeddings, **kwargs)
+            h = r + a
+            h = h + self.mlp(self.post_attention_layernorm(h))
+            return (h, w) if output_attentions else (h,)
+
+    class Layer5x(Layer4x):  # transformers 5.x contract: tensor out, past_key_values
+        def forward(self, hidden_states, attention_mask=None, position_ids=None, past_key_values=None,
+                    use_cache=False, position_embeddings=None, **kwargs):
+            r = hidden_states
+            a, _ = self.self_attn(hidden_states=self.input_layernorm(hidden_states), attention_mask=attention_mask,
+                                  position_ids=position_ids, past_key_values=past_key_values, use_cache=use_cache,
+                                  position_embeddings=position_embeddings, **kwargs)
+            h = r + a
+            return h + self.mlp(self.post_attention_layernorm(h))
+
+    x = torch.randn(1, 5, 8)
+    pe = (torch.zeros(1, 5, 8), torch.ones(1, 5, 8))
+    for cls in (Layer4x, Layer5x):
+        layer = cls()
+        want = layer(x, None, None, None, position_embeddings=pe) if cls is Layer5x else \
+            layer(x, None, None, None, False, False, None, pe)
+        layer.__dict__["_prl_orig_forward"] = layer.forward
+        layer.forward = types.MethodType(model_ops._decoder_forward, layer)
+        if cls is Layer4x:
+            got = layer(x, None, None, None, False, False, None, pe)  # checkpointing: positional
+            assert isinstance(got, tuple) and len(got) == 1 and torch.equal(got[0], want[0])
+            got = layer(x, attention_mask=None, position_embeddings=pe, output_attentions=True)
+            assert isinstance(got, tuple) and got[1] == "weights" and torch.equal(got[0], want[0])
+            assert layer.self_attn.seen["position_embeddings"] is pe
+        else:
+            got = layer(x, position_embeddings=pe, past_key_values=None)
+            assert isinstance(got, torch.Tensor) and torch.equal(got, want)

@@ -122,3 +122,83 @@ def test_actor_group_interoperates_with_reference_helper(tmp_path):
     got = torch.load(tmp_path / "actor0_params.pt")
     for n in want:
         assert torch.equal(got[n], want[n].to(torch.bfloat16)), n
+
+
+def _failing_trainer(port, exp, mode):
+    """Trainer rank of the fail-fast tests: an actor HTTP server that answers 500 ('http500')
+    or answers 200 but never joins the broadcast ('silent'); wait() must raise, quickly."""
+    import threading
+    import time
+    from http.server import BaseHTTPRequestHandler, HTTPServer
+
+    sys.path[:0] = [str(ROOT), str(ROOT / "pipelinerl-swe_amd")]
+    from pipelinerl_amd import torch_utils
+    from pipelinerl_amd.weight_update import WeightUpdateError, WeightUpdateManager
+
+    class H(BaseHTTPRequestHandler):
+        def do_POST(self):
+            self.rfile.read(int(self.headers.get("Content-Length", 0)))
+            code = 500 if mode == "http500" else 200
+            self.send_response(code)
+            self.end_headers()
+            self.wfile.write(b'{"status": "error"}' if code == 500 else b'{"status": "ok"}')
+
+        def log_message(self, *a):
+            pass
+
+    srv = HTTPServer(("127.0.0.1", 0), H)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    url = f"http://127.0.0.1:{srv.server_address[1]}"
+    model = make_model(0)
+    pg = torch_utils.init_extra_process_group(group_name="actor", backend="gloo",
+                                              init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=2)
+    mgr = WeightUpdateManager([url], model, None, pg, transport="bucketed", bucket_bytes=1000, overlap=True,
+                              packer=TorchFlatPacker(), write_message=lambda s, m: None, timeout_s=3.0,
+                              http_timeout_s=5.0)
+    t0 = time.time()
+    mgr.send_weight_update(1)
+    err = None
+    try:
+        mgr.wait()
+    except WeightUpdateError as e:
+        err = str(e)
+    Path(exp, "result.json").write_text(json.dumps({"error": err, "elapsed": time.time() - t0}))
+    os._exit(0)  # the never-matched gloo broadcast stays pending: skip its destructor
+
+
+def _failing_actor(port, exp):
+    import time
+
+    sys.path[:0] = [str(ROOT), str(ROOT / "pipelinerl-swe_amd")]
+    from pipelinerl_amd import torch_utils
+
+    torch_utils.init_extra_process_group(group_name="actor", backend="gloo", init_method=f"tcp://127.0.0.1:{port}",
+                                         rank=1, world_size=2)
+    t0 = time.time()
+    while not Path(exp, "result.json").exists() and time.time() - t0 < 60:
+        time.sleep(0.05)  # a dead actor: never receives
+    os._exit(0)
+
+
+def _run_failing(rank, port, exp, mode):
+    os.environ["OMP_NUM_THREADS"] = "1"
+    if rank == 0:
+        _failing_trainer(port, exp, mode)
+    else:
+        _failing_actor(port, exp)
+
+
+@pytest.mark.parametrize("mode", ["http500", "silent"])
+def test_failed_actor_makes_the_trainer_raise(tmp_path, mode):
+    """SURVEY.md §5 failure row: the reference logs an actor's HTTP error and then blocks in the
+    broadcast until the process-group timeout (finetune_loop.py:155-172).  Here an HTTP 500
+    raises WeightUpdateError from wait() at once; an actor that never joins the broadcast
+    raises after WeightUpdateManager's timeout (3 s in this test)."""
+    port = free_port()
+    mp.spawn(_run_failing, args=(port, str(tmp_path), mode), nprocs=2, join=True)
+    r = json.loads((tmp_path / "result.json").read_text())
+    assert r["error"] is not None
+    if mode == "http500":
+        assert "500" in r["error"] and r["elapsed"] < 3.0
+    else:
+        assert "not completed" in r["error"] and 2.5 < r["elapsed"] < 10.0

@@ -82,6 +82,16 @@ int main(int argc, char** argv) {
     argc -= 2;
     argv += 2;
   }
+  // PRL_PROBE_SKIP=i,j,...: solution indices never launched (a blacklist of faulting solutions);
+  // every index is logged to stderr (flushed) BEFORE its first launch, so a fault names it
+  std::vector<int> skip;
+  if (const char* env = getenv("PRL_PROBE_SKIP")) {
+    for (const char* q = env; *q;) {
+      skip.push_back(atoi(q));
+      while (*q && *q != ',') ++q;
+      if (*q == ',') ++q;
+    }
+  }
   if (argc < 5 || (argc - 1) % 4) {
     fprintf(stderr, "usage: %s <fwd|dgrad|wgrad> T N K [...]\n", argv[0]);
     return 2;
@@ -181,7 +191,12 @@ int main(int argc, char** argv) {
               HIPBLAS_STATUS_SUCCESS ||
           need > ws_bytes)
         continue;
+      const int idx = hipblaslt_ext::getIndexFromAlgo(all[i].algo);
+      if (std::find(skip.begin(), skip.end(), idx) != skip.end()) continue;
       ++supported;
+      fprintf(stderr, "launch %s %lld %lld %lld index %d (position %zu)\n", pass, (long long)T, (long long)N,
+              (long long)K, idx, i);
+      fflush(stderr);
       float t = time_algo(&all[i].algo);
       if (t > 0) res.emplace_back(t, (int)i);
       if (supported % 200 == 0) {
