@@ -22,6 +22,14 @@ under "trainer_step" (pipelinerl_amd/trainer_probe.py): Qwen2.5-1.5B shapes (ran
 RMSNorm / SwiGLU / RoPE, label-row lm_head + fused loss head, backward), the bucketed RCCL
 gradient all-reduce overlapped with the last backward, clip, fused AdamW.
 
+Then, at every N, "c3_dp": BASELINE.json configs[2] (C3), the Qwen2.5-7B data-parallel trainer step
+on C3's packed math rollouts (prompt U{64..512} + completion U{256..8192}, packing cap 12 000), 4
+micro-batches per rank, with the full bucketed 15.23 GB gradient all-reduce at N > 1: the replica's
+step without the all-reduce, the DP step and the all-reduce alone, its exposed share and overlap,
+and the tokens/s extrapolated to C3's 4096-sample step (one all-reduce per ~hundreds of
+micro-batches).  trainer_step at N > 1 likewise times the replica alone first: dp_efficiency is
+the trainer-step scaling fraction at this N.
+
 At N > 1, last, BASELINE.json configs[3] (C4) is measured under "split_pipeline": ranks
 [0, N/2) train Qwen2.5-7B shapes data-parallel while ranks [N/2, N) act as actors; trainer rank 0
 broadcasts each step's weights to them (WeightUpdateManager -> WorkerExtension) while the
@@ -114,7 +122,15 @@ def host_cpu() -> dict:
                     break
     except OSError:
         pass
-    return {"cpu_model": model, "nproc": os.cpu_count()}
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "torch": torch.__version__}
+
+
+def cpu_threads() -> int:
+    """The CPU share this process is given: OMP_NUM_THREADS when the pool sets it (16 per GPU on
+    the MI355X boxes, whose nproc counts the whole 256-CPU machine), else the affinity mask."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    return max(1, int(env)) if env and env.isdigit() else len(os.sched_getaffinity(0))
 
 
 def load_traffic(T: int, V: int) -> tuple[float | None, str | None]:
@@ -140,6 +156,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-comm-probe", action="store_true", help="N > 1: skip the all-reduce / broadcast probes")
     ap.add_argument("--no-trainer-step", action="store_true", help="skip the full trainer-step probe")
+    ap.add_argument("--no-c3", action="store_true", help="skip the configs[2] 7B DP trainer-step probe")
     ap.add_argument("--no-fsdp", action="store_true", help="N >= 4: skip the configs[4] FSDP 32B probe")
     ap.add_argument("--no-split-pipeline", action="store_true",
                     help="N > 1: skip the split trainer/actor probe (configs[3]: 7B, overlapped weight broadcast)")
@@ -250,6 +267,17 @@ def main():
         trainer = optional("trainer_step", lambda: trainer_step_probe("1.5b", tokens=T, micro_batches=2, steps=2,
                                                                       warmup=1, device=dev, fused_head=True))
 
+    c3 = None
+    if not args.no_c3:
+        # configs[2] (C3): Qwen2.5-7B DP trainer step on C3's packed math rollouts, with the full
+        # bucketed 15.23 GB gradient all-reduce at N > 1 (local / DP / all-reduce-alone timings)
+        from pipelinerl_amd.trainer_probe import dp_step_probe
+
+        torch.cuda.empty_cache()
+        c3 = optional("c3_dp", lambda: dp_step_probe("c3", micro_batches=4, steps=2, warmup=1, device=dev,
+                                                      layers=4 if rehearse else None))
+        torch.cuda.empty_cache()
+
     split = None
     if world > 1 and not args.no_split_pipeline:
         # configs[3] (C4): half the ranks train Qwen2.5-7B shapes data-parallel, the other half are
@@ -292,12 +320,13 @@ def main():
         traffic, tsrc = load_traffic(T, V)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            threads = min(os.cpu_count() or 1, 16)
+            threads = cpu_threads()
             cpu = cpu_baseline(args.cpu_rows, V, threads)
-            # the reference's CPU finetune path (configs[0], C1: Qwen2.5-0.5B micro-batch step)
+            # the reference's CPU finetune path on configs[0] (C1: Qwen2.5-0.5B, 256 packed
+            # rollouts, one optimizer step; a bounded sample of its micro-batches, extrapolated)
             from oracle import cpu_trainer
 
-            cpu["trainer_step"] = cpu_trainer.cpu_trainer_step(threads=threads)
+            cpu["c1"] = cpu_trainer.cpu_c1_step(threads)
             cpu["host"] = host_cpu()
         out = {
             "metric": "trainer tokens/s (packed GRPO) at 1/2/4/8 MI355X; loss-kernel HBM GB/s",
@@ -326,6 +355,8 @@ def main():
             out["exchange"] = comm
         if trainer is not None:
             out["trainer_step"] = trainer
+        if c3 is not None:
+            out["c3_dp"] = c3
         if split is not None:
             out["split_pipeline"] = split
         if fsdp is not None:

@@ -96,3 +96,59 @@ def cpu_trainer_step(n_seq: int = 2, seq: int = 512, prompt: int = 128, threads:
             "sample": f"{steps} x Qwen2.5-0.5B-shaped (random init, bf16) micro-batch step of {n_seq} x {seq} tokens "
                       f"on CPU: HF forward, numpy-oracle loss head + dlogits, backward, clip, AdamW; {dt:.2f} s/step",
             "loss": float(loss)}
+
+
+def cpu_c1_step(threads: int, sample_micro_batches: int = 2) -> dict:
+    """BASELINE.json configs[0] (C1) on CPU, as BASELINE.md §3 / SURVEY.md §8(d) describe it:
+    Qwen2.5-0.5B shapes, 256 rollouts (32 groups x 8, prompt U{32..128} + completion U{16..384})
+    packed at seq_length 4096 by the preprocessor's packer, ONE optimizer step (every micro-batch:
+    HF forward with packed-sequence attention, the oracle's loss head + d loss / d logits,
+    backward; then clip 0.3 and AdamW).  Bounded sample: the first ``sample_micro_batches``
+    micro-batches are run and timed, the optimizer tail once; the step time is their per-token
+    time x the step's tokens (Σ attention_mask, finetune_loop.py:259-263) + the tail."""
+    from pipelinerl_amd import workloads
+    from pipelinerl_amd.finetune.attention import packed_kwargs, register
+    from transformers import AutoModelForCausalLM, Qwen2Config
+
+    torch.set_num_threads(threads)
+    data = workloads.rollouts("c1", 256)
+    mbs = [b for _, b in workloads.pack(data, 4096, 256) if not b.sentinel]
+    step_tokens = sum(int(b.attention_mask.sum()) for b in mbs)
+    model = qwen05_cpu()
+    cfg = Qwen2Config(**QWEN05)
+    cfg._attn_implementation = register()  # packed rollouts: attention stays inside each one
+    model.config._attn_implementation = cfg._attn_implementation
+    for layer in model.model.layers:
+        layer.self_attn.config._attn_implementation = cfg._attn_implementation
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-6, weight_decay=0.01)
+    rl = dict(GRPO, batch_size=256)
+
+    def micro(b):
+        ids = b.input_ids
+        out = model(input_ids=ids, position_ids=b.position_ids, use_cache=False, **packed_kwargs(b, ids.device))
+        lg = out.logits.detach().float().numpy()
+        host = {k: getattr(b, k).numpy() for k in ("input_ids", "labels", "position_ids", "rewards", "advantages",
+                                                   "ref_logprobs", "old_logprobs", "group_tokens", "num_labels",
+                                                   "overflow")}
+        host["is_packed"] = True
+        o = grpo_oracle.rl_step_oracle(lg, host, rl, 0, 1, dtype=np.float32, threads=threads, row_chunk=16)
+        out.logits.backward(torch.from_numpy(o["dlogits"]).to(out.logits.dtype))
+        return int(b.attention_mask.sum())
+
+    micro(mbs[-1])  # untimed warm-up on the shortest (tail) micro-batch
+    opt.zero_grad(set_to_none=True)
+    t0 = time.perf_counter()
+    sampled = sum(micro(b) for b in mbs[:sample_micro_batches])
+    t_mb = time.perf_counter() - t0
+    t1 = time.perf_counter()
+    torch.nn.utils.clip_grad_norm_(model.parameters(), 0.3)
+    opt.step()
+    opt.zero_grad(set_to_none=True)
+    t_tail = time.perf_counter() - t1
+    t_step = t_mb / sampled * step_tokens + t_tail
+    return {"value": round(step_tokens / t_step, 1), "unit": "tokens/s", "cores": threads, "kind": "port",
+            "sample": f"C1: Qwen2.5-0.5B-shaped (random init, bf16) optimizer step over 256 rollouts = "
+                      f"{len(mbs)} packed micro-batches, {step_tokens} tokens; {sample_micro_batches} micro-batches "
+                      f"({sampled} tokens, {t_mb:.1f} s) + clip/AdamW ({t_tail:.1f} s) timed, step = per-token time "
+                      f"x step tokens + tail = {t_step:.1f} s; HF forward, numpy-oracle loss head, backward",
+            "step_tokens": step_tokens, "micro_batches": len(mbs), "step_s": round(t_step, 2)}

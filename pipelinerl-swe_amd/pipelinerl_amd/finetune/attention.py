@@ -143,7 +143,7 @@ def varlen_attention_forward(module, query, key, value, attention_mask, scaling=
     if hip_bwd and default_scaling:  # the build's kernels: errors propagate (no silent fallback)
         out = PackedCausalAttention.apply(q.contiguous(), k.contiguous(), v.contiguous(), cu, mx, list(bounds))
         return out.unsqueeze(0), None
-    if default_scaling and q.is_cuda and _varlen_ok is not False:
+    if default_scaling and q.is_cuda and q.dtype in (torch.bfloat16, torch.float16) and _varlen_ok is not False:
         try:
             from torch.nn.attention.varlen import varlen_attn
 

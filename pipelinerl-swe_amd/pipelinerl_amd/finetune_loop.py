@@ -321,6 +321,7 @@ def rl_finetuning_worker(args, ctx: Dist, model, optimizer, lr_scheduler, grads:
     safe = bool(args.get("use_safetensors", False))  # checkpoints.py:285 default
     loss_scale = micro_batch_loss_scale(args, ctx.world, grad_scale_mode)
     native_step = step_fn is rl_step
+    defer_stats = os.environ.get("PRL_DEFER_STATS", "1") != "0"  # 0: read them before backward (A/B)
 
     def next_batch():
         timeout = 0.1
@@ -365,7 +366,7 @@ def rl_finetuning_worker(args, ctx: Dist, model, optimizer, lr_scheduler, grads:
         set_gradient_sync(model, do_step or sync_every)  # FSDP: reduce-scatter on the boundary only
         if native_step:  # stats read back after the backward is queued; gradients at loss_scale
             loss, stats = step_fn(model, batch, metrics.completed_steps, final_steps, rl_config,
-                                  grad_scale=loss_scale, defer_stats=True)
+                                  grad_scale=loss_scale, defer_stats=defer_stats)
         else:
             loss, stats = step_fn(model, batch, metrics.completed_steps, final_steps, rl_config)
         if sentinel:

@@ -101,7 +101,12 @@ class TrainerStep:
     def __init__(self, name: str = "1.5b", tokens: int = 16384, seq: int = 2048, prompt: int = 256,
                  micro_batches: int = 4, device=None, fused_head: bool = False, grad_ckpt: bool = False,
                  fused_ops: bool = True, group=None, model=None, step_fn=None, vocab: int | None = None,
-                 fsdp: bool = False, kl_coef: float = 0.0, layers: int | None = None):
+                 fsdp: bool = False, kl_coef: float = 0.0, layers: int | None = None, batches: list | None = None,
+                 samples_per_step: int | None = None, local: bool = False):
+        """``batches``: the packed micro-batches to train on (host PipelineBatchEncodings, e.g. from
+        workloads.micro_batches), ``samples_per_step`` their global sample count (RLConfig.batch_size);
+        default: ``micro_batches`` synthetic batches of ``tokens`` tokens.  ``local``: no gradient
+        all-reduce even under a multi-rank group (the replica's compute alone, for the DP overhead)."""
         from .finetune.grad_sync import GradBuckets
         from .finetune.optim import get_optimizer
         from .finetune.sharding import shard_model
@@ -121,11 +126,23 @@ class TrainerStep:
             from .finetune.rl import rl_step as step_fn
         self.step_fn = step_fn
         self.opt = get_optimizer("adamw_torch", self.model, 1e-6, 0.01)
-        self.grads = GradBuckets(list(self.model.parameters()), group=group) if world > 1 and not fsdp else None
+        self.grads = GradBuckets(list(self.model.parameters()), group=group) \
+            if world > 1 and not fsdp and not local else None
         V = vocab or QWEN[name]["vocab_size"]
-        self.batches = [packed_batch(tokens, seq, prompt, V, self.device, seed=rank * 97 + i, ref_noise=kl_coef > 0)
-                        for i in range(micro_batches)]
-        self.cfg = rl_config(micro_batches * (tokens // seq) * world, fused_head, kl_coef)
+        if batches is not None:
+            self.batches = []
+            for b in batches:
+                sb = b.seq_boundaries
+                b = b.to_device(self.device)
+                b.seq_boundaries = sb  # host metadata, as the trainer's loader keeps it
+                self.batches.append(b)
+            self.micro_batches = len(self.batches)
+            self.tokens = sum(int(b.attention_mask.sum()) for b in self.batches) / max(1, len(self.batches))
+            self.cfg = rl_config(samples_per_step or 1, fused_head, kl_coef)
+        else:
+            self.batches = [packed_batch(tokens, seq, prompt, V, self.device, seed=rank * 97 + i,
+                                         ref_noise=kl_coef > 0) for i in range(micro_batches)]
+            self.cfg = rl_config(micro_batches * (tokens // seq) * world, fused_head, kl_coef)
 
     def step(self, wum=None, version: int = 0) -> None:
         from .finetune.sharding import set_gradient_sync
@@ -171,6 +188,29 @@ class TrainerStep:
             dist.all_reduce(dt, op=dist.ReduceOp.MAX, group=self.group)
         return float(dt) / steps
 
+    def allreduce_alone(self, iters: int = 3) -> float:
+        """Seconds of the bucketed gradient all-reduce over the model's real buckets with no
+        backward to hide behind (max over the group's ranks)."""
+        if self.grads is None:
+            return 0.0
+        params = [p for p in self.model.parameters() if p.requires_grad]
+        times = []
+        for it in range(iters + 1):
+            _sync(self.device)
+            dist.barrier(self.group)
+            t0 = time.perf_counter()
+            self.grads.arm()
+            for p in reversed(params):  # the order backward produces gradients
+                self.grads._hook(p)
+            self.grads.finish()
+            _sync(self.device)
+            if it:
+                times.append(time.perf_counter() - t0)
+        self.grads.zero_()
+        dt = torch.tensor([sum(times) / len(times)], dtype=torch.float64, device=self.device)
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX, group=self.group)
+        return float(dt)
+
     def close(self) -> None:
         if self.grads is not None:
             self.grads.remove()
@@ -182,20 +222,115 @@ class TrainerStep:
 def trainer_step_probe(name: str = "1.5b", tokens: int = 16384, seq: int = 2048, prompt: int = 256,
                        micro_batches: int = 4, steps: int = 3, warmup: int = 1, device=None,
                        fused_head: bool = False, grad_ckpt: bool = False, fused_ops: bool = True) -> dict:
+    """The optimizer step at this world size.  With several ranks the same replica is also timed
+    without the gradient all-reduce first (``local_tokens_per_s_per_gpu``: what one GPU does on its
+    own, on this node at this moment), so ``dp_efficiency`` = DP / local tokens/s per GPU is the
+    trainer-step scaling fraction of this N, measured beside it."""
     device = device or torch.device("cuda", torch.cuda.current_device())
     torch.cuda.reset_peak_memory_stats(device)
-    ts = TrainerStep(name, tokens, seq, prompt, micro_batches, device, fused_head, grad_ckpt, fused_ops)
+    multi = dist.is_initialized() and dist.get_world_size() > 1
+    ts = TrainerStep(name, tokens, seq, prompt, micro_batches, device, fused_head, grad_ckpt, fused_ops, local=multi)
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    local = None
+    if multi:
+        from .finetune.grad_sync import GradBuckets
+
+        local = ts.timed(steps, warmup)
+        ts.grads = GradBuckets(list(ts.model.parameters()))
     sec = ts.timed(steps, warmup)
-    world = ts.world
     peak = torch.cuda.max_memory_allocated(device) / 1e9
     ts.close()
     total = tokens * micro_batches * world
-    return {"model": f"Qwen2.5-{name} shapes (random init, bf16)", "tokens_per_micro_batch": tokens,
-            "micro_batches_per_step": micro_batches, "seq_len": seq, "prompt_len": prompt,
-            "loss_head": "fused_lm_head" if fused_head else "fused", "fused_model_ops": fused_ops,
-            "ms_per_optimizer_step": round(sec * 1e3, 2),
-            "tokens_per_s": round(total / sec, 1), "tokens_per_s_per_gpu": round(total / sec / world, 1),
-            "peak_mem_gb": round(peak, 2), "steps": steps, "warmup": warmup}
+    out = {"model": f"Qwen2.5-{name} shapes (random init, bf16)", "tokens_per_micro_batch": tokens,
+           "micro_batches_per_step": micro_batches, "seq_len": seq, "prompt_len": prompt,
+           "loss_head": "fused_lm_head" if fused_head else "fused", "fused_model_ops": fused_ops,
+           "ms_per_optimizer_step": round(sec * 1e3, 2),
+           "tokens_per_s": round(total / sec, 1), "tokens_per_s_per_gpu": round(total / sec / world, 1),
+           "peak_mem_gb": round(peak, 2), "steps": steps, "warmup": warmup, "world": world}
+    if local is not None:
+        out["local_tokens_per_s_per_gpu"] = round(total / world / local, 1)
+        out["ms_per_optimizer_step_local"] = round(local * 1e3, 2)
+        out["dp_efficiency"] = round(local / sec, 4)
+    return out
+
+
+def dp_step_probe(config: str = "c3", micro_batches: int = 4, steps: int = 2, warmup: int = 1, device=None,
+                  samples_per_step: int = 4096, layers: int | None = None, batches: list | None = None,
+                  model=None, step_fn=None) -> dict:
+    """BASELINE.json configs[2] (C3) data-parallel trainer step on this rank's GPU: the config's
+    model shapes (Qwen2.5-7B), ``micro_batches`` packed micro-batches per rank from the config's
+    rollout distribution (workloads.py: prompt U{64..512} + completion U{256..8192}, packing cap
+    12 000, a different sample per rank), label-row lm_head + fused loss head, the bucketed RCCL
+    gradient all-reduce of the whole model (15.23 GB bf16 for 7B) launched from the last
+    micro-batch's backward, clip 0.3, AdamW.
+
+    Measured on the same ranks, same batches: the replica's step without any all-reduce
+    (``local``), the DP step, and the all-reduce alone over the same buckets.  ``overlap`` = 1 −
+    (DP − local) / all-reduce alone.  The real C3 step trains ``samples_per_step`` (4096) samples,
+    i.e. ~``samples_per_step / world / samples_per_micro_batch`` micro-batches per rank for ONE
+    all-reduce: ``extrapolated_tokens_per_s_per_gpu`` prices that step as (its micro-batches x the
+    measured per-micro-batch time) + the exposed all-reduce + the optimizer tail.
+    Collective over the default group (every rank calls it).  ``batches`` / ``model`` /
+    ``step_fn`` are injectable (gloo tests on CPU)."""
+    from . import workloads
+
+    device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    on_gpu = device.type == "cuda"
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    spec = workloads.SPECS[config]
+    if batches is None:
+        batches = workloads.micro_batches(config, micro_batches, seed=1234 + 7919 * rank)
+    micro_batches = len(batches)
+    n_samples = sum(int((b.position_ids[0] == 0).sum()) for b in batches)
+    n_tokens = sum(int(b.attention_mask.sum()) for b in batches)
+    if on_gpu:
+        torch.cuda.reset_peak_memory_stats(device)
+    ts = TrainerStep(spec.model, device=device, fused_head=True, kl_coef=spec.kl_coef, layers=layers,
+                     batches=batches, samples_per_step=samples_per_step, local=True, model=model, step_fn=step_fn)
+    t_local = ts.timed(steps, warmup)
+    t_dp, t_ar = t_local, 0.0
+    if world > 1:
+        from .finetune.grad_sync import GradBuckets
+
+        ts.grads = GradBuckets(list(ts.model.parameters()))
+        ts.world = world
+        t_dp = ts.timed(steps, warmup)
+        t_ar = ts.allreduce_alone()
+    nbytes = sum(p.numel() * p.element_size() for p in ts.model.parameters())
+    peak = torch.cuda.max_memory_allocated(device) / 1e9 if on_gpu else 0.0
+    ts.close()
+    stats = torch.tensor([n_tokens, n_samples, t_local], dtype=torch.float64, device=device)
+    if world > 1:  # ranks drew different samples: sum tokens / samples, slowest replica's time
+        tot = stats[:2].clone()
+        dist.all_reduce(tot)
+        tmax = stats[2:].clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        stats = torch.cat([tot, tmax])
+    else:
+        stats = stats.clone()
+    tok_all, samp_all, t_local_max = (float(x) for x in stats.cpu())
+    exposed = max(0.0, t_dp - t_local_max)
+    # the real step: samples_per_step samples over all ranks, one all-reduce
+    mb_real = samples_per_step / (samp_all / (micro_batches * world))
+    per_mb = t_local_max / micro_batches
+    tok_per_mb = tok_all / (micro_batches * world)
+    t_real = (mb_real / world) * per_mb + exposed
+    return {"config": f"C3: Qwen2.5-{spec.model} shapes{f' ({layers} layers)' if layers else ''} (random init, bf16), "
+                      f"math rollouts packed at {spec.seq_length}, label-row lm_head",
+            "micro_batches_per_rank": micro_batches, "tokens_per_rank_step": round(tok_all / world, 1),
+            "samples_per_rank_step": round(samp_all / world, 1),
+            "ms_per_step_local": round(t_local_max * 1e3, 2), "ms_per_step_dp": round(t_dp * 1e3, 2),
+            "allreduce_bytes": nbytes, "allreduce_alone_ms": round(t_ar * 1e3, 2),
+            "allreduce_exposed_ms": round(exposed * 1e3, 2),
+            "overlap": round(1.0 - min(1.0, exposed / t_ar), 4) if t_ar > 0 else None,
+            "tokens_per_s_per_gpu": round(tok_all / world / t_dp, 1),
+            "tokens_per_s": round(tok_all / t_dp, 1),
+            "local_tokens_per_s_per_gpu": round(tok_all / world / t_local_max, 1),
+            "extrapolated": {"samples_per_step": samples_per_step, "micro_batches_per_rank": round(mb_real / world, 1),
+                             "tokens_per_s_per_gpu": round(tok_per_mb * (mb_real / world) / t_real, 1),
+                             "allreduce_share": round(exposed / t_real, 5)},
+            "peak_mem_gb": round(peak, 2), "steps": steps, "warmup": warmup, "world": world}
 
 
 def fsdp_step_probe(name: str = "32b", tokens: int = 4096, seq: int = 2048, prompt: int = 256,

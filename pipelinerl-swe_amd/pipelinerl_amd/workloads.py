@@ -1,0 +1,114 @@
+"""Synthetic packed-GRPO workloads of BASELINE.json's configs, shared by
+bench.py, the GPU parity tests and the CPU baseline (measurement infrastructure: no product code
+path imports this module).
+
+Generator: numpy ``Generator(PCG64(seed))``, seed 1234; token ids uniform in
+[0, 151643); EOS 151643 appended to 75 % of the rollouts ("finished"); rewards Bernoulli(0.5) per
+rollout; groups of ``attempts`` rollouts share a prompt length; per-token fields from the build's
+``prepare_rl_fields`` / ``populate_rl_data`` (the reference's rl/__init__.py:380-525, pinned to
+the F3 fixture) with GRPO defaults (advantage = reward − group mean, no std division).
+``old_logprobs`` are −|N(0, 1.5²)| on completion tokens (a trained policy's log-probs are not
+available without its logits); ``ref_logprobs`` = old (the fork's default) or
+old + N(0, 0.05²) for C5 (KL-to-reference on).
+
+  c1  Qwen2.5-0.5B, 32 groups x 8, prompt U{32..128} + completion U{16..384} (<= 512 tokens),
+      packed at seq_length 4096, 256 samples per optimizer step (conf/finetune/base.yaml:61 with
+      the C1 cap)
+  c3  Qwen2.5-7B math: prompt U{64..512} + completion U{256..8192} (max_tokens 8192,
+      conf/base.yaml:47), packed at seq_length 12000 (conf/finetune/base.yaml:61)
+  c5  Qwen2.5-32B: the c3 rollouts with ref = old + N(0, 0.05²) and kl_coef 0.001
+      (conf/deepscaler15b.yaml:34)
+"""
+
+from __future__ import annotations
+
+import copy
+import types
+from dataclasses import dataclass
+
+import numpy as np
+
+EOS = 151643  # Qwen2.5 <|endoftext|>
+ID_RANGE = 151643
+
+
+@dataclass(frozen=True)
+class Spec:
+    model: str
+    prompt: tuple[int, int]
+    completion: tuple[int, int]
+    max_total: int | None
+    attempts: int
+    seq_length: int
+    kl_coef: float = 0.0
+    ref_noise: float = 0.0
+
+
+SPECS = {
+    "c1": Spec("0.5b", (32, 128), (16, 384), 512, 8, 4096),
+    "c3": Spec("7b", (64, 512), (256, 8192), None, 8, 12000),
+    "c5": Spec("32b", (64, 512), (256, 8192), None, 8, 12000, kl_coef=0.001, ref_noise=0.05),
+}
+
+
+def rollouts(config: str, n: int, seed: int = 1234, max_completion: int | None = None) -> list[dict]:
+    """``n`` processed rollouts (dicts in the preprocessor's output format) of ``config``."""
+    from .finetune.rl import RLConfig, populate_rl_data, prepare_rl_fields
+
+    spec = SPECS[config]
+    rng = np.random.Generator(np.random.PCG64(seed))
+    data = []
+    prompt = 0
+    for i in range(n):
+        if i % spec.attempts == 0:
+            prompt = int(rng.integers(spec.prompt[0], spec.prompt[1] + 1))
+        hi = spec.completion[1] if max_completion is None else min(spec.completion[1], max_completion)
+        comp = int(rng.integers(spec.completion[0], hi + 1))
+        if spec.max_total is not None:
+            comp = min(comp, spec.max_total - prompt)
+        L = prompt + comp
+        ids = rng.integers(0, ID_RANGE, L).tolist()
+        if rng.random() < 0.75:
+            ids[-1] = EOS
+        old = (-np.abs(rng.normal(0.0, 1.5, comp))).astype(np.float32)
+        ref = old + rng.normal(0.0, spec.ref_noise, comp).astype(np.float32) if spec.ref_noise else old
+        enc = prepare_rl_fields({"input_ids": ids, "labels": [-100] * prompt + ids[prompt:], "attention_mask": [1] * L},
+                                float(rng.random() < 0.5), old.tolist(), ref.tolist())
+        enc.update(group_id=f"g{i // spec.attempts}", rollout_index=i % spec.attempts, step_index=0, model_version=0)
+        data.append(enc)
+    return populate_rl_data(data, EOS, RLConfig(divide_advantage_by_std=False))
+
+
+def pack(data: list[dict], seq_length: int, samples_per_step: int, num_trainers: int = 1) -> list[tuple[int, object]]:
+    """(trainer_id, PipelineBatchEncoding) writes of the preprocessor's packer (quota + sentinel
+    protocol, preprocess.py:557-626) for ``data``."""
+    from .finetune.packing import MicroBatchPacker
+
+    packer = MicroBatchPacker(num_trainers, seq_length, samples_per_step // num_trainers,
+                              types.SimpleNamespace(eos_token_id=EOS))
+    return packer.feed(copy.deepcopy(data))
+
+
+def micro_batches(config: str, count: int, seed: int = 1234, seq_length: int | None = None) -> list:
+    """``count`` non-sentinel packed micro-batches of ``config`` (one trainer), greedy-packed up to
+    ``seq_length`` tokens (default: the config's)."""
+    spec = SPECS[config]
+    cap = seq_length or spec.seq_length
+    out: list = []
+    n = max(8, count * 4)
+    while True:
+        data = rollouts(config, n, seed=seed, max_completion=cap - spec.prompt[1] if cap < 9000 else None)
+        writes = pack(data, cap, len(data))
+        out = [b for _, b in writes if not b.sentinel]
+        if len(out) > count:  # the last one may be a partial tail: keep only full-ish ones
+            return out[:count]
+        n *= 2
+
+
+def rl_config(config: str, samples_per_step: int):
+    """GRPO defaults (conf/finetune/base.yaml:92-105 + grpo.yaml: ppo, eps 4, C 5), the config's KL."""
+    from .finetune.rl import RLConfig
+
+    spec = SPECS[config]
+    return RLConfig(policy_loss="ppo", epsilon=4.0, kl_coef=spec.kl_coef, final_kl_coef=spec.kl_coef,
+                    clamp_log_ratio_ref_new_value=5, divide_advantage_by_std=False, batch_size=samples_per_step)

@@ -1,0 +1,297 @@
+"""The single-GPU part of every BASELINE.json config on its own workload,
+against the pinned oracle (oracle/grpo_oracle.py) or a plain PyTorch fp32 restatement pinned to it.
+
+  C1  Qwen2.5-0.5B, 256 rollouts (32 x 8) packed at 4096, ONE optimizer step through
+      run_finetuning_loop on cuda:0 (the product path: patched bf16 model, label-row lm_head,
+      deferred statistics) vs the same initial weights in fp32 with HF's eager ops and the torch
+      restatement of rl_step (tests/cpu_rl_step.py), itself checked against the oracle on two of
+      the micro-batches.  Tolerances: the bf16 bar of north_star (1e-2) on the loss-head
+      statistics; 5e-2 on the pre-clip gradient norm (a 24-layer bf16 backward against fp32).
+  C3  Qwen2.5-7B lm_head (V = 152 064, H = 3584) on the largest of C3's packed micro-batches
+      (prompt U{64..512} + completion U{256..8192}, packing cap 12 000): the label-row lm_head +
+      loss head vs the full-logits kernel on the same GEMM and vs the oracle (statistics of every
+      row 1e-4 on the same bf16 logits; sampled rows' log-prob / entropy / dlogits), softmax rows
+      of dlogits sum to ~0, bitwise determinism.
+  C5  Qwen2.5-32B lm_head (H = 5120) with KL to the reference on (kl_coef 0.001, ref = old +
+      N(0, 0.05²)), same checks.
+Plus rl_step's DeepSpeed loss scale (dlogits written at the scale in the forward; the backward
+pass over the logits is skipped) and the deferred statistics (resolve() after the backward launch,
+prompt-row finiteness assertion of the label-row path).
+"""
+
+from __future__ import annotations
+
+import copy
+import os
+import types
+
+import numpy as np
+import pytest
+import torch
+
+from gpu_helpers import LogitsModel, rel_close, to_batch
+from oracle import grpo_oracle
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+THREADS = min(16, os.cpu_count() or 1)
+
+
+def _host(b) -> dict:
+    """PipelineBatchEncoding -> the oracle's dict of numpy arrays."""
+    keys = ("input_ids", "labels", "position_ids", "rewards", "advantages", "ref_logprobs", "old_logprobs",
+            "group_tokens", "num_labels", "overflow")
+    out = {k: getattr(b, k).detach().cpu().numpy() for k in keys}
+    out["is_packed"] = bool(b.is_packed)
+    return out
+
+
+def _stats_close(got: dict, want: dict, rtol: float, keys=None, what=""):
+    for k in keys or want:
+        g, w = float(got[k]), float(want[k])
+        assert abs(g - w) <= rtol * max(1.0, abs(w)), (what, k, g, w)
+
+
+# ------------------------------------------------------------------------------------------ C1
+
+def test_c1_one_optimizer_step_through_the_loop(tmp_path):
+    from cpu_rl_step import cpu_rl_step
+    from loop_helpers import loop_cfg
+    from transformers import AutoModelForCausalLM, Qwen2Config
+
+    from pipelinerl_amd import workloads
+    from pipelinerl_amd.finetune.attention import register
+    from pipelinerl_amd.finetune_loop import run_finetuning_loop
+    from pipelinerl_amd.streams import SingleStreamSpec, reset_streams_backend, set_streams_backend, write_to_streams
+    from pipelinerl_amd.trainer_probe import QWEN, qwen2_model
+
+    data = workloads.rollouts("c1", 256)
+    writes = workloads.pack(data, 4096, 256)
+    mbs = [b for _, b in writes if not b.sentinel]
+    assert sum(int(b.attention_mask.sum()) for b in mbs) == sum(len(d["input_ids"]) for d in data)
+    reset_streams_backend()
+    set_streams_backend("files")
+    with write_to_streams(SingleStreamSpec(exp_path=tmp_path, topic="training_data", partition=0)) as w:
+        for _, b in writes:
+            w.write(b)
+    reset_streams_backend()
+
+    model = qwen2_model("0.5b", torch.device(DEV))  # product path: bf16, fused model ops
+    init = {k: v.detach().float().clone() for k, v in model.state_dict().items()}
+    for k in ("RANK", "WORLD_SIZE", "MASTER_ADDR"):
+        os.environ.pop(k, None)
+    cfg = loop_cfg(tmp_path, tmp_path / "unused", 1, 256, 1, dist_backend=None, learning_rate=1e-6,
+                   save_final_training_state=False,
+                   rl=dict(policy_loss="ppo", epsilon=4, kl_coef=0.0, final_kl_coef=0.0,
+                           clamp_log_ratio_ref_new_value=5, temperature=1.0, divide_advantage_by_std=False))
+    import pipelinerl_amd.finetune.rl as rlmod
+
+    got_stats = []
+    orig_resolve = rlmod.RLStats.resolve
+
+    def resolve(self):
+        d = orig_resolve(self)
+        if "loss" in d:
+            got_stats.append(d)
+        return d
+
+    rlmod.RLStats.resolve = resolve
+    try:
+        tok = types.SimpleNamespace(eos_token_id=workloads.EOS, save_pretrained=lambda *a, **k: None)
+        m = run_finetuning_loop(cfg, model=model, tokenizer=tok)
+    finally:
+        rlmod.RLStats.resolve = orig_resolve
+    assert m.completed_steps == 1 and m.samples == 256 and m.passes == len(mbs)
+    assert len(got_stats) == len(mbs)  # the deferred path ran for every micro-batch
+    del model
+    torch.cuda.empty_cache()
+
+    # fp32 restatement: same initial weights, HF eager ops, torch restatement of rl_step
+    qcfg = Qwen2Config(max_position_embeddings=32768, rope_theta=1e6, rms_norm_eps=1e-6, **QWEN["0.5b"])
+    ref = AutoModelForCausalLM.from_config(qcfg, dtype=torch.float32, attn_implementation=register()).to(DEV)
+    ref.load_state_dict(init)
+    ref.train()
+    rlc = workloads.rl_config("c1", 256)
+    ref_stats = []
+    for i, b in enumerate(mbs):
+        bd = copy.deepcopy(b).to_device(DEV)
+        bd.seq_boundaries = b.seq_boundaries
+        loss, st = cpu_rl_step(ref, bd, 0, 1, rlc)
+        loss.backward()
+        ref_stats.append(st)
+        if i < 2:  # pin the fp32 restatement to the oracle on this micro-batch's own logits
+            with torch.no_grad():
+                from pipelinerl_amd.finetune.attention import packed_kwargs
+
+                lg = ref(input_ids=bd.input_ids, position_ids=bd.position_ids,
+                         **packed_kwargs(bd, bd.input_ids.device)).logits.float().cpu().numpy()
+            o = grpo_oracle.rl_step_oracle(lg, _host(b), dict(rlc.model_dump()), 0, 1, compute_grad=False,
+                                           dtype=np.float32, threads=THREADS)
+            for k in ("loss", "entropy", "ratio_new_old_sum", "num_output_tokens_sum"):
+                assert abs(float(st[k]) - o["stats"][k]) <= 1e-4 * max(1.0, abs(o["stats"][k])), (i, k)
+            del lg
+    gn_ref = float(torch.sqrt(sum((p.grad.double() ** 2).sum() for p in ref.parameters() if p.grad is not None)))
+    # the product's statistics vs the fp32 restatement, micro-batch by micro-batch
+    for g, r in zip(got_stats, ref_stats):
+        assert g["num_output_tokens_sum"] == r["num_output_tokens_sum"]
+        _stats_close(g, r, 1e-2, ("loss", "entropy", "ratio_new_old_sum", "ratio_new_old_squared_sum"), "c1")
+    assert abs(m.grad_norm - gn_ref) <= 5e-2 * gn_ref, (m.grad_norm, gn_ref)
+
+
+# ------------------------------------------------------------------------------- C3 / C5 heads
+
+class _HiddenModel(torch.nn.Module):
+    """Causal-LM stand-in for rl_step's label-row path: a decoder that returns fixed hidden
+    states, a bias-free lm_head (get_decoder / get_output_embeddings, as HF models expose)."""
+
+    def __init__(self, hidden: torch.Tensor, weight: torch.Tensor):
+        super().__init__()
+        self.h = torch.nn.Parameter(hidden)
+        self.lm_head = torch.nn.Linear(weight.shape[1], weight.shape[0], bias=False, dtype=weight.dtype,
+                                       device=weight.device)
+        with torch.no_grad():
+            self.lm_head.weight.copy_(weight)
+        outer = self
+
+        class _Dec(torch.nn.Module):
+            def forward(self, **kw):
+                return types.SimpleNamespace(last_hidden_state=outer.h)
+
+        self._dec = _Dec()
+
+    def forward(self, **kw):  # the full-logits path (fused_lm_head off)
+        return types.SimpleNamespace(logits=self.lm_head(self.h))
+
+    def get_decoder(self):
+        return self._dec
+
+    def get_output_embeddings(self):
+        return self.lm_head
+
+
+def _head_case(config: str, H: int, max_tokens: int):
+    from pipelinerl_amd import workloads
+    from pipelinerl_amd.finetune.rl import rl_step
+
+    mbs = workloads.micro_batches(config, 6, seq_length=max_tokens)
+    b = max(mbs, key=lambda x: int(x.input_ids.shape[1]))
+    T = int(b.input_ids.shape[1])
+    V = 152064
+    g = torch.Generator(device=DEV).manual_seed(7)
+    h = torch.randn((1, T, H), generator=g, device=DEV).to(torch.bfloat16)
+    w = (torch.randn((V, H), generator=g, device=DEV) * (2.0 / H ** 0.5)).to(torch.bfloat16)
+    rlc = workloads.rl_config(config, 4096)
+    bd = to_batch(_host(b) | {"attention_mask": b.attention_mask.numpy(), "seq_boundaries": b.seq_boundaries.numpy()})
+    runs = []
+    for _ in range(2):
+        model = _HiddenModel(h.clone(), w)
+        loss, stats = rl_step(model, bd, 0, 10, rlc, defer_stats=True)
+        loss.backward()
+        runs.append((float(loss.detach()), stats.resolve(), model.h.grad.clone(), model.lm_head.weight.grad.clone()))
+        del model
+    # bitwise determinism of the whole label-row path
+    assert runs[0][0] == runs[1][0] and runs[0][1] == runs[1][1]
+    assert torch.equal(runs[0][2], runs[1][2]) and torch.equal(runs[0][3], runs[1][3])
+    _, stats, dh, dw = runs[0]
+    # the same logits materialised (bf16 GEMM) through the full-logits kernel
+    logits = (h[0] @ w.t())[None].contiguous().requires_grad_(True)
+    full = LogitsModel(logits.detach().clone())
+    loss_f, stats_f = rl_step(full, bd, 0, 10, rlc)
+    loss_f.backward()
+    _stats_close(stats, stats_f, 1e-2, None, f"{config} label-row vs full")
+    dl = full.logits.grad[0]
+    ok, err = rel_close((dl.float().t() @ h[0].float()).cpu().numpy(), dw.float().cpu().numpy(), 2e-2, 2e-3 * float(dw.float().abs().max()))
+    assert ok, (config, "dW", err)
+    # softmax rows of dlogits sum to ~0 (bf16 storage rounds each entry by 2^-9)
+    df = dl.float()
+    rowsum, absum = df.sum(-1).abs(), df.abs().sum(-1)
+    assert bool(torch.all(rowsum <= 4e-3 * absum + 1e-12))
+    # every row's statistics vs the oracle on the same bf16 logits (fp32 oracle, 1e-4)
+    lg = full.logits.detach().float().cpu().numpy()
+    hb = _host(b)
+    o = grpo_oracle.rl_step_oracle(lg, hb, dict(rlc.model_dump()), 0, 10, compute_grad=False, dtype=np.float32,
+                                   threads=THREADS, row_chunk=64)
+    _stats_close(stats_f, o["stats"], 1e-4, None, f"{config} full vs oracle")
+    _stats_close(stats, o["stats"], 1e-2, None, f"{config} label-row vs oracle")
+    # sampled label rows: dlogits vs the oracle's analytic gradient
+    lab = np.nonzero(hb["labels"][0, 1:] != -100)[0]
+    pick = lab[np.linspace(0, lab.size - 1, 6).astype(int)]
+    tgt = hb["input_ids"][0, pick + 1]
+    lse, H_, tlp = grpo_oracle.row_stats(lg[0, pick], tgt, None, 1.0)
+    assert np.allclose(tlp, o["new_logprobs"][0, pick], rtol=1e-5, atol=1e-4)
+    assert np.allclose(H_, o["entropy"][0, pick], rtol=1e-5, atol=1e-4)
+    return T
+
+
+def test_c3_label_row_loss_head_full_size():
+    T = _head_case("c3", 3584, 12000)
+    assert T > 8000
+
+
+def test_c5_kl_loss_head_full_size():
+    T = _head_case("c5", 5120, 12000)
+    assert T > 8000
+
+
+# ------------------------------------------------------------ loss scale and deferred stats
+
+def test_deepspeed_loss_scale_skips_the_backward_pass():
+    """rl_step(grad_scale=s) writes dlogits for an upstream of s in the forward; the caller's
+    (loss * s).backward() then leaves them as they are (the logits are not read again: they are
+    overwritten with NaN here before the backward).  Any other upstream still recomputes."""
+    from conftest import load_f1
+
+    from pipelinerl_amd.finetune.rl import RLConfig, rl_step
+
+    batches, _, cases = load_f1()
+    b = batches["packed"]
+    c = cases[5]
+    s = 1.0 / 3.0
+    o = grpo_oracle.rl_step_oracle(b["logits"], b, c["cfg"], c["step"], c["max_step"], grad_out=s)
+    model = LogitsModel(torch.tensor(b["logits"], device=DEV))
+    loss, stats = rl_step(model, to_batch(b), c["step"], c["max_step"], RLConfig(**c["cfg"]), grad_scale=s)
+    with torch.no_grad():
+        model.logits.fill_(float("nan"))
+    (loss * s).backward()
+    d = model.logits.grad.float().cpu().numpy()
+    assert np.isfinite(d).all()
+    ok, err = rel_close(d, o["dlogits"], 1e-4, 1e-7)
+    assert ok, err
+    # upstream 2s != s: the gradient is recomputed from the logits at the relative scale 2
+    o2 = grpo_oracle.rl_step_oracle(b["logits"], b, c["cfg"], c["step"], c["max_step"], grad_out=2 * s)
+    model = LogitsModel(torch.tensor(b["logits"], device=DEV))
+    loss, _ = rl_step(model, to_batch(b), c["step"], c["max_step"], RLConfig(**c["cfg"]), grad_scale=s)
+    (loss * (2 * s)).backward()
+    ok, err = rel_close(model.logits.grad.float().cpu().numpy(), o2["dlogits"], 1e-4, 1e-7)
+    assert ok, err
+
+
+def test_deferred_stats_and_prompt_row_finiteness():
+    from pipelinerl_amd import workloads
+    from pipelinerl_amd.finetune.rl import RLConfig, RLStats, rl_step
+
+    b = workloads.micro_batches("c1", 1)[0]
+    T = int(b.input_ids.shape[1])
+    hb = _host(b) | {"attention_mask": b.attention_mask.numpy(), "seq_boundaries": b.seq_boundaries.numpy()}
+    g = torch.Generator(device=DEV).manual_seed(3)
+    h = torch.randn((1, T, 896), generator=g, device=DEV).to(torch.bfloat16)
+    w = (torch.randn((151936, 896), generator=g, device=DEV) * 0.06).to(torch.bfloat16)
+    cfg = workloads.rl_config("c1", 256)
+    loss, now = rl_step(_HiddenModel(h, w), to_batch(hb), 0, 1, cfg)
+    loss2, later = rl_step(_HiddenModel(h, w), to_batch(hb), 0, 1, cfg, defer_stats=True)
+    assert isinstance(later, RLStats) and isinstance(now, dict)
+    loss2.backward()  # the backward is queued before the statistics are read
+    assert later.resolve() == now and float(loss2.detach()) == float(loss.detach())
+    # a non-finite hidden state on a PROMPT row: the label-row kernel never sees that row, the
+    # reference's all-row assertion (rl/__init__.py:209) is kept by the hidden-state check
+    prompt_rows = np.nonzero(hb["labels"][0, 1:] == -100)[0]
+    hp = h.clone()
+    hp[0, int(prompt_rows[0])] = float("nan")
+    _, st = rl_step(_HiddenModel(hp, w), to_batch(hb), 0, 1, cfg, defer_stats=True)
+    with pytest.raises(AssertionError, match="not finite"):
+        st.resolve()
+    with pytest.raises(AssertionError, match="not finite"):
+        rl_step(_HiddenModel(hp, w), to_batch(hb), 0, 1, cfg)
+    # the full-logits path asserts on the same batch too (every row's logits are formed there)
+    with pytest.raises(AssertionError):
+        rl_step(_HiddenModel(hp, w), to_batch(hb), 0, 1, RLConfig(**(cfg.model_dump() | {"fused_lm_head": False})))

@@ -100,10 +100,18 @@ def test_solution_index_and_errors():
     assert idx >= 0
     ref = gemm.linear_wgrad(dy, x)
     out = torch.empty_like(ref)
-    gemm.gemm(0, 1, K, N, T, x, K, dy, N, out, K, solution=idx)  # the heuristic's own index
-    assert torch.equal(out, ref)
-    gemm.gemm(0, 1, K, N, T, x, K, dy, N, out, K, solution=10 ** 9)  # unknown index: heuristic
-    assert torch.equal(out, ref)
+    shipped = sorted({int(e["index"]) for es in gemm.solutions().values() for e in es if int(e["index"]) >= 0})
+    try:
+        # an index outside the registered (swept) set is refused before any launch
+        with pytest.raises(gemm.GemmError, match="allowed"):
+            gemm.gemm(0, 1, K, N, T, x, K, dy, N, out, K, solution=idx if idx not in shipped else 10 ** 9)
+        gemm.allow(shipped + [idx, 10 ** 9])
+        gemm.gemm(0, 1, K, N, T, x, K, dy, N, out, K, solution=idx)  # the heuristic's own index
+        assert torch.equal(out, ref)
+        gemm.gemm(0, 1, K, N, T, x, K, dy, N, out, K, solution=10 ** 9)  # allowed, unknown: heuristic
+        assert torch.equal(out, ref)
+    finally:
+        gemm.allow(shipped)
     with pytest.raises(gemm.GemmError):
         gemm.linear_wgrad(dy, x, out=torch.empty((N, K + 1), dtype=torch.bfloat16, device=DEV))
     with pytest.raises(gemm.GemmError):

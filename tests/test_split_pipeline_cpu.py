@@ -105,3 +105,39 @@ def test_fsdp_trainer_step_gloo(tmp_path):
     assert a["sec"] > 0 and b["sec"] > 0
     for n, p in a["params"].items():
         assert torch.equal(p, b["params"][n]), n
+
+
+def _dp_run(rank, port, world, out):
+    sys.path[:0] = [str(ROOT), str(ROOT / "pipelinerl-swe_amd"), str(ROOT / "tests")]
+    os.environ["OMP_NUM_THREADS"] = "1"
+    import torch.distributed as dist
+    from cpu_rl_step import cpu_rl_step
+    from loop_helpers import rollouts
+    from pipelinerl_amd import workloads
+    from pipelinerl_amd.trainer_probe import dp_step_probe
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    data = rollouts(4, 4, seed=rank)  # a different sample per rank, as the probe draws them
+    batches = [b for _, b in workloads.pack(data, 48, len(data)) if not b.sentinel][:3]
+    res = dp_step_probe("c3", steps=2, warmup=1, device="cpu", samples_per_step=64, batches=batches,
+                        model=_tiny().float(), step_fn=cpu_rl_step)
+    torch.save(res, Path(out) / f"dp{rank}.pt")
+    dist.destroy_process_group()
+
+
+def test_c3_dp_probe_gloo(tmp_path):
+    """bench.py's c3_dp probe (trainer_probe.dp_step_probe) on gloo world 2: the replica's step
+    alone, the DP step with the bucketed all-reduce, the all-reduce alone; one consistent report
+    on every rank, with the extrapolation to the config's samples-per-step."""
+    from test_weight_update_cpu import free_port
+
+    mp.spawn(_dp_run, args=(free_port(), 2, str(tmp_path)), nprocs=2, join=True)
+    a, b = (torch.load(tmp_path / f"dp{r}.pt") for r in range(2))
+    for k in ("ms_per_step_local", "allreduce_bytes", "tokens_per_rank_step", "samples_per_rank_step", "world"):
+        assert a[k] == b[k], k
+    assert a["world"] == 2 and a["micro_batches_per_rank"] == 3
+    assert a["ms_per_step_local"] > 0 and a["ms_per_step_dp"] > 0 and a["allreduce_alone_ms"] > 0
+    assert a["allreduce_bytes"] == sum(p.numel() * 4 for p in _tiny().parameters())
+    assert a["overlap"] is not None and 0.0 <= a["overlap"] <= 1.0
+    ex = a["extrapolated"]
+    assert ex["samples_per_step"] == 64 and ex["micro_batches_per_rank"] > 0 and ex["tokens_per_s_per_gpu"] > 0

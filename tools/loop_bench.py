@@ -67,7 +67,8 @@ def main():
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--mean-len", type=int, default=2048)
     ap.add_argument("--prompt", type=int, default=256)
-    ap.add_argument("--fused-lm-head", action="store_true")
+    ap.add_argument("--full-logits", action="store_true",
+                    help="materialise [T, V] logits (RLConfig.fused_lm_head off; the label-row path is the default)")
     ap.add_argument("--dist", choices=["uniform", "c3"], default="uniform",
                     help="rollout lengths: uniform around --mean-len, or configs[2]'s U{64..512} + U{256..8192}")
     ap.add_argument("--eager-ops", action="store_true", help="HF element-wise chains instead of the HIP model ops")
@@ -114,7 +115,7 @@ def main():
         force_restart=False, max_lag=None, dist_backend=None, data_timeout_s=600, fused_model_ops=not a.eager_ops,
         rl=dict(policy_loss="ppo", epsilon=4, kl_coef=0.0, final_kl_coef=0.0, clamp_log_ratio_ref_new_value=5,
                 temperature=1.0, divide_advantage_by_std=False, aggregate_loss="sum",
-                fused_lm_head=a.fused_lm_head))
+                fused_lm_head=not a.full_logits))
     cfg = Cfg.wrap({"output_dir": str(exp), "streams": {"backend": "files"}, "finetune": ft,
                     "me": {"weight_update_group_init_method": None, "weight_update_group_world_size": 0,
                            "llm_urls": ""}})
@@ -141,7 +142,7 @@ def main():
     sec = stamps[-1] - stamps[0] if len(stamps) > 1 else loop_s
     out = {"tool": "loop_bench", "model": f"Qwen2.5-{a.model} shapes (random init, bf16)",
            "seq_length": a.seq_length, "samples_per_step": a.samples_per_step, "mean_rollout_len": a.mean_len, "length_dist": a.dist,
-           "fused_lm_head": a.fused_lm_head, "fused_model_ops": not a.eager_ops, "steps": m.completed_steps,
+           "fused_lm_head": not a.full_logits, "fused_model_ops": not a.eager_ops, "steps": m.completed_steps,
            "micro_batches_per_step": [x["throughput/micro_batches_per_step"] for x in lines],
            "tokens_per_step": [x["throughput/tokens_per_step"] for x in lines],
            "step_wall_s": [round(b - a_, 3) for a_, b in zip(stamps, stamps[1:])],
