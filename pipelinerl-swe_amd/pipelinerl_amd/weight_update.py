@@ -139,6 +139,13 @@ class HipFlatPacker:
         _native.check(lib.prl_unflatten_bf16(flat.data_ptr(), P, D, N, O, len(tensors), st), "prl_unflatten_bf16")
 
 
+def parameters_info(named: list[tuple[str, torch.Tensor]]) -> list[ParameterInfo]:
+    """The request's parameter list (finetune_loop.py:192-196): one entry per named parameter, in
+    order, full shape (a sharded parameter reports its global shape, as ZeRO-3's ds_shape does),
+    dtype always bf16 (what is broadcast)."""
+    return [ParameterInfo(name=n, shape=list(p.shape), dtype=str(torch.bfloat16)) for n, p in named]
+
+
 def unwrap_model(model):
     m = getattr(model, "module", model)
     return getattr(m, "pretrained_model", m)  # value-head wrapper: broadcast the LM only
@@ -222,7 +229,7 @@ class WeightUpdateManager:
         sharded = _is_sharded(named)
         if not self.is_main and not sharded:
             return
-        infos = [ParameterInfo(name=n, shape=list(p.shape), dtype=str(torch.bfloat16)) for n, p in named]
+        infos = parameters_info(named)
         layout = FlatLayout.from_infos(infos)
         dev = named[0][1].device
         if sharded:

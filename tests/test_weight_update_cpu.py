@@ -202,3 +202,54 @@ def test_failed_actor_makes_the_trainer_raise(tmp_path, mode):
         assert "500" in r["error"] and r["elapsed"] < 3.0
     else:
         assert "not completed" in r["error"] and 2.5 < r["elapsed"] < 10.0
+
+
+def test_f4_request_and_actor_group_layout():
+    """F4 (tests/golden/make_f4.py): the request the reference trainer builds for a 0.5B-shaped
+    model (finetune_loop.py:178-199, 290 entries in named_parameters order) and the actor-group
+    layout of the reference's world map (world.py:133-184, vllm1.py:62).  The build's request and
+    its actors' group ranks must be the same."""
+    from conftest import GOLDEN
+    from transformers import Qwen2Config, Qwen2ForCausalLM
+
+    sys.path[:0] = [str(ROOT / "pipelinerl-swe_amd")]
+    from pipelinerl_amd import actor as actor_mod
+    from pipelinerl_amd.weight_update import FlatLayout, WeightUpdateRequest, parameters_info, unwrap_model
+
+    f4 = json.loads((GOLDEN / "f4_weight_update.json").read_text())
+    cfg = Qwen2Config(hidden_size=896, intermediate_size=4864, num_hidden_layers=24, num_attention_heads=14,
+                      num_key_value_heads=2, vocab_size=151936, tie_word_embeddings=True)
+    with torch.device("meta"):
+        model = Qwen2ForCausalLM(cfg)
+    ours = [i.model_dump() for i in parameters_info(list(unwrap_model(model).named_parameters()))]
+    assert ours == f4["request"]["parameters_info"] and len(ours) == f4["num_parameters"] == 290
+    # the reference's message parses into ours (the extension fields default to the compat mode)
+    req = WeightUpdateRequest(**f4["request"])
+    assert req.transport == "per_tensor" and req.version == 4096
+    dumped = req.model_dump()
+    assert {k: dumped[k] for k in ("kind", "version", "parameters_info")} == \
+        {k: f4["request"][k] for k in ("kind", "version", "parameters_info")}
+    layout = FlatLayout.from_infos(req.parameters_info)
+    assert sum(layout.numels) == f4["numel"] and all(o % 8 == 0 for o in layout.offsets)
+    # actor group ranks: every worker of every actor LLM gets the reference's pg_rank, and the
+    # ranks 1..size-1 of the reference's weight_update_group_size are covered exactly once
+    seen = []
+
+    def fake_group(**kw):
+        seen.append((kw["rank"], kw["world_size"]))
+        return object()
+
+    orig = actor_mod.torch_utils.init_extra_process_group
+    actor_mod.torch_utils.init_extra_process_group = fake_group
+    try:
+        for g in f4["groups"]:
+            seen.clear()
+            for idx, r, pg in g["actor_pg_ranks"]:
+                w = actor_mod.WorkerExtension()
+                w.rank = r
+                w.init_actor_update_group(idx, g["gpus_per_llm"], "tcp://127.0.0.1:1", g["weight_update_group_size"])
+                assert w.pg_rank == pg
+            assert sorted(x[0] for x in seen) == list(range(1, g["weight_update_group_size"]))
+            assert all(x[1] == g["weight_update_group_size"] for x in seen)
+    finally:
+        actor_mod.torch_utils.init_extra_process_group = orig
