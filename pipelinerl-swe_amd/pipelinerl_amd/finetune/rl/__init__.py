@@ -178,7 +178,7 @@ def rl_step(model, batch: PipelineBatchEncoding, current_step: int, max_step: in
     fields = prepare_fields(batch, logits.device)
     if fused_head:
         loss, stats_dev, _ = linear_grpo_loss(hidden, _lm_head_of(model, False).weight, fields, params,
-                                              config.lm_head_chunk_rows)
+                                              config.lm_head_chunk_rows, getattr(batch, "_label_rows", None))
     else:
         loss, stats_dev, _ = grpo_loss(logits, fields, params, values)
 

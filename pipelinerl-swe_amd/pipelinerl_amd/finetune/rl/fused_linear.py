@@ -59,7 +59,7 @@ def _c_batch(ptr: int, dtype: torch.dtype, B: int, L: int, V: int, ld: int, f: d
 
 class LinearGrpoLossFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, hidden, weight, fields, params: GrpoParams, chunk_rows: int):
+    def forward(ctx, hidden, weight, fields, params: GrpoParams, chunk_rows: int, label_rows=None):
         if hidden.device.type != "cuda":
             raise RuntimeError("the fused lm_head + GRPO loss runs on a HIP device only (no CPU fallback)")
         if hidden.dim() != 3 or weight.dim() != 2 or hidden.shape[-1] != weight.shape[1]:
@@ -83,8 +83,11 @@ class LinearGrpoLossFn(torch.autograd.Function):
         stream = torch.cuda.current_stream(dev).cuda_stream
         cp = params.to_c(write_grad)
         if Q > 0:
-            mask = (fields["labels"][:, 1:] != -100).reshape(-1)
-            qsel = torch.nonzero(mask).reshape(-1)  # one host sync: the GEMM shapes need the count
+            if label_rows is not None and label_rows.device == dev:  # counted on the host by the loader
+                qsel = label_rows
+            else:
+                mask = (fields["labels"][:, 1:] != -100).reshape(-1)
+                qsel = torch.nonzero(mask).reshape(-1)  # one host sync: the GEMM shapes need the count
             hrow = qsel + torch.div(qsel, L - 1, rounding_mode="floor")  # q = b*(L-1)+t -> b*L+t
             R = int(qsel.numel())
             step = max(1, int(chunk_rows))
@@ -143,11 +146,14 @@ class LinearGrpoLossFn(torch.autograd.Function):
             if ctx.needs_input_grad[1]:
                 d_weight = (ctx.dw.float() * g).to(ctx.w_dtype)  # g applied in fp32 (not rounded to bf16)
         ctx.dh = ctx.dw = None
-        return d_hidden, d_weight, None, None, None
+        return d_hidden, d_weight, None, None, None, None
 
 
 def linear_grpo_loss(hidden: torch.Tensor, weight: torch.Tensor, fields: dict, params: GrpoParams,
-                     chunk_rows: int = 65536):
+                     chunk_rows: int = 65536, label_rows: torch.Tensor | None = None):
     """(loss, stats [NSTAT] f64 device, rows [8, B*(L-1)]) of lm_head(hidden) -> GRPO loss head,
-    scoring only the label rows.  ``weight``: the lm_head weight [V, H] (no bias)."""
-    return LinearGrpoLossFn.apply(hidden, weight, fields, params, chunk_rows)
+    scoring only the label rows.  ``weight``: the lm_head weight [V, H] (no bias).
+    ``label_rows``: the rows q = b*(L-1)+t with a label (int64, on the device), if the caller
+    counted them on the host (the trainer's loader does); else they are found on the device and
+    their count read back."""
+    return LinearGrpoLossFn.apply(hidden, weight, fields, params, chunk_rows, label_rows)

@@ -13,7 +13,7 @@ from typing import Any, Union
 
 import numpy as np
 import torch
-from pydantic import BaseModel, ConfigDict, field_validator
+from pydantic import PrivateAttr, BaseModel, ConfigDict, field_validator
 
 LONG_FIELDS = ("input_ids", "attention_mask", "labels", "position_ids", "image_grid_thw")
 FLOAT_FIELDS = ("rewards", "advantages", "ref_logprobs", "old_logprobs", "group_tokens", "num_labels",
@@ -79,6 +79,10 @@ class PipelineBatchEncoding(BaseModel):
 
     pixel_values: torch.Tensor | None = None
     image_grid_thw: torch.Tensor | None = None
+    # build-only, not part of the stream format: the loss rows q = b*(L-1)+t whose label is not
+    # -100, computed on the host by the trainer's loader (the label-row lm_head needs their count
+    # on the host: without this it reads it back from the device, a sync per micro-batch)
+    _label_rows: torch.Tensor | None = PrivateAttr(default=None)
 
     @field_validator(*LONG_FIELDS, mode="before")
     @classmethod
@@ -100,7 +104,16 @@ class PipelineBatchEncoding(BaseModel):
             val = getattr(self, name)
             if isinstance(val, torch.Tensor):
                 setattr(self, name, val.to(device, non_blocking=non_blocking))
+        if self._label_rows is not None:
+            self._label_rows = self._label_rows.to(device, non_blocking=non_blocking)
         return self
+
+    def label_rows_from_host(self) -> torch.Tensor:
+        """Record (and return) the label rows of this batch from its host-side labels."""
+        lab = self.labels
+        rows = torch.nonzero((lab[:, 1:] != -100).reshape(-1)).reshape(-1)
+        self._label_rows = rows
+        return rows
 
     @classmethod
     def from_dict(cls, data: dict[str, Any], **defaults) -> "PipelineBatchEncoding":

@@ -116,10 +116,14 @@ def run_data_loader(data_stream: SingleStreamSpec, batch_queue: Queue, device: t
                 ntok = int(b.attention_mask.sum())
                 nseq = batch_sequence_count(b)
                 if device.type == "cuda":
+                    # the label-row lm_head's count, known on the host (PRL_HOST_LABEL_ROWS=0: A/B)
+                    rows = b.label_rows_from_host() if os.environ.get("PRL_HOST_LABEL_ROWS", "1") != "0" else None
                     for name in type(b).model_fields:
                         v = getattr(b, name)
                         if isinstance(v, torch.Tensor) and name != "seq_boundaries":  # host metadata
                             setattr(b, name, v.pin_memory().to(device, non_blocking=True))
+                    if rows is not None:
+                        b._label_rows = rows.pin_memory().to(device, non_blocking=True)
                 batch_queue.put((b, ntok, nseq))
         if stop is None or not stop.is_set():  # the reader went idle for `timeout` s: fail, not hang
             batch_queue.put(TimeoutError(f"no training data on {data_stream} for {timeout} s"))

@@ -282,6 +282,14 @@ def test_deferred_stats_and_prompt_row_finiteness():
     assert isinstance(later, RLStats) and isinstance(now, dict)
     loss2.backward()  # the backward is queued before the statistics are read
     assert later.resolve() == now and float(loss2.detach()) == float(loss.detach())
+    # label rows counted on the host (as the trainer's loader does): no device read-back, same result
+    bh = to_batch(hb, "cpu")
+    rows = bh.label_rows_from_host()
+    assert torch.equal(rows, torch.nonzero((bh.labels[:, 1:] != -100).reshape(-1)).reshape(-1))
+    bh.to_device(DEV)
+    assert bh._label_rows.device.type == "cuda"
+    loss3, st3 = rl_step(_HiddenModel(h, w), bh, 0, 1, cfg)
+    assert st3 == now and float(loss3.detach()) == float(loss.detach())
     # a non-finite hidden state on a PROMPT row: the label-row kernel never sees that row, the
     # reference's all-row assertion (rl/__init__.py:209) is kept by the hidden-state check
     prompt_rows = np.nonzero(hb["labels"][0, 1:] == -100)[0]

@@ -88,3 +88,21 @@ def test_pipeline_batch_encoding_roundtrip_and_slices():
     assert b2.rewards.dtype == torch.float32 and b2.seq_boundaries.dtype == torch.int32
     with pytest.raises(ValueError):
         b.make_slices(5)
+
+
+def test_label_rows_from_host_and_to_device():
+    """PipelineBatchEncoding.label_rows_from_host: the loss rows q = b*(L-1)+t with a label
+    (rl/__init__.py:152-153's mask, flattened), carried through to_device."""
+    import torch
+
+    from pipelinerl_amd.finetune.types import PipelineBatchEncoding
+
+    lab = torch.tensor([[-100, -100, 5, 6, -100, 7], [-100, 1, 2, -100, -100, -100]])
+    z = torch.zeros(2, 6)
+    b = PipelineBatchEncoding(input_ids=lab.clamp(min=0), attention_mask=torch.ones_like(lab), labels=lab,
+                              rewards=z, advantages=z, ref_logprobs=z, old_logprobs=z, group_tokens=z + 1,
+                              num_labels=z, overflow=z, model_version=0)
+    rows = b.label_rows_from_host()
+    assert rows.tolist() == [1, 2, 4, 5, 6]  # row 0: t = 1, 2, 4; row 1: t = 0, 1 (q = 5 + t)
+    b.to_device("cpu")
+    assert b._label_rows is rows or torch.equal(b._label_rows, rows)
