@@ -29,6 +29,8 @@ def main():
 
     from pipelinerl_amd.trainer_probe import dp_step_probe
 
+    torch.cuda.set_device(0)
+
     r = dp_step_probe(a.config, micro_batches=a.micro_batches, steps=a.steps, warmup=a.warmup,
                       device=torch.device("cuda", 0), layers=a.layers)
     print(json.dumps(r), flush=True)

@@ -27,6 +27,9 @@ def per_launch(d: Path, counter: str) -> tuple[float, int]:
                 vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
     if not vals:
         raise SystemExit(f"no {counter} rows for {KERNEL} in {f}")
+    lo, hi = min(vals.values()), max(vals.values())
+    if hi > 1.1 * lo:  # the same kernel at another shape (e.g. the label-row path) was traced too
+        raise SystemExit(f"{counter}: launches of {KERNEL} differ ({lo:.0f} .. {hi:.0f} KB): not all at T={T}")
     return sum(vals.values()) / len(vals), len(vals)
 
 

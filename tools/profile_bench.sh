@@ -3,11 +3,11 @@
 # Outputs (small CSVs only) under gpurun_out/prof_bench, gpurun_out/pmc_fetch, gpurun_out/pmc_write.
 set -u
 export TMPDIR=/tmp
-B="bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-trainer-step"
+B="bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-trainer-step --no-c3"
 bash tools/prof_stats.sh prof_bench 240 $B || exit $?
 for c in FETCH_SIZE WRITE_SIZE; do
   d=pmc_$( [ $c = FETCH_SIZE ] && echo fetch || echo write )
-  timeout -s KILL 150 rocprofv3 --pmc $c --output-format csv -d /tmp/$d -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-trainer-step > gpurun_out/$d.log 2>&1 || exit $?
+  timeout -s KILL 150 rocprofv3 --pmc $c --output-format csv -d /tmp/$d -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-trainer-step --no-c3 > gpurun_out/$d.log 2>&1 || exit $?
   mkdir -p gpurun_out/$d
   find /tmp/$d -name "*counter_collection.csv" -exec cp {} gpurun_out/$d/ \;
 done
