@@ -23,6 +23,7 @@ CSRC = PKG / "csrc"
 LIB = PKG / "libprl_hip.so"
 COMM_LIB = PKG / "libprl_comm.so"
 GEMM_LIB = PKG / "libprl_gemm.so"
+DATA_LIB = PKG / "libprl_data.so"
 ARCH = "gfx950"
 SOURCES = ["grpo_loss.hip", "flat_pack.hip", "model_ops.hip", "attn_bwd.hip"]
 
@@ -82,6 +83,31 @@ def build_gemm(force: bool = False) -> Path:
     return GEMM_LIB
 
 
+def build_data(force: bool = False) -> Path:
+    """libprl_data.so: host-only C++ (the stream codec and preprocessing arithmetic,
+    include/prl_data.h); g++, no HIP."""
+    src, hdr, pyconv = CSRC / "data.cpp", INCLUDE / "prl_data.h", CSRC / "pyconv.cpp"
+    if not force and DATA_LIB.exists() and DATA_LIB.stat().st_mtime > max(
+            src.stat().st_mtime, hdr.stat().st_mtime, pyconv.stat().st_mtime):
+        return DATA_LIB
+    cxx = os.environ.get("CXX") or shutil.which("g++") or shutil.which("c++")
+    if not cxx:
+        raise RuntimeError("no C++ compiler found for libprl_data.so")
+    tmp = DATA_LIB.with_suffix(".so.tmp")
+    import sysconfig
+    pyinc = Path(sysconfig.get_paths()["include"])
+    # the Python-object helpers (pyconv.cpp) need Python.h; their symbols resolve against the
+    # interpreter that loads the library
+    extra = [f"-I{pyinc}", str(pyconv)] if (pyinc / "Python.h").exists() else []
+    cmd = [cxx, "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall", f"-I{INCLUDE}", str(src), *extra, "-o", str(tmp),
+           "-lpthread"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"{cxx} failed for data.cpp:\n{r.stderr[-8000:]}")
+    os.replace(tmp, DATA_LIB)
+    return DATA_LIB
+
+
 def build(force: bool = False, resource_usage: bool = False, verbose: bool = False,
           defines: dict[str, str] | None = None, out: Path | None = None) -> Path:
     target = out or LIB
@@ -131,3 +157,4 @@ if __name__ == "__main__":
     print(out)
     print(build_comm(force=True))
     print(build_gemm(force=True))
+    print(build_data(force=True))

@@ -7,16 +7,34 @@ the first is masked so no token is predicted across a sequence boundary).
 
 from __future__ import annotations
 
+import array
 from typing import Any
 
 import numpy as np
 import torch
 
+from .. import native_data
 from .rl import RL_DATA_COLUMNS
 from .types import PipelineBatchEncoding
 from .utils import create_sentinel_example
 
 MASKED_TOKEN_ID = -100
+
+
+def _concat(seqs, code: str, dtype) -> np.ndarray:
+    """Concatenate lists / arrays into one flat array: libprl_data's list loop (2-5 ns per
+    element) for plain int / float lists, else array.array's."""
+    total = sum(len(s) if isinstance(s, (list, tuple, np.ndarray)) else 1 for s in seqs)
+    fast = native_data.concat_lists(seqs, native_data.DT_I64 if code == "q" else native_data.DT_F64, total)
+    if fast is not None:
+        return fast
+    buf = array.array(code)
+    for s in seqs:
+        if isinstance(s, (list, tuple)):
+            buf.extend(s)
+        else:
+            buf.extend(np.atleast_1d(np.asarray(s, dtype=dtype)).tolist())
+    return np.frombuffer(buf, dtype=dtype) if len(buf) else np.empty(0, dtype)
 
 
 def collate_packed(examples: list[dict[str, Any]], tokenizer, seq_parallel: int,
@@ -29,27 +47,14 @@ def collate_packed(examples: list[dict[str, Any]], tokenizer, seq_parallel: int,
         version = max(e["model_version"] for e in examples)
         examples = examples + [create_sentinel_example(padding, tokenizer=tokenizer, model_version=version)]
         total += padding
-    lens = np.array([len(e["input_ids"]) for e in examples], dtype=np.int64)
-    bounds = np.zeros(len(examples) + 1, dtype=np.int32)
-    bounds[1:] = np.cumsum(lens)
-    ids = np.empty(total, dtype=np.int64)
-    labels = np.empty(total, dtype=np.int64)
-    pos = np.empty(total, dtype=np.int64)
-    for i, e in enumerate(examples):
-        a, b = int(bounds[i]), int(bounds[i + 1])
-        ids[a:b] = e["input_ids"]
-        pos[a:b] = np.arange(b - a)
-        labels[a:b] = e["labels"]
-        if i > 0 and b > a:
-            labels[a] = label_pad_value
+    lens = np.fromiter((len(e["input_ids"]) for e in examples), np.int64, len(examples))
+    ids, labels, pos, bounds = native_data.collate_arrays(
+        lens, _concat([e["input_ids"] for e in examples], "q", np.int64),
+        _concat([e["labels"] for e in examples], "q", np.int64), label_pad_value)
     extra = [c for c in RL_DATA_COLUMNS if c in examples[0]]
     fields: dict[str, Any] = {}
     for k in extra:
-        vals = []
-        for e in examples:
-            v = e[k]
-            vals.extend(v) if isinstance(v, (list, tuple)) else vals.append(v)
-        fields[k] = torch.tensor([vals], dtype=torch.float32)
+        fields[k] = torch.from_numpy(_concat([e[k] for e in examples], "d", np.float64).astype(np.float32))[None]
     return PipelineBatchEncoding(
         input_ids=torch.from_numpy(ids)[None], labels=torch.from_numpy(labels)[None],
         attention_mask=torch.ones(1, total, dtype=torch.long), position_ids=torch.from_numpy(pos)[None],

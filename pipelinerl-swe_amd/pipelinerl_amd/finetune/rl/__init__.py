@@ -270,38 +270,37 @@ def populate_rl_data(dataset: list[dict[str, Any]], eos_token_id: int, config: R
     """Group advantages, group_tokens, overflow and num_labels (rl/__init__.py:380-501).
 
     Groups are keyed by (group_id, step_index); mean and sample std (ddof=1, NaN for a single
-    rollout) of each rollout's first-token reward; advantage = r - mean, or
-    (r - mean) / (nan_to_num(std) + 1e-4) when divide_advantage_by_std.
+    rollout) of each rollout's first-token reward, the mean rollout length: pandas' groupby
+    aggregations (Kahan mean, Welford std), computed by libprl_data (prl_rl_group_stats).
+    advantage = r - mean, or (r - mean) / (nan_to_num(std) + 1e-4) when divide_advantage_by_std.
     """
+    from ... import native_data
+
     keys = [f"{e['group_id']}_{e['step_index']}" for e in dataset]
     first_reward: dict[tuple[str, Any], float] = {}
     for k, e in zip(keys, dataset):
         r0 = e["rewards"][0]
         prev = first_reward.setdefault((k, e["rollout_index"]), r0)
         assert prev == r0, "rewards must be the same for every step of a rollout"
-    groups: dict[str, list[int]] = {}
-    for i, k in enumerate(keys):
-        groups.setdefault(k, []).append(i)
-    gstats = {}
-    for k, idx in groups.items():
-        rs = np.array([dataset[i]["rewards"][0] for i in idx], dtype=np.float64)
-        ns = np.array([len(dataset[i]["input_ids"]) for i in idx], dtype=np.float64)
-        std = float(rs.std(ddof=1)) if rs.size > 1 else float("nan")
-        gstats[k] = (float(rs.mean()), std, float(ns.mean()))
-    zero_var = sum(1 for m, s, _ in gstats.values() if not (s >= 1e-6))
+    index: dict[str, int] = {}
+    group_of = np.fromiter((index.setdefault(k, len(index)) for k in keys), np.int64, len(keys))
+    reward0 = np.fromiter((e["rewards"][0] for e in dataset), np.float64, len(dataset))
+    length = np.fromiter((len(e["input_ids"]) for e in dataset), np.int64, len(dataset))
+    mean, std, tokens = native_data.rl_group_stats(group_of, len(index), reward0, length)
+    zero_var = int(np.count_nonzero(~(std >= 1e-6)))
     if zero_var:
         logger.warning(f"Found {zero_var} groups with zero variance!")
-    for k, e in zip(keys, dataset):
-        mean, std, gt = gstats[k]
-        if config.divide_advantage_by_std:
-            denom = (0.0 if math.isnan(std) else std) + 1e-4
-            e["advantages"] = [(r - mean) / denom for r in e["rewards"]]
-        else:
-            e["advantages"] = [(r - mean) for r in e["rewards"]]
+    denom = np.where(np.isnan(std), 0.0, std) + 1e-4
+    for g, e in zip(group_of.tolist(), dataset):
         n = len(e["input_ids"])
-        e["group_tokens"] = [gt] * n
+        r = np.asarray(e["rewards"], dtype=np.float64)
+        adv = (r - mean[g]) / denom[g] if config.divide_advantage_by_std else r - mean[g]
+        e["advantages"] = adv.tolist()
+        e["group_tokens"] = [float(tokens[g])] * n
         e["overflow"] = [0.0 if eos_token_id in e["input_ids"] else 1.0] * len(e["overflow"])
-        e["num_labels"] = [sum(1 for lab in e["labels"] if lab != -100)] * n
+        lab = e["labels"]
+        e["num_labels"] = [len(lab) - lab.count(-100) if isinstance(lab, list)
+                           else int(np.count_nonzero(np.asarray(lab) != -100))] * n
     return dataset
 
 

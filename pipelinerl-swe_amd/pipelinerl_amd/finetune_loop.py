@@ -46,6 +46,7 @@ from .finetune.optim import get_optimizer
 from .finetune.rl import RLConfig, RLStats, rl_step
 from .finetune.rl.utils import aggregate_rl_stats
 from .finetune.sharding import fsdp_requested, set_gradient_sync, shard_model
+from . import native_data
 from .finetune.types import PipelineBatchEncoding, TrainingMetrics
 from .streams import SingleStreamSpec, read_stream, set_streams_backend, write_to_streams
 from .weight_update import (TRAINER_TOPIC, ParameterInfo, SamplesProcessed, WeightUpdateManager,  # noqa: F401
@@ -107,12 +108,15 @@ def run_data_loader(data_stream: SingleStreamSpec, batch_queue: Queue, device: t
                     stop: threading.Event | None = None, timeout: float | None = None) -> None:
     """Reads PipelineBatchEncoding micro-batches (finetune_loop.py:92-115); token counts are
     taken on the host before the pinned, non-blocking H2D copy."""
+    native = os.environ.get("PRL_NATIVE_DECODE", "1") != "0"  # 0: json + validators (A/B)
+    pin = device.type == "cuda"
     try:
         with read_stream(data_stream, timeout=timeout) as reader:
-            for doc in reader.read():
+            for line in reader.read_lines():
                 if stop is not None and stop.is_set():
                     return
-                b = PipelineBatchEncoding(**doc)
+                # libprl_data decodes the numeric fields into pinned tensors without the GIL
+                b = native_data.decode_batch(line, pin=pin) if native else PipelineBatchEncoding(**json.loads(line))
                 ntok = int(b.attention_mask.sum())
                 nseq = batch_sequence_count(b)
                 if device.type == "cuda":
@@ -121,7 +125,7 @@ def run_data_loader(data_stream: SingleStreamSpec, batch_queue: Queue, device: t
                     for name in type(b).model_fields:
                         v = getattr(b, name)
                         if isinstance(v, torch.Tensor) and name != "seq_boundaries":  # host metadata
-                            setattr(b, name, v.pin_memory().to(device, non_blocking=True))
+                            setattr(b, name, (v if v.is_pinned() else v.pin_memory()).to(device, non_blocking=True))
                     if rows is not None:
                         b._label_rows = rows.pin_memory().to(device, non_blocking=True)
                 batch_queue.put((b, ntok, nseq))

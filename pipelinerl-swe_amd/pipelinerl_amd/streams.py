@@ -91,6 +91,14 @@ def _jsonable(x: Any) -> Any:
 
 
 def dumps(data: Any) -> str:
+    """One stream line.  A pydantic model or dict (a PipelineBatchEncoding, a message) goes
+    through libprl_data's encoder, byte-identical to json.dumps of the lists (numeric tensors /
+    arrays formatted natively); anything else through json."""
+    if isinstance(data, BaseModel):
+        data = data.model_dump()
+    if isinstance(data, dict) and all(isinstance(k, str) for k in data):
+        from . import native_data
+        return native_data.encode_document(data)
     return json.dumps(_jsonable(data), separators=(",", ":"))
 
 
@@ -160,34 +168,32 @@ class FileStreamReader:
                 raise TimeoutError(f"stream {self.stream} was not created")
             logger.warning(f"Waiting for {self.stream} to be created")
             time.sleep(min(RECHECK_DELAY, self.poll * 10))
-        self._file = open(self._path, "r")
+        self._file = open(self._path, "rb")
         return self
 
     def __exit__(self, *exc):
         self._file.close()
 
-    def read(self) -> Iterator[Any]:
+    def read_lines(self) -> Iterator[bytes]:
+        """Complete lines, as bytes (a line without its newline is still being written: wait
+        for it).  Returns after `timeout` s without a new line."""
         pos = self._file.tell()
         idle = time.time()
         while True:
             line = self._file.readline()
-            if line.endswith("\n"):
-                try:
-                    doc = json.loads(line)
-                except json.JSONDecodeError:  # a partially flushed line: reopen and retry
-                    self._file.close()
-                    self._file = open(self._path, "r")
-                    self._file.seek(pos)
-                    time.sleep(self.poll)
-                    continue
+            if line.endswith(b"\n"):
                 pos = self._file.tell()
                 idle = time.time()
-                yield doc
+                yield line
             else:
                 if self.timeout is not None and time.time() - idle > self.timeout:
                     return
                 self._file.seek(pos)
                 time.sleep(self.poll)
+
+    def read(self) -> Iterator[Any]:
+        for line in self.read_lines():
+            yield json.loads(line)
 
 
 def _check_backend():
