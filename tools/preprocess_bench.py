@@ -38,7 +38,31 @@ while i < len(out):
     if not cur: cur=[out[i]]; i+=1
     collate_packed(cur, types.SimpleNamespace(eos_token_id=EOS), 1); nb+=1
 t4=time.time()
-res = {"rollouts": len(out), "tokens": ntok, "micro_batches": nb,
+# the training_data stream codec on the same micro-batches: json + validators vs libprl_data
+from pipelinerl_amd import native_data
+from pipelinerl_amd.finetune.types import PipelineBatchEncoding
+from pipelinerl_amd.streams import _jsonable
+batches = []
+i = 0
+while i < len(out) and len(batches) < 40:
+    cur=[]; tot=0
+    while i < len(out) and tot + len(out[i]["input_ids"]) <= 12000:
+        cur.append(out[i]); tot += len(out[i]["input_ids"]); i += 1
+    if not cur: cur=[out[i]]; i+=1
+    batches.append(collate_packed(cur, types.SimpleNamespace(eos_token_id=EOS), 1))
+btok = sum(int(b.attention_mask.sum()) for b in batches)
+native_data.decode_batch(native_data.encode_document(batches[0].model_dump()).encode())  # load + first-call costs
+t5 = time.time(); lines_py = [json.dumps(_jsonable(b.model_dump()), separators=(",", ":")) for b in batches]; t6 = time.time()
+lines = [native_data.encode_document(b.model_dump()).encode() for b in batches]; t7 = time.time()
+assert [l.decode() for l in lines] == lines_py
+t8 = time.time(); [PipelineBatchEncoding(**json.loads(l)) for l in lines]; t9 = time.time()
+[native_data.decode_batch(l, threads=1) for l in lines]; t10 = time.time()
+[native_data.decode_batch(l, threads=4) for l in lines]; t11 = time.time()
+codec = {"micro_batches": len(batches), "tokens": btok, "MB": round(sum(map(len, lines)) / 1e6, 1),
+         "encode_Mtok_s": {"python": round(btok / (t6 - t5) / 1e6, 2), "native": round(btok / (t7 - t6) / 1e6, 2)},
+         "decode_Mtok_s": {"python": round(btok / (t9 - t8) / 1e6, 2), "native_1thread": round(btok / (t10 - t9) / 1e6, 2),
+                           "native_4threads": round(btok / (t11 - t10) / 1e6, 2)}}
+res = {"codec": codec, "rollouts": len(out), "tokens": ntok, "micro_batches": nb,
        "build": {"populate_s": round(t2 - t1, 3), "populate_Mtok_s": round(ntok / (t2 - t1) / 1e6, 2),
                  "collate_s": round(t4 - t3, 3), "collate_Mtok_s": round(ntok / (t4 - t3) / 1e6, 2)}}
 if "--reference" in sys.argv:
