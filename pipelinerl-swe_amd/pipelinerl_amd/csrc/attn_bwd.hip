@@ -100,6 +100,13 @@ __device__ __forceinline__ void stage_store(const Stage& st, char* base, int tid
   }
 }
 
+#ifndef PRL_ATTN_EXP_NOLOAD
+#define PRL_ATTN_EXP_NOLOAD 0  // timing experiment only (wrong results): backward stages after the first not loaded
+#endif
+#ifndef PRL_ATTN_EXP_NOEXP
+#define PRL_ATTN_EXP_NOEXP 0  // timing experiment only (wrong results): backward exp2 replaced by a multiply
+#endif
+__device__ __forceinline__ float bexp2(float x) { return PRL_ATTN_EXP_NOEXP ? x * 0.5f : __builtin_amdgcn_exp2f(x); }
 #ifndef PRL_ATTN_INTERLEAVE
 #define PRL_ATTN_INTERLEAVE 1  // 0: one tile at a time everywhere (A/B builds, tools/build_variants.py)
 #endif
@@ -156,7 +163,7 @@ __device__ __forceinline__ void dkdv_probs(const f32x16& S, const f32x16& dP, co
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int r = 4 * gg + j;
-      float p = fexp2(__builtin_fmaf(S[r], c2, -Lr[j]));
+      float p = bexp2(__builtin_fmaf(S[r], c2, -Lr[j]));
       if (MASK) {
         const int t = q0 + 8 * gg + 4 * hi + j;
         p = (kval && key <= t && t < s1) ? p : 0.f;
@@ -258,7 +265,7 @@ __device__ __forceinline__ void attn_bwd_dkdv(const __bf16* __restrict__ q, cons
     }
     __syncthreads();
     const int qn = q00 + STAGE;  // prefetch the next stage behind this stage's MFMAs
-    if (qn < s1) {
+    if (qn < s1 && !PRL_ATTN_EXP_NOLOAD) {
       nq = stage_load(q, rsq, h, qn, s1, tid);
       nd = stage_load(dout, rsq, h, qn, s1, tid);
       if (tid < STAGE && qn + tid < s1) {
@@ -312,7 +319,7 @@ __device__ __forceinline__ void dq_probs(const f32x16& St, const f32x16& dPt, in
                                          float c2, float lq, float dq_delta, bf16x8* sb) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
-    float p = fexp2(__builtin_fmaf(St[r], c2, -lq));
+    float p = bexp2(__builtin_fmaf(St[r], c2, -lq));
     if (MASK) {
       const int kj = k0 + 8 * (r >> 2) + 4 * hi + (r & 3);
       p = (qval && kj <= qq && kj < s1) ? p : 0.f;
@@ -389,7 +396,7 @@ __device__ __forceinline__ void attn_bwd_dq(const __bf16* __restrict__ q, const 
     stage_store(nk, sK, tid);
     stage_store(nv, sV, tid);
     __syncthreads();
-    if (k00 + STAGE < kend) {
+    if (k00 + STAGE < kend && !PRL_ATTN_EXP_NOLOAD) {
       nk = stage_load(k, rsk, g, k00 + STAGE, s1, tid);
       nv = stage_load(v, rsk, g, k00 + STAGE, s1, tid);
     }

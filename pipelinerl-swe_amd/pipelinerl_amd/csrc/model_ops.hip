@@ -192,6 +192,9 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_narrow(const uint16_t* __rest
 // wave order, so the block needs H floats of LDS instead of 4 H, and w / x / dy stay packed
 // between uses: 0.254 -> 0.217 ms at 16384 x 3584 (tools/ew_bench.py).  Narrow rows keep the
 // 4-row fold (rmsnorm_bwd_narrow), which measured faster at H = 1536 (0.179 vs 0.193 ms).
+#ifndef PRL_NORM_WIDE_DRES_EARLY
+#define PRL_NORM_WIDE_DRES_EARLY 1  // A/B (add_rmsnorm 8192 x 3584 bwd incl. autograd): 0.144-0.148 -> 0.130 ms
+#endif
 template <int NV, bool ADD>
 __global__ __launch_bounds__(256) void rmsnorm_bwd_wide(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
                                                    const uint16_t* __restrict__ w, const float* __restrict__ rstd,
@@ -213,6 +216,8 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_wide(const uint16_t* __restri
     for (int j = 0; j < 8; ++j) acc[k][j] = 0.f;
   }
   u32x4 xv[NV], gv[NV];
+  constexpr bool kEarly = ADD && PRL_NORM_WIDE_DRES_EARLY;  // dres loaded with x / dy (in flight across the reduction)
+  u32x4 dvv[kEarly ? NV : 1];
   auto load_row = [&](int64_t r, u32x4* xo, u32x4* go) {
     const u32x4* xr = reinterpret_cast<const u32x4*>(x + r * H);
     const u32x4* gr = reinterpret_cast<const u32x4*>(dy + r * H);
@@ -221,6 +226,9 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_wide(const uint16_t* __restri
       const int c = k * 64 + lane;
       xo[k] = c < nv8 ? __builtin_nontemporal_load(xr + c) : u32x4{0, 0, 0, 0};
       go[k] = c < nv8 ? __builtin_nontemporal_load(gr + c) : u32x4{0, 0, 0, 0};
+      if constexpr (kEarly)
+        dvv[k] = c < nv8 ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(dres + r * H) + c)
+                         : u32x4{0, 0, 0, 0};
     }
   };
   if (wave < rows) load_row(wave, xv, gv);
@@ -266,7 +274,9 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_wide(const uint16_t* __restri
           o[j] = pack(rs * g0 - cfac * lo(xv[k][j]), rs * g1 - cfac * hi(xv[k][j]));
         }
         if constexpr (ADD) {  // + the residual branch's gradient, summed as autograd would (bf16 + bf16)
-          const u32x4 dv = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(dres + r * H) + c);
+          u32x4 dv;
+          if constexpr (kEarly) dv = dvv[k];
+          else dv = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(dres + r * H) + c);
 #pragma unroll
           for (int j = 0; j < 4; ++j) o[j] = pack(lo(o[j]) + lo(dv[j]), hi(o[j]) + hi(dv[j]));
         }

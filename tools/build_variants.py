@@ -20,6 +20,12 @@ VARIANTS = {
     "swiglu_u2": {"SWIGLU_UNROLL": "2"},
     "attn_fwd_1wave": {"PRL_ATTN_FWD_MINB": "1"},
     "attn_serial": {"PRL_ATTN_INTERLEAVE": "0"},
+    "attn_exp_noload": {"PRL_ATTN_EXP_NOLOAD": "1"},
+    "attn_exp_noexp": {"PRL_ATTN_EXP_NOEXP": "1"},
+    "attn_exp_noload_noexp": {"PRL_ATTN_EXP_NOLOAD": "1", "PRL_ATTN_EXP_NOEXP": "1"},
+    "norm_dres_early": {"PRL_NORM_WIDE_DRES_EARLY": "1"},
+    "norm_grid1536": {"PRL_NORM_GRID": "1536"},
+    "norm_grid3072_early": {"PRL_NORM_GRID": "3072", "PRL_NORM_WIDE_DRES_EARLY": "1"},
     "norm_grid2048": {"PRL_NORM_GRID": "2048"},
     "norm_fwd2048": {"PRL_NORM_FWD_GRID": "2048"},
 }
