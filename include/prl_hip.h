@@ -200,6 +200,15 @@ int prl_unflatten_bf16(const void* src, void* const* dsts, const int32_t* dtypes
                        const int64_t* numels, const int64_t* src_offsets, int32_t n,
                        void* stream);
 
+/* Weight-gradient scale / accumulate (bf16 destination), the upstream scale read on the device:
+ *   t = bf16(float(src[i]) * (*scale));  dst[i] = accumulate ? bf16(float(dst[i]) + float(t)) : t
+ * src f32 or bf16, n elements, src / dst 16-B aligned.  In place (dst == src, bf16, accumulate 0)
+ * nothing is written when *scale == 1.  Replaces the ATen chain `(dw.float() * g).to(bf16)` +
+ * AccumulateGrad's `grad += dw` behind the reference's lm_head weight gradient
+ * (pipelinerl/finetune_loop.py:620-629, loss.backward over the lm_head of rl/__init__.py:197). */
+int prl_grad_scale_bf16(const void* src, int32_t src_dtype, const float* scale, void* dst, int64_t n,
+                        int32_t accumulate, void* stream);
+
 /* Sum of squares of n device tensors (f32 or bf16) accumulated into *out (device f64).
  * *out is overwritten. */
 int prl_grad_sqnorm(const void* const* srcs, const int32_t* dtypes, const int64_t* numels,

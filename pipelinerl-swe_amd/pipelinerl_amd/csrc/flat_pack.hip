@@ -121,6 +121,54 @@ __global__ __launch_bounds__(256) void sqnorm_kernel(PackGroup g, double* __rest
   if (threadIdx.x == 0) atomicAdd(out, part[0] + part[1] + part[2] + part[3]);
 }
 
+// Gradient scale / accumulate for the fused lm_head's weight gradient (finetune/rl/fused_linear.py):
+// t = bf16(float(src) * s) with s = *scale read on the device (no host sync); then dst = t, or
+// dst = bf16(float(dst) + float(t)) (autograd's AccumulateGrad add of the two bf16 tensors, in one
+// pass instead of a float() copy, a multiply, a cast and an add).  In place (dst == src, bf16, no
+// accumulate) the kernel returns at once when s == 1: t = src exactly.
+template <bool SRC_F32, bool ACC>
+__global__ __launch_bounds__(256) void grad_scale_kernel(const void* __restrict__ src, const float* __restrict__ scale,
+                                                         uint16_t* dst, int64_t n, int skip_if_one) {
+  const float s = *scale;
+  if (skip_if_one && s == 1.0f) return;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t nv = n >> 3;
+  auto one = [&](float x, uint16_t d) -> uint16_t {
+    const float t = bf_to_f(f_to_bf(x * s));
+    return ACC ? f_to_bf(bf_to_f(d) + t) : f_to_bf(t);
+  };
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
+    float x[8];
+    if (SRC_F32) {
+      const f32x4 a = reinterpret_cast<const f32x4*>(src)[2 * v], b = reinterpret_cast<const f32x4*>(src)[2 * v + 1];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        x[j] = a[j];
+        x[4 + j] = b[j];
+      }
+    } else {
+      const u32x4 a = reinterpret_cast<const u32x4*>(src)[v];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        x[2 * j] = bf_lo(a[j]);
+        x[2 * j + 1] = bf_hi(a[j]);
+      }
+    }
+    u32x4 d = ACC ? reinterpret_cast<const u32x4*>(dst)[v] : u32x4{0, 0, 0, 0};
+    u32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint16_t lo = one(x[2 * j], (uint16_t)(d[j] & 0xffffu)), hi = one(x[2 * j + 1], (uint16_t)(d[j] >> 16));
+      o[j] = (uint32_t)lo | ((uint32_t)hi << 16);
+    }
+    reinterpret_cast<u32x4*>(dst)[v] = o;
+  }
+  for (int64_t i = (nv << 3) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const float x = SRC_F32 ? static_cast<const float*>(src)[i] : bf_to_f(static_cast<const uint16_t*>(src)[i]);
+    dst[i] = one(x, ACC ? dst[i] : (uint16_t)0);
+  }
+}
+
 static int grid_x_for(const PackGroup& g) {
   int64_t mx = 1;
   for (int i = 0; i < g.n; ++i) mx = g.numel[i] > mx ? g.numel[i] : mx;
@@ -180,6 +228,29 @@ int prl_unflatten_bf16(const void* src, void* const* dsts, const int32_t* dtypes
     if (e != hipSuccess) return (int)e;
   }
   return PRL_OK;
+}
+
+int prl_grad_scale_bf16(const void* src, int32_t src_dtype, const float* scale, void* dst, int64_t n,
+                        int32_t accumulate, void* stream) {
+  if (!src || !scale || !dst || n < 0) return PRL_E_INVALID;
+  if (src_dtype != PRL_F32 && src_dtype != PRL_BF16) return PRL_E_UNSUPPORTED;
+  if ((reinterpret_cast<uintptr_t>(src) & 15) || (reinterpret_cast<uintptr_t>(dst) & 15)) return PRL_E_INVALID;
+  if (n == 0) return PRL_OK;
+  const bool f32 = src_dtype == PRL_F32;
+  const int skip = !accumulate && !f32 && src == dst;
+  int64_t blocks = (n / 8 + 255) / 256;
+  blocks = blocks < 1 ? 1 : (blocks > 4096 ? 4096 : blocks);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  uint16_t* d = static_cast<uint16_t*>(dst);
+  if (f32 && accumulate)
+    hipLaunchKernelGGL((grad_scale_kernel<true, true>), dim3((unsigned)blocks), dim3(256), 0, s, src, scale, d, n, skip);
+  else if (f32)
+    hipLaunchKernelGGL((grad_scale_kernel<true, false>), dim3((unsigned)blocks), dim3(256), 0, s, src, scale, d, n, skip);
+  else if (accumulate)
+    hipLaunchKernelGGL((grad_scale_kernel<false, true>), dim3((unsigned)blocks), dim3(256), 0, s, src, scale, d, n, skip);
+  else
+    hipLaunchKernelGGL((grad_scale_kernel<false, false>), dim3((unsigned)blocks), dim3(256), 0, s, src, scale, d, n, skip);
+  return (int)hipGetLastError();
 }
 
 int prl_grad_sqnorm(const void* const* srcs, const int32_t* dtypes, const int64_t* numels, int32_t n,

@@ -58,6 +58,8 @@ class GradBuckets:
         self.stream = torch.cuda.Stream(device=dev) if self.on_gpu else None
         self._avg = self.on_gpu and dist.get_backend(group) == "nccl" and reduce == "mean"
         self._hooks = [p.register_post_accumulate_grad_hook(self._hook) for p in params]
+        for p in params:  # model_ops._wgrad may add into .grad in the GEMM while not armed (no hook due)
+            p._prl_grad_buckets = self
 
     def _make(self, ps: list[torch.Tensor]) -> None:
         total = sum(p.numel() for p in ps)

@@ -178,6 +178,45 @@ class RopeFn(torch.autograd.Function):
         return dq.transpose(1, 2), dk.transpose(1, 2), None, None
 
 
+# Weight-gradient accumulation in the wgrad GEMM's epilogue: when a weight already holds a
+# gradient (the micro-batches after the first of an optimizer step, or the DP loop's gradient
+# buckets, which are never None), dW = dY^T X is added into it by the GEMM (beta = 1) instead of
+# being written to a new tensor that autograd's AccumulateGrad then adds with a separate bf16 add
+# kernel (a [N, K] read-read-write per weight per micro-batch: ~2 % of a 7B C3 step).  The sum is
+# rounded to bf16 once instead of twice.  Not used when a post-accumulate hook must see the
+# gradient (an armed GradBuckets, any other hook) or under FSDP (shard_model switches it off):
+# there autograd accumulates as before.  PRL_FUSE_GRAD_ACCUM=0 turns it off (A/B).
+_FUSE_GRAD_ACCUM = os.environ.get("PRL_FUSE_GRAD_ACCUM", "1") != "0"
+
+
+def disable_fused_grad_accumulation() -> None:
+    global _FUSE_GRAD_ACCUM
+    _FUSE_GRAD_ACCUM = False
+
+
+def _accum_target(w):
+    if not _FUSE_GRAD_ACCUM or not isinstance(w, torch.nn.Parameter):
+        return None
+    g = w.grad
+    if g is None or g.dtype != w.dtype or g.shape != w.shape or not g.is_contiguous():
+        return None
+    hooks = w._post_accumulate_grad_hooks
+    if hooks:
+        owner = getattr(w, "_prl_grad_buckets", None)  # finetune/grad_sync.py: fires only when armed
+        if owner is None or owner.armed or len(hooks) != 1:
+            return None
+    return g
+
+
+def _wgrad(dy, x, w):
+    """dW for parameter w, or None after adding it into w.grad in the GEMM (see above)."""
+    g = _accum_target(w)
+    if g is not None:
+        gemm.linear_wgrad(dy, x, out=g, accumulate=True)
+        return None
+    return gemm.linear_wgrad(dy, x)
+
+
 class PrlLinearFn(torch.autograd.Function):
     """F.linear whose GEMMs run through prl_gemm (the ROCm hipBLASLt, include/prl_gemm.h).
 
@@ -191,6 +230,7 @@ class PrlLinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b):
         ctx.save_for_backward(x, w)
+        ctx.param = w  # the Parameter itself (its .grad: the fused accumulation)
         ctx.has_bias = b is not None
         return _fwd_gemm(x, w, b)
 
@@ -199,7 +239,7 @@ class PrlLinearFn(torch.autograd.Function):
         x, w = ctx.saved_tensors
         dy = dy if dy.is_contiguous() else dy.contiguous()
         dx = gemm.linear_dgrad(dy, w) if ctx.needs_input_grad[0] else None
-        dw = gemm.linear_wgrad(dy, x) if ctx.needs_input_grad[1] else None
+        dw = _wgrad(dy, x, ctx.param) if ctx.needs_input_grad[1] else None
         db = None
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = dy.reshape(-1, dy.shape[-1]).sum(0, dtype=torch.float32).to(dy.dtype)
@@ -217,6 +257,7 @@ class SharedInputLinearFn(torch.autograd.Function):
         ws, bs = wb[0::2], wb[1::2]
         ctx.set_materialize_grads(False)  # an unused output's gradient stays None: no GEMMs for it
         ctx.save_for_backward(x, *ws)
+        ctx.params = ws
         ctx.has_bias = tuple(b is not None for b in bs)
         return tuple(_fwd_gemm(x, w, b) for w, b in zip(ws, bs))
 
@@ -232,7 +273,7 @@ class SharedInputLinearFn(torch.autograd.Function):
             dy = dy if dy.is_contiguous() else dy.contiguous()
             if ctx.needs_input_grad[0]:
                 dx = gemm.linear_dgrad(dy, w) if dx is None else gemm.linear_dgrad(dy, w, out=dx, accumulate=True)
-            dw = gemm.linear_wgrad(dy, x) if ctx.needs_input_grad[1 + 2 * i] else None
+            dw = _wgrad(dy, x, ctx.params[i]) if ctx.needs_input_grad[1 + 2 * i] else None
             db = None
             if ctx.has_bias[i] and ctx.needs_input_grad[2 + 2 * i]:
                 db = dy.reshape(-1, dy.shape[-1]).sum(0, dtype=torch.float32).to(dy.dtype)

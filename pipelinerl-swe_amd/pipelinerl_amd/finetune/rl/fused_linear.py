@@ -57,6 +57,30 @@ def _c_batch(ptr: int, dtype: torch.dtype, B: int, L: int, V: int, ld: int, f: d
         f["num_labels"].data_ptr(), f["overflow"].data_ptr(), None)
 
 
+def _weight_grad(dw: torch.Tensor, g: torch.Tensor, param, w_dtype):
+    """The lm_head weight gradient bf16(dw * g) (g: the upstream scale, fp32 on the device, not
+    rounded to bf16).  bf16 weights: one prl_grad_scale_bf16 pass — added into param.grad when
+    it already holds a gradient (the result autograd's AccumulateGrad would store, without the
+    extra tensors; returns None then), else scaled in place (nothing written when g == 1)."""
+    if w_dtype != torch.bfloat16 or not dw.is_contiguous() or dw.data_ptr() % 16:
+        return (dw.float() * g).to(w_dtype)
+    from ..model_ops import _accum_target
+
+    lib = _native.load()
+    stream = torch.cuda.current_stream(dw.device).cuda_stream
+    src_dt = _native.PRL_F32 if dw.dtype == torch.float32 else _native.PRL_BF16
+    g = g.reshape(1).contiguous()
+    target = _accum_target(param)
+    if target is not None and target.data_ptr() % 16 == 0:
+        _native.check(lib.prl_grad_scale_bf16(dw.data_ptr(), src_dt, g.data_ptr(), target.data_ptr(), dw.numel(), 1,
+                                              stream), "prl_grad_scale_bf16")
+        return None
+    out = dw if src_dt == _native.PRL_BF16 else torch.empty(dw.shape, dtype=torch.bfloat16, device=dw.device)
+    _native.check(lib.prl_grad_scale_bf16(dw.data_ptr(), src_dt, g.data_ptr(), out.data_ptr(), dw.numel(), 0, stream),
+                  "prl_grad_scale_bf16")
+    return out
+
+
 class LinearGrpoLossFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, hidden, weight, fields, params: GrpoParams, chunk_rows: int, label_rows=None):
@@ -131,6 +155,7 @@ class LinearGrpoLossFn(torch.autograd.Function):
         if write_grad and dw is None:  # no label rows: zero weight gradient
             dw = torch.zeros((V, Hd), dtype=torch.float32, device=dev)
         ctx.dh, ctx.dw = dh, dw
+        ctx.param = weight  # the Parameter (its .grad: fused accumulation, _weight_grad)
         ctx.shape = (B, L, Hd)
         ctx.h_dtype, ctx.w_dtype = hidden.dtype, weight.dtype
         ctx.grad_scale = float(params.grad_scale)
@@ -144,7 +169,7 @@ class LinearGrpoLossFn(torch.autograd.Function):
             if ctx.needs_input_grad[0]:
                 d_hidden = (ctx.dh.view(ctx.shape) * g.to(ctx.dh.dtype)).to(ctx.h_dtype)
             if ctx.needs_input_grad[1]:
-                d_weight = (ctx.dw.float() * g).to(ctx.w_dtype)  # g applied in fp32 (not rounded to bf16)
+                d_weight = _weight_grad(ctx.dw, g, ctx.param, ctx.w_dtype)
         ctx.dh = ctx.dw = None
         return d_hidden, d_weight, None, None, None, None
 

@@ -163,7 +163,9 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = N
 
 def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = None,
                  accumulate: bool = False) -> torch.Tensor:
-    """dW = dY^T X ([N, K]); ``out`` fp32 with accumulate=True adds into it (chunked lm_head)."""
+    """dW = dY^T X ([N, K]); with ``out`` ([N, K] contiguous, fp32 or bf16) and accumulate=True the
+    GEMM adds into it (beta = 1): the chunked lm_head's fp32 sum, a weight's gradient accumulated
+    over micro-batches (finetune/model_ops.py _wgrad)."""
     d2, x2 = _rows(dy), _rows(x)
     T, N = d2.shape
     K = x2.shape[1]
@@ -173,6 +175,8 @@ def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = N
         raise GemmError("linear_wgrad: out must be a contiguous [N, K] tensor")
     dd = F32 if out.dtype == torch.float32 else BF16
     sol = solution_for("wgrad", T, N, K, dd, accumulate)
+    if sol is None and accumulate:  # a swept beta = 0 solution; prl_gemm checks it supports beta = 1
+        sol = solution_for("wgrad", T, N, K, dd)
     gemm(N_, T_, K, N, T, x2, K, d2, N, out, K, beta=1.0 if accumulate else 0.0, solution=-1 if sol is None else sol)
     return out
 
