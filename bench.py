@@ -239,7 +239,11 @@ def main():
         try:
             return fn()
         except Exception as e:  # noqa: BLE001
+            import traceback
+
             failed.append(name)
+            # every rank's own failure on stderr (rank 0's line carries only its own)
+            print(f"[rank {rank}] probe {name} failed:\n{traceback.format_exc()}", file=sys.stderr, flush=True)
             torch.cuda.empty_cache()
             return {"error": f"{type(e).__name__}: {e}"[:400]}
 

@@ -75,7 +75,7 @@ def packed_batch(T: int, seq: int, prompt: int, V: int, device, seed: int = 0, r
     return b
 
 
-def rl_config(samples_per_step: int, fused_head: bool = False, kl_coef: float = 0.0):
+def rl_config(samples_per_step: int, fused_head: bool = True, kl_coef: float = 0.0):
     from .finetune.rl import RLConfig
 
     # GRPO defaults (conf/finetune/base.yaml + grpo.yaml): ppo, eps 4, kl 0, C 5; C5 turns KL on
@@ -99,7 +99,7 @@ class TrainerStep:
     """
 
     def __init__(self, name: str = "1.5b", tokens: int = 16384, seq: int = 2048, prompt: int = 256,
-                 micro_batches: int = 4, device=None, fused_head: bool = False, grad_ckpt: bool = False,
+                 micro_batches: int = 4, device=None, fused_head: bool = True, grad_ckpt: bool = False,
                  fused_ops: bool = True, group=None, model=None, step_fn=None, vocab: int | None = None,
                  fsdp: bool = False, kl_coef: float = 0.0, layers: int | None = None, batches: list | None = None,
                  samples_per_step: int | None = None, local: bool = False):
@@ -221,7 +221,7 @@ class TrainerStep:
 
 def trainer_step_probe(name: str = "1.5b", tokens: int = 16384, seq: int = 2048, prompt: int = 256,
                        micro_batches: int = 4, steps: int = 3, warmup: int = 1, device=None,
-                       fused_head: bool = False, grad_ckpt: bool = False, fused_ops: bool = True) -> dict:
+                       fused_head: bool = True, grad_ckpt: bool = False, fused_ops: bool = True) -> dict:
     """The optimizer step at this world size.  With several ranks the same replica is also timed
     without the gradient all-reduce first (``local_tokens_per_s_per_gpu``: what one GPU does on its
     own, on this node at this moment), so ``dp_efficiency`` = DP / local tokens/s per GPU is the
