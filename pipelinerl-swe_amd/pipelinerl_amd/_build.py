@@ -109,7 +109,7 @@ def build_data(force: bool = False) -> Path:
 
 
 def build(force: bool = False, resource_usage: bool = False, verbose: bool = False,
-          defines: dict[str, str] | None = None, out: Path | None = None) -> Path:
+          defines: dict[str, str] | None = None, out: Path | None = None, extra_flags: list[str] | None = None) -> Path:
     target = out or LIB
     if out is None and not force and not resource_usage and not _stale():
         return LIB
@@ -122,6 +122,7 @@ def build(force: bool = False, resource_usage: bool = False, verbose: bool = Fal
         flags.append("-Rpass-analysis=kernel-resource-usage")
     for k, v in (defines or {}).items():
         flags.append(f"-D{k}={v}")
+    flags += list(extra_flags or [])
 
     def compile_one(src: str):
         obj = objdir / (Path(src).stem + ".o")
@@ -146,10 +147,10 @@ def build(force: bool = False, resource_usage: bool = False, verbose: bool = Fal
     return target
 
 
-def build_variant(name: str, defines: dict[str, str]) -> Path:
+def build_variant(name: str, defines: dict[str, str], extra_flags: list[str] | None = None) -> Path:
     """An experiment build (e.g. cache-policy A/B) at variants/libprl_hip_<name>.so; load it
     with PRL_LIB=<path>."""
-    return build(defines=defines, out=VARIANT_DIR / f"libprl_hip_{name}.so")
+    return build(defines=defines, out=VARIANT_DIR / f"libprl_hip_{name}.so", extra_flags=extra_flags)
 
 
 if __name__ == "__main__":

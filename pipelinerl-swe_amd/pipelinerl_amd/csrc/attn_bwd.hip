@@ -140,13 +140,26 @@ __device__ __forceinline__ void interleave() {
 __device__ __forceinline__ bool dkdv_live(int kw, int q0, int s1) {  // wave-uniform
   return !(kw >= s1 || kw > q0 + TILE - 1 || q0 >= s1);
 }
-// S = Q K^T and dP = dO V^T with the key on the lane (K, V rows in registers: kf, vf)
-__device__ __forceinline__ void dkdv_scores(const char* tQ, const char* tdO, const bf16x8* kf, const bf16x8* vf,
-                                            int l32, int hi, f32x16& S, f32x16& dP) {
+// S = Q K^T and dP = dO V^T with the key on the lane.  K, V rows: PRL_ATTN_KV_LDS = 1 reads them
+// from the workgroup's K / V images in LDS (kf / vf point at the wave's 32 rows there), 0 holds
+// them in registers (64 VGPRs: with them the S / dP accumulators spill to AGPRs, and every
+// softmax input costs a v_accvgpr_read)
+#ifndef PRL_ATTN_KV_LDS
+#define PRL_ATTN_KV_LDS 0  // A/B: 1 (K/V, Q/dO from LDS, 182 VGPRs) measured 8-12 % slower (profiles/r02_attn_regs_ab.jsonl)
+#endif
+#if PRL_ATTN_KV_LDS
+typedef const char* KvRef;
+__device__ __forceinline__ bf16x8 kv_frag(KvRef base, int l32, int c, int hi) { return row_read(base, l32, 2 * c + hi); }
+#else
+typedef const bf16x8* KvRef;
+__device__ __forceinline__ bf16x8 kv_frag(KvRef f, int, int c, int) { return f[c]; }
+#endif
+__device__ __forceinline__ void dkdv_scores(const char* tQ, const char* tdO, KvRef kf, KvRef vf, int l32, int hi,
+                                            f32x16& S, f32x16& dP) {
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
-    S = mfma(row_read(tQ, l32, 2 * c + hi), kf[c], S);
-    dP = mfma(row_read(tdO, l32, 2 * c + hi), vf[c], dP);
+    S = mfma(row_read(tQ, l32, 2 * c + hi), kv_frag(kf, l32, c, hi), S);
+    dP = mfma(row_read(tdO, l32, 2 * c + hi), kv_frag(vf, l32, c, hi), dP);
   }
 }
 // P = 2^(c2 S - L2), dS = P (dP - delta) in bf16, the 16 query rows of this lane's accumulator in
@@ -186,7 +199,7 @@ __device__ __forceinline__ void dkdv_acc(const char* tQ, const char* tdO, int la
 }
 // one tile, masked (the diagonal and ragged ends)
 __device__ __forceinline__ void dkdv_tile(const char* tQ, const char* tdO, const float* tL, const float* tDl, int q0,
-                                          const bf16x8* kf, const bf16x8* vf, int key, bool kval, int s1, int lane,
+                                          KvRef kf, KvRef vf, int key, bool kval, int s1, int lane,
                                           float c2, f32x16* dKt, f32x16* dVt) {
   const int hi = lane >> 5, l32 = lane & 31;
   f32x16 S = f32x16{}, dP = f32x16{};
@@ -197,7 +210,7 @@ __device__ __forceinline__ void dkdv_tile(const char* tQ, const char* tdO, const
 }
 // two unmasked tiles (a = the stage's first 32 rows, b = the next 32), interleaved
 __device__ __forceinline__ void dkdv_pair(const char* tQ, const char* tdO, const float* tL, const float* tDl,
-                                          const bf16x8* kf, const bf16x8* vf, int key, bool kval, int s1, int lane,
+                                          KvRef kf, KvRef vf, int key, bool kval, int s1, int lane,
                                           float c2, f32x16* dKt, f32x16* dVt) {
   const int hi = lane >> 5, l32 = lane & 31;
   const char *tQb = tQ + TILE * 256, *tdOb = tdO + TILE * 256;
@@ -226,7 +239,7 @@ __device__ __forceinline__ void attn_bwd_dkdv(const __bf16* __restrict__ q, cons
                                               const int32_t* __restrict__ items, __bf16* __restrict__ dk,
                                               __bf16* __restrict__ dv, int64_t T, int H, int Hkv, float c2,
                                               float scale, int it, int g, char* sQ, char* sdO, float* sL,
-                                              float* sDl) {
+                                              float* sDl, char* sKV) {
   const int tid = threadIdx.x;
   const int s1 = items[3 * it + 1], kb = items[3 * it + 2];
   const int lane = tid & 63, w = tid >> 6, hi = lane >> 5, l32 = lane & 31;
@@ -235,12 +248,24 @@ __device__ __forceinline__ void attn_bwd_dkdv(const __bf16* __restrict__ q, cons
   const int kw = kb + 32 * w;
   const int key = kw + l32;
   const bool kval = key < s1;
+#if PRL_ATTN_KV_LDS
+  {  // the block's 128 K and V rows into two swizzled images (visible after the loop's first barriers)
+    const Stage k0 = stage_load(k, rsk, g, kb, s1, tid), k1 = stage_load(k, rsk, g, kb + STAGE, s1, tid);
+    const Stage v0 = stage_load(v, rsk, g, kb, s1, tid), v1 = stage_load(v, rsk, g, kb + STAGE, s1, tid);
+    stage_store(k0, sKV, tid);
+    stage_store(k1, sKV + STAGE * 256, tid);
+    stage_store(v0, sKV + 128 * 256, tid);
+    stage_store(v1, sKV + 128 * 256 + STAGE * 256, tid);
+  }
+  const KvRef kf = sKV + 32 * w * 256, vf = sKV + 128 * 256 + 32 * w * 256;
+#else
   bf16x8 kf[8], vf[8];
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
     kf[c] = kval ? ld8(k + (int64_t)key * rsk + g * D + 16 * c + 8 * hi) : zero8();
     vf[c] = kval ? ld8(v + (int64_t)key * rsk + g * D + 16 * c + 8 * hi) : zero8();
   }
+#endif
   f32x16 dKt[4], dVt[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -304,12 +329,12 @@ __device__ __forceinline__ void attn_bwd_dkdv(const __bf16* __restrict__ q, cons
 __device__ __forceinline__ bool dq_live(int qw, int k0, int s1, int kend) {  // wave-uniform
   return !(qw >= s1 || k0 > qw + TILE - 1 || k0 >= kend);
 }
-__device__ __forceinline__ void dq_scores(const char* tK, const char* tV, const bf16x8* qf, const bf16x8* of, int l32,
-                                          int hi, f32x16& St, f32x16& dPt) {
+__device__ __forceinline__ void dq_scores(const char* tK, const char* tV, KvRef qf, KvRef of, int l32, int hi,
+                                          f32x16& St, f32x16& dPt) {
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
-    St = mfma(row_read(tK, l32, 2 * c + hi), qf[c], St);
-    dPt = mfma(row_read(tV, l32, 2 * c + hi), of[c], dPt);
+    St = mfma(row_read(tK, l32, 2 * c + hi), kv_frag(qf, l32, c, hi), St);
+    dPt = mfma(row_read(tV, l32, 2 * c + hi), kv_frag(of, l32, c, hi), dPt);
   }
 }
 // dS^T in bf16.  MASK = false when every key of the tile is at or below every query of the wave
@@ -334,7 +359,7 @@ __device__ __forceinline__ void dq_acc(const char* tK, int lane, const bf16x8* s
     for (int ks = 0; ks < 2; ++ks) dQt[dc] = mfma(tr_operand(tK, lane, dc, ks), sb[ks], dQt[dc]);
 }
 // one tile, masked
-__device__ __forceinline__ void dq_tile(const char* tK, const char* tV, int k0, const bf16x8* qf, const bf16x8* of,
+__device__ __forceinline__ void dq_tile(const char* tK, const char* tV, int k0, KvRef qf, KvRef of,
                                         int qq, bool qval, int s1, int lane, float c2, float lq, float dq_delta,
                                         f32x16* dQt) {
   const int hi = lane >> 5, l32 = lane & 31;
@@ -345,7 +370,7 @@ __device__ __forceinline__ void dq_tile(const char* tK, const char* tV, int k0, 
   dq_acc(tK, lane, sb, dQt);
 }
 // two unmasked tiles, interleaved as in dkdv_pair
-__device__ __forceinline__ void dq_pair(const char* tK, const char* tV, const bf16x8* qf, const bf16x8* of, int qq,
+__device__ __forceinline__ void dq_pair(const char* tK, const char* tV, KvRef qf, KvRef of, int qq,
                                         bool qval, int s1, int lane, float c2, float lq, float dq_delta, f32x16* dQt) {
   const int hi = lane >> 5, l32 = lane & 31;
   const char *tKb = tK + TILE * 256, *tVb = tV + TILE * 256;
@@ -369,7 +394,7 @@ __device__ __forceinline__ void attn_bwd_dq(const __bf16* __restrict__ q, const 
                                                    const float* __restrict__ lse2, const float* __restrict__ delta,
                                                    const int32_t* __restrict__ items, __bf16* __restrict__ dq,
                                                    int64_t T, int H, int Hkv, float c2, float scale, int it, int h,
-                                                   char* sK, char* sV) {
+                                                   char* sK, char* sV, char* sQO) {
   const int tid = threadIdx.x;
   const int s0 = items[3 * it], s1 = items[3 * it + 1], qb = items[3 * it + 2];
   const int lane = tid & 63, w = tid >> 6, hi = lane >> 5, l32 = lane & 31;
@@ -378,12 +403,24 @@ __device__ __forceinline__ void attn_bwd_dq(const __bf16* __restrict__ q, const 
   const int qw = qb + 32 * w;
   const int qq = qw + l32;
   const bool qval = qq < s1;
+#if PRL_ATTN_KV_LDS
+  {  // the block's 128 Q and dO rows into two swizzled images (visible after the loop's barriers)
+    const Stage q0 = stage_load(q, rs, h, qb, s1, tid), q1 = stage_load(q, rs, h, qb + STAGE, s1, tid);
+    const Stage o0 = stage_load(dout, rs, h, qb, s1, tid), o1 = stage_load(dout, rs, h, qb + STAGE, s1, tid);
+    stage_store(q0, sQO, tid);
+    stage_store(q1, sQO + STAGE * 256, tid);
+    stage_store(o0, sQO + 128 * 256, tid);
+    stage_store(o1, sQO + 128 * 256 + STAGE * 256, tid);
+  }
+  const KvRef qf = sQO + 32 * w * 256, of = sQO + 128 * 256 + 32 * w * 256;
+#else
   bf16x8 qf[8], of[8];
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
     qf[c] = qval ? ld8(q + (int64_t)qq * rs + h * D + 16 * c + 8 * hi) : zero8();
     of[c] = qval ? ld8(dout + (int64_t)qq * rs + h * D + 16 * c + 8 * hi) : zero8();
   }
+#endif
   const float lq = qval ? lse2[(int64_t)h * T + qq] : 0.f;
   const float dq_delta = qval ? delta[(int64_t)h * T + qq] : 0.f;
   f32x16 dQt[4];
@@ -452,13 +489,18 @@ __global__ __launch_bounds__(256) void attn_bwd_fused(const __bf16* __restrict__
                                                       int H, int Hkv, float c2, float scale) {
   __shared__ __attribute__((aligned(16))) char s0[STAGE * D * 2], s1[STAGE * D * 2];
   __shared__ __attribute__((aligned(16))) float sL[STAGE], sDl[STAGE];
+#if PRL_ATTN_KV_LDS
+  __shared__ __attribute__((aligned(16))) char sKV[2 * 128 * D * 2];  // K and V images of the key block
+#else
+  char* sKV = nullptr;
+#endif
   const int b = blockIdx.x;
   if (b < n_kv * Hkv)
     attn_bwd_dkdv(q, k, v, dout, lse2, delta, kv_items, dk, dv, T, H, Hkv, c2, scale, b / Hkv, b % Hkv, s0, s1, sL,
-                  sDl);
+                  sDl, sKV);
   else {
     const int lq = xcd_group_remap(b - n_kv * Hkv, (int)gridDim.x - n_kv * Hkv, H / Hkv);
-    attn_bwd_dq(q, k, v, dout, lse2, delta, q_items, dq, T, H, Hkv, c2, scale, lq / H, lq % H, s0, s1);
+    attn_bwd_dq(q, k, v, dout, lse2, delta, q_items, dq, T, H, Hkv, c2, scale, lq / H, lq % H, s0, s1, sKV);
   }
 }
 

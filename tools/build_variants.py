@@ -23,6 +23,8 @@ VARIANTS = {
     "attn_exp_noload": {"PRL_ATTN_EXP_NOLOAD": "1"},
     "attn_exp_noexp": {"PRL_ATTN_EXP_NOEXP": "1"},
     "attn_exp_noload_noexp": {"PRL_ATTN_EXP_NOLOAD": "1", "PRL_ATTN_EXP_NOEXP": "1"},
+    "attn_kv_regs": {"PRL_ATTN_KV_LDS": "0"},
+    "attn_vgpr_form": {"PRL_ATTN_KV_LDS": "1", "__flags__": "-mllvm --amdgpu-mfma-vgpr-form=1"},
     "norm_dres_early": {"PRL_NORM_WIDE_DRES_EARLY": "1"},
     "norm_grid1536": {"PRL_NORM_GRID": "1536"},
     "norm_grid3072_early": {"PRL_NORM_GRID": "3072", "PRL_NORM_WIDE_DRES_EARLY": "1"},
@@ -34,4 +36,6 @@ if __name__ == "__main__":
     build(force=True)
     names = sys.argv[1:] or list(VARIANTS)
     for n in names:
-        print(build_variant(n, VARIANTS[n]))
+        d = dict(VARIANTS[n])
+        flags = d.pop("__flags__", "").split()
+        print(build_variant(n, d, flags))
