@@ -46,6 +46,7 @@ from .finetune.optim import get_optimizer
 from .finetune.rl import RLConfig, RLStats, rl_step
 from .finetune.rl.utils import aggregate_rl_stats
 from .finetune.sharding import fsdp_requested, set_gradient_sync, shard_model
+from .finetune.trace import PhaseTrace
 from . import native_data
 from .finetune.types import PipelineBatchEncoding, TrainingMetrics
 from .streams import SingleStreamSpec, read_stream, set_streams_backend, write_to_streams
@@ -330,6 +331,8 @@ def rl_finetuning_worker(args, ctx: Dist, model, optimizer, lr_scheduler, grads:
     loss_scale = micro_batch_loss_scale(args, ctx.world, grad_scale_mode)
     native_step = step_fn is rl_step
     defer_stats = os.environ.get("PRL_DEFER_STATS", "1") != "0"  # 0: read them before backward (A/B)
+    trace = PhaseTrace(ctx.device, bool(args.get("trace_gpu_phases", False)) or os.environ.get("PRL_TRACE_GPU") == "1")
+    trace_md: dict[str, float] = {}
 
     def next_batch():
         timeout = 0.1
@@ -347,6 +350,7 @@ def rl_finetuning_worker(args, ctx: Dist, model, optimizer, lr_scheduler, grads:
         if first_pass:
             first_pass = False
             step_start = time.time()
+            trace.start()
         t_wait = time.time()
         batch, ntok, nseq = next_batch()
         sentinel = bool(batch.sentinel)
@@ -377,11 +381,13 @@ def rl_finetuning_worker(args, ctx: Dist, model, optimizer, lr_scheduler, grads:
                                   grad_scale=loss_scale, defer_stats=defer_stats)
         else:
             loss, stats = step_fn(model, batch, metrics.completed_steps, final_steps, rl_config)
+        trace.mark("forward")
         if sentinel:
             loss = loss * 0.0
         elif loss_scale != 1.0:
             loss = loss * loss_scale  # DeepSpeed's engine.backward: loss / gradient_accumulation_steps
         loss.backward()
+        trace.mark("backward")
         if isinstance(stats, RLStats):
             stats = stats.resolve()  # also raises the reference's non-finite assertions
         if not sentinel:
@@ -406,8 +412,10 @@ def rl_finetuning_worker(args, ctx: Dist, model, optimizer, lr_scheduler, grads:
 
         if grads is not None:
             grads.finish()
+        trace.mark("allreduce_wait")
         clip = args.get("gradient_clipping_threshold")
         gn = torch.nn.utils.clip_grad_norm_(model.parameters(), clip if clip else float("inf"))
+        trace.mark("clip")
         if wum is not None:
             wum.poll()  # a failed update (actor error / timeout) ends training here
             wum.before_optimizer_step()
@@ -417,7 +425,9 @@ def rl_finetuning_worker(args, ctx: Dist, model, optimizer, lr_scheduler, grads:
         else:
             optimizer.zero_grad(set_to_none=True)
         lr_scheduler.step()
+        trace.mark("optimizer")
         metrics.grad_norm = float(gn)
+        trace_md = trace.collect()  # the device has just been waited for (grad norm read)
 
         time_to_stop = metrics.completed_steps >= final_steps
         time_to_log = metrics.completed_steps % args.log_each_n_steps == 0
@@ -439,6 +449,7 @@ def rl_finetuning_worker(args, ctx: Dist, model, optimizer, lr_scheduler, grads:
                 avg["rl/ess"] = (avg["rl/ratio_new_old_sum"] ** 2 / avg["rl/ratio_new_old_squared_sum"]
                                  / avg["rl/num_output_tokens_sum"])
             md.update(avg)
+            md.update(trace_md)
             rl_metrics = defaultdict(list)
             lag = {}
             tokens_processed, passes_took, mb_sizes = [], [], []

@@ -182,3 +182,38 @@ def test_grad_scale_convention_follows_the_backend():
     args = Cfg.wrap({"seq_parallel": 1, "gradient_accumulation_passes": 1024})
     assert micro_batch_loss_scale(args, 4, "deepspeed") == 1 / 256
     assert micro_batch_loss_scale(args, 4, "accelerate") == 1.0
+
+
+def test_phase_trace_metrics(tmp_path):
+    """finetune.trace_gpu_phases: per-step trace/<phase>_ms for forward, backward, all-reduce wait,
+    clip and optimizer (summed over the step's micro-batches) and trace/gpu_step_ms in the logged
+    metrics (wall-clock marks on a CPU device, HIP events on a GPU); the phases add up to the step."""
+    exp = tmp_path / "t"
+    exp.mkdir()
+    per_step, _ = _setup(exp, 1)
+    mp.spawn(_rank_main, args=(1, free_port(), str(exp), 1, per_step, {"trace_gpu_phases": True}), nprocs=1, join=True)
+    lines = [json.loads(x) for x in (exp / "finetune" / "logs" / "metrics.jsonl").read_text().splitlines()]
+    keys = {f"trace/{p}_ms" for p in ("forward", "backward", "allreduce_wait", "clip", "optimizer")}
+    assert keys | {"trace/gpu_step_ms"} <= set(lines[-1])
+    parts = sum(lines[-1][k] for k in keys)
+    assert lines[-1]["trace/forward_ms"] > 0 and lines[-1]["trace/backward_ms"] > 0
+    assert parts <= lines[-1]["trace/gpu_step_ms"] + 1e-6
+
+
+def test_phase_trace_unit():
+    from pipelinerl_amd.finetune.trace import PhaseTrace
+
+    t = PhaseTrace(torch.device("cpu"))
+    t.start()
+    for _ in range(3):
+        t.mark("forward")
+        t.mark("backward")
+    t.mark("optimizer")
+    out = t.collect()
+    assert set(out) == {"trace/forward_ms", "trace/backward_ms", "trace/optimizer_ms", "trace/gpu_step_ms"}
+    assert abs(sum(v for k, v in out.items() if k != "trace/gpu_step_ms") - out["trace/gpu_step_ms"]) < 1e-6
+    assert t.collect() == {}  # collect() resets
+    off = PhaseTrace(torch.device("cpu"), enabled=False)
+    off.start()
+    off.mark("forward")
+    assert off.collect() == {}

@@ -65,11 +65,17 @@ def test_trainer_loop_one_gpu(tmp_path):
     reset_streams_backend()
     for k in ("RANK", "WORLD_SIZE", "MASTER_ADDR"):
         os.environ.pop(k, None)
-    cfg = loop_cfg(tmp_path, tmp_path / "tiny_qwen2", 1, 8, 2, load_as_bf16=True, dist_backend=None)
+    cfg = loop_cfg(tmp_path, tmp_path / "tiny_qwen2", 1, 8, 2, load_as_bf16=True, dist_backend=None,
+                   trace_gpu_phases=True)
     m = run_finetuning_loop(cfg)
     assert m.completed_steps == 2 and m.samples == 16
     lines = [json.loads(x) for x in (tmp_path / "finetune" / "logs" / "metrics.jsonl").read_text().splitlines()]
     assert all(np.isfinite(line["rl/loss"]) for line in lines)
+    # HIP-event phase times (finetune/trace.py): every phase measured, within the step's span
+    for line in lines:
+        phases = [line[f"trace/{p}_ms"] for p in ("forward", "backward", "allreduce_wait", "clip", "optimizer")]
+        assert all(v >= 0 for v in phases) and line["trace/forward_ms"] > 0 and line["trace/backward_ms"] > 0
+        assert sum(phases) <= line["trace/gpu_step_ms"] * (1 + 1e-4) + 1e-3
     assert (tmp_path / "finetune" / "current" / "model.safetensors").exists()
 
 
