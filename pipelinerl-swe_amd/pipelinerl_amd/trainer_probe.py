@@ -25,6 +25,9 @@ QWEN = {  # published Qwen2.5 shapes (config.json of each checkpoint)
                num_key_value_heads=4, vocab_size=152064, tie_word_embeddings=False),
     "32b": dict(hidden_size=5120, intermediate_size=27648, num_hidden_layers=64, num_attention_heads=40,
                 num_key_value_heads=8, vocab_size=152064, tie_word_embeddings=False),
+    # tests: the product path (patched ops, HIP attention at head dim 128) on a two-layer model
+    "tiny": dict(hidden_size=512, intermediate_size=1024, num_hidden_layers=2, num_attention_heads=4,
+                 num_key_value_heads=2, vocab_size=512, tie_word_embeddings=True),
 }
 
 
