@@ -241,6 +241,16 @@ int prl_add_rmsnorm_backward(const void* dy, const void* dh, const void* h, cons
 int prl_swiglu_forward(const void* gate, const void* up, void* out, int64_t n, void* stream);
 int prl_swiglu_backward(const void* dout, const void* gate, const void* up, void* dgate, void* dup,
                         int64_t n, void* stream);
+/* The same over [rows, cols] matrices with row strides (elements; cols and strides multiples of 8,
+ * pointers 16-B aligned): gate / up as the column halves of one fused gate_up GEMM output, the
+ * backward writing dgate / dup into the halves of one [rows, 2 cols] buffer.  Bit-identical to
+ * the contiguous forms.  Replaces Qwen2MLP's act_fn(gate_proj(x)) * up_proj(x) (transformers
+ * modeling_qwen2.py) run inside the reference's model forward (finetune_loop.py:620-629). */
+int prl_swiglu_forward_rows(const void* gate, const void* up, void* out, int64_t rows, int64_t cols,
+                            int64_t ld_gate, int64_t ld_up, int64_t ld_out, void* stream);
+int prl_swiglu_backward_rows(const void* dout, const void* gate, const void* up, void* dgate, void* dup,
+                             int64_t rows, int64_t cols, int64_t ld_dout, int64_t ld_gate, int64_t ld_up,
+                             int64_t ld_dgate, int64_t ld_dup, void* stream);
 /* q [tokens, hq, d], k [tokens, hkv, d] token-major; cos / sin [tokens, d] (HF layout:
  * halves repeated).  Out-of-place; backward applies the transposed rotation. */
 int prl_rope_forward(const void* q, const void* k, const void* cos, const void* sin, void* q_out,

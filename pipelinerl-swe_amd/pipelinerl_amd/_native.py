@@ -92,6 +92,10 @@ _SIGNATURES = {
                                          c_void_p, c_size_t, c_int64, c_int64, c_void_p]),
     "prl_swiglu_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     "prl_swiglu_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
+    "prl_swiglu_forward_rows": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64,
+                                        c_void_p]),
+    "prl_swiglu_backward_rows": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64,
+                                         c_int64, c_int64, c_int64, c_int64, c_void_p]),
     "prl_rope_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32,
                                  c_int32, c_int32, c_void_p]),
     "prl_rope_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32,

@@ -429,6 +429,71 @@ __global__ __launch_bounds__(256) void swiglu_bwd(const u32x4* __restrict__ dh, 
   }
 }
 
+// Row-strided SwiGLU for the fused gate/up GEMM (finetune/model_ops.py GateUpSwiGLUFn): gate and up
+// are the two column halves of one [rows, 2 I] GEMM output (row stride ld, 8-element vectors), the
+// backward writes dgate / dup into the two halves of one [rows, 2 I] buffer, which the fused dgrad
+// and wgrad GEMMs read as they stand.  Same per-element arithmetic as swiglu_fwd / swiglu_bwd
+// (bit-identical outputs).  Grid-stride over rows; a row's vectors over the block, SWIGLU_UNROLL
+// (bwd: 2) vectors in flight per thread.
+__global__ __launch_bounds__(256) void swiglu_fwd_rows(const u32x4* __restrict__ g, const u32x4* __restrict__ u,
+                                                       u32x4* __restrict__ h, int64_t rows, int cols8, int64_t ldg,
+                                                       int64_t ldu, int64_t ldh) {
+  constexpr int U = SWIGLU_UNROLL;
+  for (int64_t r = blockIdx.x; r < rows; r += gridDim.x) {
+    const u32x4 *gr = g + r * ldg, *ur = u + r * ldu;
+    u32x4* hr = h + r * ldh;
+    int c = threadIdx.x;
+    for (; c + (U - 1) * 256 < cols8; c += U * 256) {
+      u32x4 gv[U], uv[U];
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        gv[k] = __builtin_nontemporal_load(gr + c + k * 256);
+        uv[k] = __builtin_nontemporal_load(ur + c + k * 256);
+      }
+#pragma unroll
+      for (int k = 0; k < U; ++k) __builtin_nontemporal_store(swiglu_vec(gv[k], uv[k]), hr + c + k * 256);
+    }
+    for (; c < cols8; c += 256)
+      __builtin_nontemporal_store(swiglu_vec(__builtin_nontemporal_load(gr + c), __builtin_nontemporal_load(ur + c)),
+                                  hr + c);
+  }
+}
+__global__ __launch_bounds__(256) void swiglu_bwd_rows(const u32x4* __restrict__ dh, const u32x4* __restrict__ g,
+                                                       const u32x4* __restrict__ u, u32x4* __restrict__ dg,
+                                                       u32x4* __restrict__ du, int64_t rows, int cols8, int64_t lddh,
+                                                       int64_t ldg, int64_t ldu, int64_t lddg, int64_t lddu) {
+  constexpr int U = SWIGLU_UNROLL > 2 ? 2 : SWIGLU_UNROLL;
+  for (int64_t r = blockIdx.x; r < rows; r += gridDim.x) {
+    const u32x4 *dr = dh + r * lddh, *gr = g + r * ldg, *ur = u + r * ldu;
+    u32x4 *dgr = dg + r * lddg, *dur = du + r * lddu;
+    int c = threadIdx.x;
+    for (; c + (U - 1) * 256 < cols8; c += U * 256) {
+      u32x4 dv[U], gv[U], uv[U];
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        dv[k] = __builtin_nontemporal_load(dr + c + k * 256);
+        gv[k] = __builtin_nontemporal_load(gr + c + k * 256);
+        uv[k] = __builtin_nontemporal_load(ur + c + k * 256);
+      }
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        u32x4 og, ou;
+        swiglu_bwd_vec(dv[k], gv[k], uv[k], og, ou);
+        __builtin_nontemporal_store(og, dgr + c + k * 256);
+        __builtin_nontemporal_store(ou, dur + c + k * 256);
+      }
+    }
+    for (; c < cols8; c += 256) {
+      u32x4 og, ou;
+      swiglu_bwd_vec(__builtin_nontemporal_load(dr + c), __builtin_nontemporal_load(gr + c),
+                     __builtin_nontemporal_load(ur + c), og, ou);
+      __builtin_nontemporal_store(og, dgr + c);
+      __builtin_nontemporal_store(ou, dur + c);
+    }
+  }
+}
+
+
 // ---------------------------------------------------------------------------------------
 // RoPE on q [T, Hq, D] and k [T, Hkv, D] (token-major, contiguous), cos / sin [T, D].
 // One thread per (token, head, 4 rotation pairs).  dir = +1 forward, -1 backward
@@ -635,6 +700,38 @@ int prl_swiglu_backward(const void* dout, const void* gate, const void* up, void
   const int64_t n8 = n / 8;
   hipLaunchKernelGGL(swiglu_bwd, dim3(ew_grid(n8)), dim3(256), 0, static_cast<hipStream_t>(stream),
                      (const u32x4*)dout, (const u32x4*)gate, (const u32x4*)up, (u32x4*)dgate, (u32x4*)dup, n8);
+  return (int)hipGetLastError();
+}
+
+static int rows_grid(int64_t rows) { return (int)(rows < 2048 ? (rows > 0 ? rows : 1) : 2048); }
+
+int prl_swiglu_forward_rows(const void* gate, const void* up, void* out, int64_t rows, int64_t cols, int64_t ld_gate,
+                            int64_t ld_up, int64_t ld_out, void* stream) {
+  if (!gate || !up || !out || rows < 0 || cols < 0 || ld_gate < cols || ld_up < cols || ld_out < cols)
+    return PRL_E_INVALID;
+  if (cols % 8 || ld_gate % 8 || ld_up % 8 || ld_out % 8 || !a16(gate) || !a16(up) || !a16(out) ||
+      cols / 8 > 0x7FFFFFFF)
+    return PRL_E_UNSUPPORTED;
+  if (rows == 0 || cols == 0) return PRL_OK;
+  hipLaunchKernelGGL(swiglu_fwd_rows, dim3(rows_grid(rows)), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     (const u32x4*)gate, (const u32x4*)up, (u32x4*)out, rows, (int)(cols / 8), ld_gate / 8, ld_up / 8,
+                     ld_out / 8);
+  return (int)hipGetLastError();
+}
+
+int prl_swiglu_backward_rows(const void* dout, const void* gate, const void* up, void* dgate, void* dup, int64_t rows,
+                             int64_t cols, int64_t ld_dout, int64_t ld_gate, int64_t ld_up, int64_t ld_dgate,
+                             int64_t ld_dup, void* stream) {
+  if (!dout || !gate || !up || !dgate || !dup || rows < 0 || cols < 0 || ld_dout < cols || ld_gate < cols ||
+      ld_up < cols || ld_dgate < cols || ld_dup < cols)
+    return PRL_E_INVALID;
+  if (cols % 8 || ld_dout % 8 || ld_gate % 8 || ld_up % 8 || ld_dgate % 8 || ld_dup % 8 || !a16(dout) ||
+      !a16(gate) || !a16(up) || !a16(dgate) || !a16(dup) || cols / 8 > 0x7FFFFFFF)
+    return PRL_E_UNSUPPORTED;
+  if (rows == 0 || cols == 0) return PRL_OK;
+  hipLaunchKernelGGL(swiglu_bwd_rows, dim3(rows_grid(rows)), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     (const u32x4*)dout, (const u32x4*)gate, (const u32x4*)up, (u32x4*)dgate, (u32x4*)dup, rows,
+                     (int)(cols / 8), ld_dout / 8, ld_gate / 8, ld_up / 8, ld_dgate / 8, ld_dup / 8);
   return (int)hipGetLastError();
 }
 

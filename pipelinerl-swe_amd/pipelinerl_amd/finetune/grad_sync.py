@@ -42,7 +42,11 @@ class GradBuckets:
         self.buckets: list[_Bucket] = []
         cur: list[torch.Tensor] = []
         cur_bytes = 0
-        for p in reversed(params):
+        order = list(reversed(params))  # roughly the order the backward produces them
+        for i in range(len(order) - 1):  # a parameter that must follow another (fused GEMM rows)
+            if getattr(order[i], "_prl_follows", None) is order[i + 1]:
+                order[i], order[i + 1] = order[i + 1], order[i]
+        for p in order:
             nbytes = p.numel() * p.element_size()
             if cur and (cur_bytes + nbytes > bucket_bytes or p.dtype != cur[0].dtype or p.device != cur[0].device):
                 self._make(cur)

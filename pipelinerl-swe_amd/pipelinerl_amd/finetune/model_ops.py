@@ -217,6 +217,122 @@ def _wgrad(dy, x, w):
     return gemm.linear_wgrad(dy, x)
 
 
+# Fused gate/up projection: one GEMM over the concatenated [2 I, H] weight instead of two over
+# [I, H] (7B at 8 192 tokens through prl_gemm: forward 1.82 -> 1.53 ms, dgrad 1.93 -> 1.65 ms,
+# wgrad 1.66 -> 1.58 ms per layer, tools/fused_proj_bench.py, profiles/r02_fused_proj_bench.jsonl).  The weights stay separate Parameters; the
+# concatenation is cached and rebuilt only when a member's version counter moves (once per
+# optimizer step).  Off under FSDP (shard_model) and with PRL_FUSED_GATE_UP=0 (A/B).
+_FUSED_GATE_UP = os.environ.get("PRL_FUSED_GATE_UP", "1") != "0"
+# Used up to this many tokens per micro-batch: the fused [2 I, H] shape runs the library heuristic
+# (no swept solution), which wins at C3's <= 12 000-token micro-batches (7B step 1539 -> 1527 ms,
+# profiles/r02_fused_gate_up_ab.jsonl) and loses at 65 536 (1.5B C2 step 1211 -> 1225 ms)
+_FUSED_GATE_UP_MAX_ROWS = int(os.environ.get("PRL_FUSED_GATE_UP_MAX_ROWS", "12288"))
+
+
+def disable_fused_projections() -> None:
+    global _FUSED_GATE_UP
+    _FUSED_GATE_UP = False
+
+
+def _fused_weight(holder, ws) -> torch.Tensor:
+    """cat(ws) cached on the module ``holder`` (so it lives and dies with the model), rebuilt when
+    a member's version counter or storage changes."""
+    ver = tuple(w._version for w in ws) + tuple(w.data_ptr() for w in ws)
+    hit = holder.__dict__.get("_prl_fused_w")
+    if hit is not None and hit[0] == ver:
+        return hit[1]
+    with torch.no_grad():
+        wf = torch.cat([w.detach() for w in ws])
+    holder.__dict__["_prl_fused_w"] = (ver, wf)
+    return wf
+
+
+def _adjacent_grads(gs) -> torch.Tensor | None:
+    """The [sum N, K] view over gradient tensors that sit back to back in one storage, else None."""
+    if any(g is None for g in gs):
+        return None
+    K = gs[0].shape[1]
+    for a, b in zip(gs, gs[1:]):
+        if (b.untyped_storage().data_ptr() != a.untyped_storage().data_ptr() or b.shape[1] != K
+                or b.storage_offset() != a.storage_offset() + a.numel()):
+            return None
+    return torch.as_strided(gs[0], (sum(g.shape[0] for g in gs), K), (K, 1))
+
+
+def _wgrad_group(dy, x, params):
+    """Weight gradients of layers fused along N (dW = dY^T X, one GEMM): added in the GEMM into
+    their .grad when those sit back to back (and no hook is due), else returned as row blocks of
+    one [sum N, K] tensor for autograd to accumulate."""
+    targets = [_accum_target(p) for p in params]
+    if all(t is not None for t in targets):
+        G = _adjacent_grads(targets)
+        if G is not None and G.data_ptr() % 16 == 0:
+            gemm.linear_wgrad(dy, x, out=G, accumulate=True)
+            return [None] * len(params)
+    dW = gemm.linear_wgrad(dy, x)
+    if (_FUSE_GRAD_ACCUM and all(isinstance(p, torch.nn.Parameter) and p.grad is None
+                                 and not p._post_accumulate_grad_hooks for p in params)):
+        # the step's first micro-batch: the gradients become row blocks of dW, so the next
+        # micro-batches find them back to back (what AccumulateGrad would store: dW itself)
+        a = 0
+        for p in params:
+            p.grad = dW[a:a + p.shape[0]]
+            a += p.shape[0]
+        return [None] * len(params)
+    out, a = [], 0
+    for p in params:
+        out.append(dW[a:a + p.shape[0]])
+        a += p.shape[0]
+    return out
+
+
+class GateUpSwiGLUFn(torch.autograd.Function):
+    """h = bf16(silu(x Wg^T)) * (x Wu^T) with gate and up as one GEMM over cat(Wg, Wu) (bias-free
+    layers, Qwen2MLP): the GEMM output [T, 2 I] feeds the row-strided SwiGLU kernel; the backward
+    writes dgate / dup into one [T, 2 I] buffer for one dgrad and one wgrad GEMM.  Saves x and
+    the GEMM output (what the separate form saves: x, gate, up)."""
+
+    @staticmethod
+    def forward(ctx, x, wg, wu, holder):
+        I, H = wg.shape
+        wf = _fused_weight(holder, (wg, wu))
+        x2 = x.reshape(-1, H)
+        rows = x2.shape[0]
+        gu = gemm.linear_fwd(x2, wf, solution=_fused_solution("fwd", rows, 2 * I, H))
+        h = torch.empty((rows, I), dtype=x.dtype, device=x.device)
+        _native.check(_native.load().prl_swiglu_forward_rows(gu.data_ptr(), gu.data_ptr() + 2 * I, h.data_ptr(), rows,
+                                                             I, 2 * I, 2 * I, I, _stream(x)),
+                      "prl_swiglu_forward_rows")
+        ctx.save_for_backward(x2, gu, wf)
+        ctx.params = (wg, wu)
+        ctx.shape = x.shape
+        return h.view(*x.shape[:-1], I)
+
+    @staticmethod
+    def backward(ctx, dh):
+        x2, gu, wf = ctx.saved_tensors
+        wg, wu = ctx.params
+        I = wg.shape[0]
+        rows = x2.shape[0]
+        dh = dh.reshape(rows, I)
+        dh = dh if dh.is_contiguous() else dh.contiguous()
+        dgu = torch.empty_like(gu)
+        _native.check(_native.load().prl_swiglu_backward_rows(dh.data_ptr(), gu.data_ptr(), gu.data_ptr() + 2 * I,
+                                                              dgu.data_ptr(), dgu.data_ptr() + 2 * I, rows, I, I,
+                                                              2 * I, 2 * I, 2 * I, 2 * I, _stream(dh)),
+                      "prl_swiglu_backward_rows")
+        dx = gemm.linear_dgrad(dgu, wf) if ctx.needs_input_grad[0] else None
+        dwg = dwu = None
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            dwg, dwu = _wgrad_group(dgu, x2, (wg, wu))
+        return (dx.view(ctx.shape) if dx is not None else None), dwg, dwu, None
+
+
+def _fused_solution(pas: str, T: int, N: int, K: int) -> int:
+    sol = gemm.solution_for(pas, T, N, K)
+    return -1 if sol is None else sol  # -1: the ROCm 7.2 library heuristic (measured, fused_proj_bench)
+
+
 class PrlLinearFn(torch.autograd.Function):
     """F.linear whose GEMMs run through prl_gemm (the ROCm hipBLASLt, include/prl_gemm.h).
 
@@ -349,6 +465,12 @@ def _rmsnorm_forward(self, hidden_states):
 
 def _mlp_forward(self, x):
     gp, up = self.gate_proj, self.up_proj
+    if (_FUSED_GATE_UP and x.numel() // max(1, x.shape[-1]) <= _FUSED_GATE_UP_MAX_ROWS
+            and getattr(gp, "_prl_linear", False) and getattr(up, "_prl_linear", False)
+            and gp.bias is None and up.bias is None and gp.weight.shape == up.weight.shape
+            and gp.weight.shape[0] % 8 == 0 and _linear_ok(x, gp.weight) and _linear_ok(x, up.weight)
+            and x.data_ptr() % 16 == 0):
+        return self.down_proj(GateUpSwiGLUFn.apply(x, gp.weight, up.weight, self))
     if getattr(gp, "_prl_linear", False) and getattr(up, "_prl_linear", False) and _linear_ok(x, gp.weight) \
             and _linear_ok(x, up.weight):
         g, u = SharedInputLinearFn.apply(x, gp.weight, gp.bias, up.weight, up.bias)
@@ -464,6 +586,9 @@ def patch_model(model) -> dict:
         elif (name.endswith("MLP") and all(hasattr(m, a) for a in ("gate_proj", "up_proj", "down_proj"))
               and type(getattr(m, "act_fn", None)).__name__ in _SILU):
             m.forward = types.MethodType(_mlp_forward, m)
+            # gate and up gradients side by side in gradient buckets (finetune/grad_sync.py), in
+            # the fused GEMM's row order, so GateUpSwiGLUFn can add into both in one wgrad GEMM
+            m.up_proj.weight._prl_follows = m.gate_proj.weight
             n_mlp += 1
         elif name.endswith("Attention"):
             mods.add(type(m).__module__)

@@ -51,9 +51,10 @@ def shard_model(model, fsdp_cfg=None, grad_reduce: str = "mean", reshard_after_f
     from torch.distributed.device_mesh import init_device_mesh
     from torch.distributed.fsdp import MixedPrecisionPolicy, fully_shard
 
-    from .model_ops import disable_fused_grad_accumulation
+    from .model_ops import disable_fused_grad_accumulation, disable_fused_projections
 
     disable_fused_grad_accumulation()  # FSDP2 owns the unsharded gradients: autograd accumulates them
+    disable_fused_projections()  # and re-gathers the weights every forward: no concatenation cache
     dev = next(model.parameters()).device
     mesh = init_device_mesh(dev.type, (dist.get_world_size(),))
     fsdp_cfg = fsdp_cfg or {}

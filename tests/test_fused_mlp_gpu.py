@@ -1,0 +1,80 @@
+"""The fused gate/up projection (finetune/model_ops.py GateUpSwiGLUFn: one GEMM over cat(Wg, Wu),
+row-strided SwiGLU kernels prl_swiglu_forward_rows / _backward_rows) against the separate form it
+replaces (two GEMMs + contiguous SwiGLU), on the GPU."""
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _bits(t):
+    return t.contiguous().view(torch.int16)
+
+
+def test_swiglu_rows_bit_exact_to_contiguous():
+    """Row-strided kernels == the contiguous kernels on the same values (gate / up as the two
+    halves of a [rows, 2 I] buffer; dgate / dup written into the halves of another)."""
+    from pipelinerl_amd import _native
+
+    lib = _native.load()
+    st = torch.cuda.current_stream().cuda_stream
+    g = torch.Generator(device=DEV).manual_seed(3)
+    rows, I = 333, 1128  # I / 8 = 141 vectors: a ragged tail of the unrolled loop
+    gu = (torch.randn((rows, 2 * I), generator=g, device=DEV) * 3).to(torch.bfloat16)
+    dh = torch.randn((rows, I), generator=g, device=DEV).to(torch.bfloat16)
+    gate, up = gu[:, :I].contiguous(), gu[:, I:].contiguous()
+    h_ref = torch.empty_like(gate)
+    _native.check(lib.prl_swiglu_forward(gate.data_ptr(), up.data_ptr(), h_ref.data_ptr(), gate.numel(), st), "fwd")
+    h = torch.empty_like(gate)
+    _native.check(lib.prl_swiglu_forward_rows(gu.data_ptr(), gu.data_ptr() + 2 * I, h.data_ptr(), rows, I, 2 * I,
+                                              2 * I, I, st), "fwd rows")
+    assert torch.equal(_bits(h), _bits(h_ref))
+    dg_ref, du_ref = torch.empty_like(gate), torch.empty_like(up)
+    _native.check(lib.prl_swiglu_backward(dh.data_ptr(), gate.data_ptr(), up.data_ptr(), dg_ref.data_ptr(),
+                                          du_ref.data_ptr(), gate.numel(), st), "bwd")
+    dgu = torch.empty_like(gu)
+    _native.check(lib.prl_swiglu_backward_rows(dh.data_ptr(), gu.data_ptr(), gu.data_ptr() + 2 * I, dgu.data_ptr(),
+                                               dgu.data_ptr() + 2 * I, rows, I, I, 2 * I, 2 * I, 2 * I, 2 * I, st),
+                  "bwd rows")
+    assert torch.equal(_bits(dgu[:, :I]), _bits(dg_ref)) and torch.equal(_bits(dgu[:, I:]), _bits(du_ref))
+    # argument checks before any launch
+    assert lib.prl_swiglu_forward_rows(gu.data_ptr(), gu.data_ptr(), h.data_ptr(), rows, I, I - 8, I, I, st) == 1001
+    assert lib.prl_swiglu_forward_rows(gu.data_ptr(), gu.data_ptr(), h.data_ptr(), rows, I + 4, 2 * I, 2 * I, 2 * I,
+                                       st) != 0
+
+
+def test_fused_gate_up_matches_separate(monkeypatch):
+    """GateUpSwiGLUFn == SharedInputLinearFn + SwiGLUFn over three micro-batches: the output to
+    bf16 GEMM rounding, dx likewise, the accumulated weight gradients likewise; after the first
+    micro-batch the two gradients are row blocks of one buffer (later micro-batches add into them in
+    the wgrad GEMM); a weight update invalidates the cached concatenation."""
+    from pipelinerl_amd.finetune import model_ops
+
+    g = torch.Generator(device=DEV).manual_seed(5)
+    T, H, I = 1000, 512, 1408
+    holder = torch.nn.Module()
+    wg = torch.nn.Parameter((torch.randn((I, H), generator=g, device=DEV) * 0.05).to(torch.bfloat16))
+    wu = torch.nn.Parameter((torch.randn((I, H), generator=g, device=DEV) * 0.05).to(torch.bfloat16))
+    wg2, wu2 = (torch.nn.Parameter(w.detach().clone()) for w in (wg, wu))
+    xs = [(torch.randn((1, T, H), generator=g, device=DEV)).to(torch.bfloat16) for _ in range(3)]
+    dys = [torch.randn((1, T, I), generator=g, device=DEV).to(torch.bfloat16) for _ in range(3)]
+    for i, (x, dy) in enumerate(zip(xs, dys)):
+        xa, xb = x.clone().requires_grad_(), x.clone().requires_grad_()
+        ha = model_ops.GateUpSwiGLUFn.apply(xa, wg, wu, holder)
+        gsep, usep = model_ops.SharedInputLinearFn.apply(xb, wg2, None, wu2, None)
+        hb = model_ops.SwiGLUFn.apply(gsep, usep)
+        assert (ha.float() - hb.float()).abs().max() <= 2e-2 * hb.float().abs().max()
+        ha.backward(dy)
+        hb.backward(dy)
+        assert (xa.grad.float() - xb.grad.float()).abs().max() <= 2e-2 * xb.grad.float().abs().max()
+        if i == 0:  # the gradients are row blocks of one [2 I, H] buffer from here on
+            assert wu.grad.data_ptr() == wg.grad.data_ptr() + wg.grad.numel() * 2
+    for a, b in ((wg, wg2), (wu, wu2)):
+        assert (a.grad.float() - b.grad.float()).abs().max() <= 2e-2 * b.grad.float().abs().max()
+    wf = holder.__dict__["_prl_fused_w"][1]
+    assert torch.equal(wf, torch.cat([wg.detach(), wu.detach()]))
+    with torch.no_grad():
+        wg.add_(1.0)  # an optimizer-style in-place update bumps the version: the cache is rebuilt
+    assert torch.equal(model_ops._fused_weight(holder, (wg, wu)), torch.cat([wg.detach(), wu.detach()]))

@@ -132,7 +132,10 @@ def test_linear_wgrad_accumulates_in_the_gemm(tmp_path, monkeypatch):
         if getattr(f, "_prl_fused", False):
             mq.apply_rotary_pos_emb = f._prl_orig
     nl = base.config.num_hidden_layers
-    assert sum(calls) == 2 * (7 * nl + 1)  # micro-batches 2 and 3: q k v o gate up down per layer + lm_head
+    from pipelinerl_amd.finetune import model_ops
+
+    per_layer = 6 if model_ops._FUSED_GATE_UP else 7  # q k v o down + gate_up (one fused GEMM) or gate, up
+    assert sum(calls) == 2 * (per_layer * nl + 1)  # micro-batches 2 and 3, + lm_head
     _compare(ref, got)
 
 
