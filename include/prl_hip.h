@@ -255,6 +255,11 @@ int prl_swiglu_backward_rows(const void* dout, const void* gate, const void* up,
  * halves repeated).  Out-of-place; backward applies the transposed rotation. */
 int prl_rope_forward(const void* q, const void* k, const void* cos, const void* sin, void* q_out,
                      void* k_out, int64_t tokens, int32_t hq, int32_t hkv, int32_t d, void* stream);
+/* prl_rope_forward with the inputs' token strides given (elements, multiples of 4): q and k read
+ * as column ranges of one fused q/k/v projection output [tokens, ld] (outputs contiguous). */
+int prl_rope_forward_strided(const void* q, const void* k, const void* cos, const void* sin, void* q_out,
+                             void* k_out, int64_t tokens, int32_t hq, int32_t hkv, int32_t d, int64_t ld_q,
+                             int64_t ld_k, void* stream);
 int prl_rope_backward(const void* dq_out, const void* dk_out, const void* cos, const void* sin,
                       void* dq, void* dk, int64_t tokens, int32_t hq, int32_t hkv, int32_t d,
                       void* stream);

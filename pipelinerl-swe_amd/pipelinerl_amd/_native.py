@@ -98,6 +98,8 @@ _SIGNATURES = {
                                          c_int64, c_int64, c_int64, c_int64, c_void_p]),
     "prl_rope_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32,
                                  c_int32, c_int32, c_void_p]),
+    "prl_rope_forward_strided": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32,
+                                         c_int32, c_int32, c_int64, c_int64, c_void_p]),
     "prl_rope_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32,
                                   c_int32, c_int32, c_void_p]),
     "prl_attn_bwd_preprocess": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int64, c_void_p, c_void_p,

@@ -502,7 +502,7 @@ template <int DIR>
 __global__ __launch_bounds__(256) void rope_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
                                                    const uint16_t* __restrict__ cs, const uint16_t* __restrict__ sn,
                                                    uint16_t* __restrict__ qo, uint16_t* __restrict__ ko,
-                                                   int64_t tokens, int hq, int hkv, int D) {
+                                                   int64_t tokens, int hq, int hkv, int D, int64_t ldq, int64_t ldk) {
   const int half = D >> 1, chunks = half >> 2;  // 4 pairs per thread
   const int per_tok = (hq + hkv) * chunks;
   const int64_t total = tokens * per_tok;
@@ -512,7 +512,7 @@ __global__ __launch_bounds__(256) void rope_kernel(const uint16_t* __restrict__ 
     const int rem = (int)(idx - t * per_tok);
     const int h = rem / chunks, c = rem - h * chunks;
     const bool isq = h < hq;
-    const uint16_t* src = isq ? q + (t * hq + h) * D : k + (t * hkv + (h - hq)) * D;
+    const uint16_t* src = isq ? q + t * ldq + h * D : k + t * ldk + (h - hq) * D;  // token strides (fused qkv)
     uint16_t* dst = isq ? qo + (t * hq + h) * D : ko + (t * hkv + (h - hq)) * D;
     const int i = c * 4;
     const u32x2 x1 = *reinterpret_cast<const u32x2*>(src + i), x2 = *reinterpret_cast<const u32x2*>(src + half + i);
@@ -736,9 +736,15 @@ int prl_swiglu_backward_rows(const void* dout, const void* gate, const void* up,
 }
 
 static int rope_launch(int dir, const void* q, const void* k, const void* cs, const void* sn, void* qo, void* ko,
-                       int64_t tokens, int32_t hq, int32_t hkv, int32_t d, void* stream) {
-  if (!q || !k || !cs || !sn || !qo || !ko || tokens < 0 || hq <= 0 || hkv < 0 || d <= 0) return PRL_E_INVALID;
-  if (d % 8 || !a8(q) || !a8(k) || !a8(cs) || !a8(sn) || !a8(qo) || !a8(ko)) return PRL_E_UNSUPPORTED;
+                       int64_t tokens, int32_t hq, int32_t hkv, int32_t d, void* stream, int64_t ldq = -1,
+                       int64_t ldk = -1) {
+  if (ldq < 0) ldq = (int64_t)hq * d;
+  if (ldk < 0) ldk = (int64_t)hkv * d;
+  if (!q || !k || !cs || !sn || !qo || !ko || tokens < 0 || hq <= 0 || hkv < 0 || d <= 0 || ldq < (int64_t)hq * d ||
+      ldk < (int64_t)hkv * d)
+    return PRL_E_INVALID;
+  if (d % 8 || ldq % 4 || ldk % 4 || !a8(q) || !a8(k) || !a8(cs) || !a8(sn) || !a8(qo) || !a8(ko))
+    return PRL_E_UNSUPPORTED;
   if (tokens == 0) return PRL_OK;
   const int64_t total = tokens * (int64_t)(hq + hkv) * (d / 8);
   const int64_t g = (total + 255) / 256;
@@ -746,11 +752,19 @@ static int rope_launch(int dir, const void* q, const void* k, const void* cs, co
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (dir > 0)
     hipLaunchKernelGGL(rope_kernel<1>, dim3(grid), dim3(256), 0, s, (const uint16_t*)q, (const uint16_t*)k,
-                       (const uint16_t*)cs, (const uint16_t*)sn, (uint16_t*)qo, (uint16_t*)ko, tokens, hq, hkv, d);
+                       (const uint16_t*)cs, (const uint16_t*)sn, (uint16_t*)qo, (uint16_t*)ko, tokens, hq, hkv, d, ldq,
+                       ldk);
   else
     hipLaunchKernelGGL(rope_kernel<-1>, dim3(grid), dim3(256), 0, s, (const uint16_t*)q, (const uint16_t*)k,
-                       (const uint16_t*)cs, (const uint16_t*)sn, (uint16_t*)qo, (uint16_t*)ko, tokens, hq, hkv, d);
+                       (const uint16_t*)cs, (const uint16_t*)sn, (uint16_t*)qo, (uint16_t*)ko, tokens, hq, hkv, d, ldq,
+                       ldk);
   return (int)hipGetLastError();
+}
+
+int prl_rope_forward_strided(const void* q, const void* k, const void* cos, const void* sin, void* q_out,
+                             void* k_out, int64_t tokens, int32_t hq, int32_t hkv, int32_t d, int64_t ld_q,
+                             int64_t ld_k, void* stream) {
+  return rope_launch(1, q, k, cos, sin, q_out, k_out, tokens, hq, hkv, d, stream, ld_q, ld_k);
 }
 
 int prl_rope_forward(const void* q, const void* k, const void* cos, const void* sin, void* q_out, void* k_out,

@@ -43,9 +43,11 @@ class GradBuckets:
         cur: list[torch.Tensor] = []
         cur_bytes = 0
         order = list(reversed(params))  # roughly the order the backward produces them
-        for i in range(len(order) - 1):  # a parameter that must follow another (fused GEMM rows)
-            if getattr(order[i], "_prl_follows", None) is order[i + 1]:
-                order[i], order[i + 1] = order[i + 1], order[i]
+        for p in params:  # a parameter that must sit right after another (rows of one fused GEMM)
+            f = getattr(p, "_prl_follows", None)
+            if f is not None and any(q is f for q in order):
+                order.pop(next(i for i, q in enumerate(order) if q is p))  # by identity (tensor == is elementwise)
+                order.insert(next(i for i, q in enumerate(order) if q is f) + 1, p)
         for p in order:
             nbytes = p.numel() * p.element_size()
             if cur and (cur_bytes + nbytes > bucket_bytes or p.dtype != cur[0].dtype or p.device != cur[0].device):

@@ -154,11 +154,13 @@ class RopeFn(torch.autograd.Function):
     def forward(ctx, q, k, cos, sin):
         B, hq, T, D = q.shape
         hkv = k.shape[1]
-        qt, kt = q.transpose(1, 2), k.transpose(1, 2)  # contiguous [B, T, H, D]
-        qo, ko = torch.empty_like(qt), torch.empty_like(kt)
-        _native.check(_native.load().prl_rope_forward(qt.data_ptr(), kt.data_ptr(), cos.data_ptr(), sin.data_ptr(),
-                                                      qo.data_ptr(), ko.data_ptr(), B * T, hq, hkv, D, _stream(q)),
-                      "prl_rope_forward")
+        qt, kt = q.transpose(1, 2), k.transpose(1, 2)  # [B, T, H, D]: contiguous, or token-strided (fused qkv)
+        qo = torch.empty((B, T, hq, D), dtype=q.dtype, device=q.device)
+        ko = torch.empty((B, T, hkv, D), dtype=k.dtype, device=k.device)
+        _native.check(_native.load().prl_rope_forward_strided(qt.data_ptr(), kt.data_ptr(), cos.data_ptr(),
+                                                              sin.data_ptr(), qo.data_ptr(), ko.data_ptr(), B * T, hq,
+                                                              hkv, D, qt.stride(1), kt.stride(1), _stream(q)),
+                      "prl_rope_forward_strided")
         ctx.save_for_backward(cos, sin)
         ctx.dims = (B, T, hq, hkv, D)
         return qo.transpose(1, 2), ko.transpose(1, 2)
@@ -230,20 +232,20 @@ _FUSED_GATE_UP_MAX_ROWS = int(os.environ.get("PRL_FUSED_GATE_UP_MAX_ROWS", "1228
 
 
 def disable_fused_projections() -> None:
-    global _FUSED_GATE_UP
-    _FUSED_GATE_UP = False
+    global _FUSED_GATE_UP, _FUSED_QKV
+    _FUSED_GATE_UP = _FUSED_QKV = False
 
 
-def _fused_weight(holder, ws) -> torch.Tensor:
+def _fused_weight(holder, ws, slot: str = "_prl_fused_w") -> torch.Tensor:
     """cat(ws) cached on the module ``holder`` (so it lives and dies with the model), rebuilt when
     a member's version counter or storage changes."""
     ver = tuple(w._version for w in ws) + tuple(w.data_ptr() for w in ws)
-    hit = holder.__dict__.get("_prl_fused_w")
+    hit = holder.__dict__.get(slot)
     if hit is not None and hit[0] == ver:
         return hit[1]
     with torch.no_grad():
         wf = torch.cat([w.detach() for w in ws])
-    holder.__dict__["_prl_fused_w"] = (ver, wf)
+    holder.__dict__[slot] = (ver, wf)
     return wf
 
 
@@ -326,6 +328,59 @@ class GateUpSwiGLUFn(torch.autograd.Function):
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
             dwg, dwu = _wgrad_group(dgu, x2, (wg, wu))
         return (dx.view(ctx.shape) if dx is not None else None), dwg, dwu, None
+
+
+# Fused q/k/v projection: one GEMM over cat(Wq, Wk, Wv) (+ the concatenated bias in the epilogue)
+# instead of three (7B 8 k tokens 0.97 -> 0.75 ms per layer fwd + dgrad + wgrad alone,
+# profiles/r02_fused_proj_bench.jsonl).  q / k / v leave as column ranges of the [T, Nq + 2 Nkv]
+# output (RoPE reads them strided); the backward concatenates their gradients for one dgrad and one
+# wgrad GEMM.  OFF by default (PRL_FUSED_QKV=1 turns it on): in the C3 7B step it cut kernel time
+# 1.1 % but the step's wall time rose 3.3 % (GPU idle between kernels, not yet explained;
+# profiles/r02_fused_qkv_ab.jsonl, profiles/r02_c3_qkv_kernel_stats_*.csv); +0.4 % at C2.
+_FUSED_QKV = os.environ.get("PRL_FUSED_QKV", "0") == "1"
+
+
+class QKVFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, holder, *wb):
+        ws, bs = wb[0::2], wb[1::2]
+        H = ws[0].shape[1]
+        ns = [w.shape[0] for w in ws]
+        wf = _fused_weight(holder, ws)
+        has_bias = all(b is not None for b in bs)
+        bf = _fused_weight(holder, bs, "_prl_fused_b") if has_bias else None
+        x2 = x.reshape(-1, H)
+        rows = x2.shape[0]
+        y = gemm.linear_fwd(x2, wf, bf, solution=_fused_solution("fwd", rows, sum(ns), H))
+        ctx.save_for_backward(x2, wf)
+        ctx.params, ctx.ns, ctx.has_bias, ctx.shape = ws, ns, tuple(b is not None for b in bs), x.shape
+        ctx.set_materialize_grads(False)
+        outs, a = [], 0
+        for n in ns:
+            outs.append(y[:, a:a + n].view(*x.shape[:-1], n))
+            a += n
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *dys):
+        x2, wf = ctx.saved_tensors
+        rows = x2.shape[0]
+        parts = [d.reshape(rows, n) if d is not None else torch.zeros((rows, n), dtype=x2.dtype, device=x2.device)
+                 for d, n in zip(dys, ctx.ns)]
+        dy = torch.cat(parts, dim=1)
+        dx = gemm.linear_dgrad(dy, wf).view(ctx.shape) if ctx.needs_input_grad[0] else None
+        dws = _wgrad_group(dy, x2, ctx.params) if any(ctx.needs_input_grad[2::2]) else [None] * len(ctx.ns)
+        dbs = [None] * len(ctx.ns)
+        if any(ctx.has_bias) and any(ctx.needs_input_grad[3::2]):
+            db = dy.sum(0, dtype=torch.float32).to(dy.dtype)
+            a = 0
+            for i, n in enumerate(ctx.ns):
+                dbs[i] = db[a:a + n] if ctx.has_bias[i] else None
+                a += n
+        grads = [dx, None]
+        for dw, db in zip(dws, dbs):
+            grads += [dw, db]
+        return tuple(grads)
 
 
 def _fused_solution(pas: str, T: int, N: int, K: int) -> int:
@@ -425,7 +480,12 @@ class _Group:
         if not all(_linear_ok(x, m.weight) for m in self.mods):
             return None
         wb = [t for m in self.mods for t in (m.weight, m.bias)]
-        ys = SharedInputLinearFn.apply(x, *wb)
+        biases = [m.bias for m in self.mods]
+        if (_FUSED_QKV and x.data_ptr() % 16 == 0 and
+                (all(b is None for b in biases) or all(b is not None and b.dtype == torch.bfloat16 for b in biases))):
+            ys = QKVFn.apply(x, self, *wb)
+        else:
+            ys = SharedInputLinearFn.apply(x, *wb)
         self.x = x
         self.out = {id(m): y for m, y in zip(self.mods, ys) if m is not lin}
         return ys[self.mods.index(lin)]
@@ -546,13 +606,22 @@ def _decoder_forward(self, hidden_states, *args, **kwargs):
     return (h2, attn_w) if attn_kw.get("output_attentions") else (h2,)
 
 
+def _token_major(t) -> bool:
+    """t [B, T, H, D]: contiguous, or rows of a wider token-major buffer (a fused-qkv column range:
+    stride(1) = the buffer's row, H and D dense)."""
+    B, T, H, D = t.shape
+    return (t.is_cuda and t.dtype == torch.bfloat16 and t.stride(3) == 1 and t.stride(2) == D
+            and t.stride(1) >= H * D and t.stride(1) % 4 == 0 and (B == 1 or t.stride(0) == T * t.stride(1))
+            and t.data_ptr() % 8 == 0)
+
+
 def _rope_ok(q, k, cos, sin) -> bool:
     if q.dim() != 4 or k.dim() != 4 or cos.dim() != 3:
         return False
     qt, kt = q.transpose(1, 2), k.transpose(1, 2)
     B, hq, T, D = q.shape
-    return (_ok(qt, kt, cos, sin) and D % 8 == 0 and cos.shape == (B, T, D) and sin.shape == (B, T, D)
-            and k.shape[0] == B and k.shape[2] == T and k.shape[3] == D)
+    return (_token_major(qt) and _token_major(kt) and _ok(cos, sin) and D % 8 == 0 and cos.shape == (B, T, D)
+            and sin.shape == (B, T, D) and k.shape[0] == B and k.shape[2] == T and k.shape[3] == D)
 
 
 def _make_rope(orig):
@@ -610,6 +679,9 @@ def patch_model(model) -> dict:
                     g = _Group(lins)
                     for l in lins:
                         l.__dict__["_prl_group"] = g
+                    # q, k, v gradients back to back in gradient buckets: rows of the fused GEMM
+                    lins[1].weight._prl_follows = lins[0].weight
+                    lins[2].weight._prl_follows = lins[1].weight
                 n_group += 1
     # decoder layers (input_layernorm / self_attn / post_attention_layernorm / mlp, Qwen2 / Llama
     # style): residual adds fused into the norms.  PRL_ADD_NORM=0 keeps the eager adds (A/B)

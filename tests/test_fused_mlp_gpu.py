@@ -78,3 +78,58 @@ def test_fused_gate_up_matches_separate(monkeypatch):
     with torch.no_grad():
         wg.add_(1.0)  # an optimizer-style in-place update bumps the version: the cache is rebuilt
     assert torch.equal(model_ops._fused_weight(holder, (wg, wu)), torch.cat([wg.detach(), wu.detach()]))
+
+
+def test_fused_qkv_matches_separate():
+    """QKVFn (one GEMM over cat(Wq, Wk, Wv), concatenated bias in the epilogue) == the separate
+    SharedInputLinearFn over three micro-batches: q / k / v, dx, the weight and bias gradients to
+    bf16 GEMM rounding; q / k / v leave as column ranges of one buffer, the weight gradients become
+    row blocks of one buffer after the first micro-batch."""
+    from pipelinerl_amd.finetune import model_ops
+
+    g = torch.Generator(device=DEV).manual_seed(9)
+    T, H, NQ, NKV = 777, 512, 512, 128
+    holder = type("H", (), {})()
+    def par(*shape, s=0.05):
+        return torch.nn.Parameter((torch.randn(shape, generator=g, device=DEV) * s).to(torch.bfloat16))
+    wb = [par(NQ, H), par(NQ, s=0.5), par(NKV, H), par(NKV, s=0.5), par(NKV, H), par(NKV, s=0.5)]
+    wb2 = [torch.nn.Parameter(t.detach().clone()) for t in wb]
+    for i in range(3):
+        x = torch.randn((1, T, H), generator=g, device=DEV).to(torch.bfloat16)
+        dys = [torch.randn((1, T, n), generator=g, device=DEV).to(torch.bfloat16) for n in (NQ, NKV, NKV)]
+        xa, xb = x.clone().requires_grad_(), x.clone().requires_grad_()
+        ya = model_ops.QKVFn.apply(xa, holder, *wb)
+        yb = model_ops.SharedInputLinearFn.apply(xb, *wb2)
+        assert ya[1].data_ptr() == ya[0].data_ptr() + NQ * 2  # column ranges of one [T, NQ + 2 NKV] buffer
+        for a, b in zip(ya, yb):
+            assert (a.float() - b.float()).abs().max() <= 2e-2 * b.float().abs().max()
+        torch.autograd.backward(ya, dys)
+        torch.autograd.backward(yb, dys)
+        assert (xa.grad.float() - xb.grad.float()).abs().max() <= 2e-2 * xb.grad.float().abs().max()
+        if i == 0:
+            assert wb[2].grad.data_ptr() == wb[0].grad.data_ptr() + NQ * H * 2
+    for a, b in zip(wb, wb2):
+        assert (a.grad.float() - b.grad.float()).abs().max() <= 2e-2 * b.grad.float().abs().max() + 1e-3
+
+
+def test_rope_reads_token_strided_inputs():
+    """RopeFn on q / k given as column ranges of a fused [T, Nq + 2 Nkv] buffer == on contiguous
+    copies, bit for bit."""
+    from pipelinerl_amd.finetune.model_ops import RopeFn
+
+    g = torch.Generator(device=DEV).manual_seed(2)
+    T, HQ, HKV, D = 300, 4, 2, 128
+    y = torch.randn((T, (HQ + 2 * HKV) * D), generator=g, device=DEV).to(torch.bfloat16)
+    pos = torch.arange(T, device=DEV).float()
+    inv = 1.0 / (1e6 ** (torch.arange(0, D, 2, device=DEV).float() / D))
+    f = torch.outer(pos, inv)
+    emb = torch.cat([f, f], -1)
+    cos, sin = emb.cos().to(torch.bfloat16)[None], emb.sin().to(torch.bfloat16)[None]
+    q = y[:, :HQ * D].view(1, T, HQ, D).transpose(1, 2)
+    k = y[:, HQ * D:(HQ + HKV) * D].view(1, T, HKV, D).transpose(1, 2)
+    qc = q.transpose(1, 2).contiguous().transpose(1, 2)
+    kc = k.transpose(1, 2).contiguous().transpose(1, 2)
+    a = RopeFn.apply(q, k, cos, sin)
+    b = RopeFn.apply(qc, kc, cos, sin)
+    for u, v in zip(a, b):
+        assert torch.equal(_bits(u), _bits(v))

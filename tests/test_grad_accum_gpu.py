@@ -134,7 +134,8 @@ def test_linear_wgrad_accumulates_in_the_gemm(tmp_path, monkeypatch):
     nl = base.config.num_hidden_layers
     from pipelinerl_amd.finetune import model_ops
 
-    per_layer = 6 if model_ops._FUSED_GATE_UP else 7  # q k v o down + gate_up (one fused GEMM) or gate, up
+    # q/k/v (one fused GEMM or three), o, gate/up (one or two), down per layer
+    per_layer = (1 if model_ops._FUSED_QKV else 3) + 1 + (1 if model_ops._FUSED_GATE_UP else 2) + 1
     assert sum(calls) == 2 * (per_layer * nl + 1)  # micro-batches 2 and 3, + lm_head
     _compare(ref, got)
 

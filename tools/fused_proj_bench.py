@@ -45,6 +45,16 @@ for group, ns in (("qkv", [H, KV, KV]), ("gate_up", [I, I])):
     res = {"model": model, "T": T, "group": group, "N": ns}
     res["fwd_sep_ms"] = timed(lambda: [gemm.linear_fwd(x, w) for w in ws])
     res["fwd_fused_ms"] = timed(lambda: gemm.linear_fwd(x, wf))
+    if group == "qkv":  # Qwen2's q/k/v carry a bias: in the GEMM epilogue (prl_gemm) or torch's F.linear
+        bs = [torch.randn(n, generator=g, device="cuda").to(torch.bfloat16) for n in ns]
+        bf = torch.cat(bs)
+        res["fwd_bias_sep_ms"] = timed(lambda: [gemm.linear_fwd(x, w, b) for w, b in zip(ws, bs)])
+        res["fwd_bias_sep_torch_ms"] = timed(lambda: [torch.nn.functional.linear(x, w, b) for w, b in zip(ws, bs)])
+        res["fwd_bias_fused_ms"] = timed(lambda: gemm.linear_fwd(x, wf, bf))
+        res["fwd_bias_fused_torch_ms"] = timed(lambda: torch.nn.functional.linear(x, wf, bf))
+        dq = torch.randn((T, ns[0]), generator=g, device="cuda").to(torch.bfloat16)
+        res["cat_dy_ms"] = timed(lambda: torch.cat([dq, dys[1], dys[2]], dim=1))
+        res["bias_sum_fused_ms"] = timed(lambda: dyf.sum(0, dtype=torch.float32).to(torch.bfloat16))
 
     def dgrad_sep():
         gemm.linear_dgrad(dys[0], ws[0], out=dx)
