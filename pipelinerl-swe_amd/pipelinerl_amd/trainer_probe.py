@@ -125,9 +125,10 @@ class TrainerStep:
             if group is not None:
                 raise ValueError("fsdp shards over the default process group")
             self.model = shard_model(self.model)
-        if step_fn is None:
-            from .finetune.rl import rl_step as step_fn
-        self.step_fn = step_fn
+        from .finetune.rl import rl_step
+
+        self.native_step = step_fn is None or step_fn is rl_step
+        self.step_fn = step_fn if step_fn is not None else rl_step
         self.opt = get_optimizer("adamw_torch", self.model, 1e-6, 0.01)
         self.grads = GradBuckets(list(self.model.parameters()), group=group) \
             if world > 1 and not fsdp and not local else None
@@ -155,8 +156,13 @@ class TrainerStep:
                 self.grads.arm()
             if self.fsdp:  # reduce-scatter on the boundary micro-batch only (the reference's no_sync)
                 set_gradient_sync(self.model, i == len(self.batches) - 1)
-            loss, _ = self.step_fn(self.model, b, 0, 100, self.cfg)
-            loss.backward()
+            if self.native_step:  # as the loop runs it: statistics read after the backward is queued
+                loss, stats = self.step_fn(self.model, b, 0, 100, self.cfg, defer_stats=True)
+                loss.backward()
+                stats.resolve()  # the reference's non-finite assertions
+            else:
+                loss, _ = self.step_fn(self.model, b, 0, 100, self.cfg)
+                loss.backward()
         if self.grads is not None:
             self.grads.finish()
         torch.nn.utils.clip_grad_norm_(self.model.parameters(), 0.3)
