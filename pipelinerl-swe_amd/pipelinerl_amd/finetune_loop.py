@@ -48,6 +48,7 @@ from .finetune.rl.utils import aggregate_rl_stats
 from .finetune.sharding import fsdp_requested, set_gradient_sync, shard_model
 from .finetune.trace import PhaseTrace
 from . import native_data
+from .hostgc import freeze_setup_heap
 from .finetune.types import PipelineBatchEncoding, TrainingMetrics
 from .streams import SingleStreamSpec, read_stream, set_streams_backend, write_to_streams
 from .weight_update import (TRAINER_TOPIC, ParameterInfo, SamplesProcessed, WeightUpdateManager,  # noqa: F401
@@ -259,6 +260,7 @@ def run_finetuning_loop(cfg, step_fn: Callable = rl_step, model=None, tokenizer=
                               args=(data_stream, batch_queue, ctx.device, stop, args.get("data_timeout_s")),
                               daemon=True)
     model.train()
+    freeze_setup_heap()  # no generation-2 walks over the set-up heap mid-step (hostgc.py)
     loader.start()
     try:
         return rl_finetuning_worker(args, ctx, model, optimizer, lr_scheduler, grads, wum, tokenizer, metrics,

@@ -147,6 +147,9 @@ class TrainerStep:
             self.batches = [packed_batch(tokens, seq, prompt, V, self.device, seed=rank * 97 + i,
                                          ref_noise=kl_coef > 0) for i in range(micro_batches)]
             self.cfg = rl_config(micro_batches * (tokens // seq) * world, fused_head, kl_coef)
+        from .hostgc import freeze_setup_heap
+
+        freeze_setup_heap()  # as the loop does before its first step
 
     def step(self, wum=None, version: int = 0) -> None:
         from .finetune.sharding import set_gradient_sync

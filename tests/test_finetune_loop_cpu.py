@@ -217,3 +217,26 @@ def test_phase_trace_unit():
     off.start()
     off.mark("forward")
     assert off.collect() == {}
+
+
+def test_freeze_setup_heap(monkeypatch):
+    """hostgc.freeze_setup_heap moves the set-up heap to the permanent generation (no
+    generation-2 walk over it mid-step); PRL_GC_FREEZE=0 leaves the collector alone; objects made
+    after the freeze are still collected."""
+    import gc
+
+    from pipelinerl_amd.hostgc import freeze_setup_heap
+
+    try:
+        monkeypatch.setenv("PRL_GC_FREEZE", "0")
+        gc.unfreeze()
+        assert not freeze_setup_heap() and gc.get_freeze_count() == 0
+        monkeypatch.setenv("PRL_GC_FREEZE", "1")
+        assert freeze_setup_heap() and gc.get_freeze_count() > 1000
+        a, b = [], []
+        a.append(b)
+        b.append(a)  # a reference cycle made after the freeze
+        del a, b
+        assert gc.collect() >= 2
+    finally:
+        gc.unfreeze()

@@ -25,7 +25,37 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--layers", type=int, default=None)
     a = ap.parse_args()
+    import gc
+    import time
+
     import torch
+
+    # host garbage collections inside the timed steps (TrainerStep.timed), by generation: count
+    # and total ms (the stalls pipelinerl_amd/hostgc.py removes)
+    gcs = {g: [0, 0.0] for g in range(3)}
+    t_gc = [0.0]
+    window = [False]
+
+    def on_gc(phase, info):
+        if phase == "start":
+            t_gc[0] = time.perf_counter()
+        elif window[0]:
+            gcs[info["generation"]][0] += 1
+            gcs[info["generation"]][1] += (time.perf_counter() - t_gc[0]) * 1e3
+
+    from pipelinerl_amd.trainer_probe import TrainerStep
+
+    timed = TrainerStep.timed
+
+    def timed_window(self, *args, **kw):
+        window[0] = True
+        try:
+            return timed(self, *args, **kw)
+        finally:
+            window[0] = False
+
+    TrainerStep.timed = timed_window
+    gc.callbacks.append(on_gc)
 
     from pipelinerl_amd.trainer_probe import dp_step_probe
 
@@ -33,6 +63,7 @@ def main():
 
     r = dp_step_probe(a.config, micro_batches=a.micro_batches, steps=a.steps, warmup=a.warmup,
                       device=torch.device("cuda", 0), layers=a.layers)
+    r["host_gc"] = {f"gen{g}": {"n": n, "ms": round(ms, 1)} for g, (n, ms) in gcs.items()}
     print(json.dumps(r), flush=True)
 
 
