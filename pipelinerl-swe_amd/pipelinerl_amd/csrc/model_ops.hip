@@ -25,13 +25,32 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ float lo(uint32_t v) { return __builtin_bit_cast(float, v << 16); }
 __device__ __forceinline__ float hi(uint32_t v) { return __builtin_bit_cast(float, v & 0xFFFF0000u); }
-__device__ __forceinline__ uint32_t rne(float f) {  // float -> bf16 bits, round to nearest even
+// float -> bf16, round to nearest even.  gfx950 converts in hardware (v_cvt_pk_bf16_f32, two
+// values per instruction, RNE, NaN stays NaN): 1-2 vector instructions where the integer
+// sequence below takes 5-6 per value, and these kernels run ~40 such roundings per element pair
+// (the eager chain's intermediate bf16 casts).  PRL_HW_BF16=0 keeps the integer sequence (A/B).
+#ifndef PRL_HW_BF16
+#define PRL_HW_BF16 1
+#endif
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t rne(float f) {  // bf16 bits in the low half
+#if PRL_HW_BF16
+  return __builtin_bit_cast(uint16_t, (__bf16)f);
+#else
   const uint32_t u = __builtin_bit_cast(uint32_t, f);
   if ((u & 0x7FFFFFFFu) > 0x7F800000u) return (u >> 16) | 0x40u;  // NaN stays NaN
   return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+#endif
 }
 __device__ __forceinline__ float r16(float f) { return __builtin_bit_cast(float, rne(f) << 16); }  // bf16 round
-__device__ __forceinline__ uint32_t pack(float a, float b) { return rne(a) | (rne(b) << 16); }
+__device__ __forceinline__ uint32_t pack(float a, float b) {
+#if PRL_HW_BF16
+  const bf16x2_t v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(uint32_t, v);
+#else
+  return rne(a) | (rne(b) << 16);
+#endif
+}
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -30,6 +30,7 @@ VARIANTS = {
     "norm_grid3072_early": {"PRL_NORM_GRID": "3072", "PRL_NORM_WIDE_DRES_EARLY": "1"},
     "norm_grid2048": {"PRL_NORM_GRID": "2048"},
     "norm_fwd2048": {"PRL_NORM_FWD_GRID": "2048"},
+    "bf16_sw": {"PRL_HW_BF16": "0"},
 }
 
 if __name__ == "__main__":
