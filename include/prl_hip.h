@@ -209,6 +209,20 @@ int prl_unflatten_bf16(const void* src, void* const* dsts, const int32_t* dtypes
 int prl_grad_scale_bf16(const void* src, int32_t src_dtype, const float* scale, void* dst, int64_t n,
                         int32_t accumulate, void* stream);
 
+/* AdamW step over n tensors (csrc/adamw.hip): params / grads / exp_avgs / exp_avg_sqs are device
+ * pointers of `dtype` (PRL_BF16 or PRL_F32, all four alike), steps[i] the device float step count
+ * of tensor i (already incremented for this step, as torch's fused AdamW expects it), numels[i] its
+ * element count; the pointer arrays themselves are host memory.  grad_scale: NULL, or a device
+ * scalar of `dtype` every gradient is multiplied by first (the gradient-clipping coefficient,
+ * stored-and-reloaded rounding as torch._foreach_mul_ would leave it; the gradients themselves are
+ * not written).  Bit-identical to torch.optim.AdamW(fused=True) after clip_grad_norm_ (ADAMW mode,
+ * no amsgrad / maximize).  Every entry is validated before the first launch.  Replaces
+ * clip_grad_norm_'s multiply + optimizer.step() at pipelinerl/finetune_loop.py:700-719. */
+int prl_adamw_step(int32_t n, void* const* params, const void* const* grads, void* const* exp_avgs,
+                   void* const* exp_avg_sqs, const float* const* steps, const int64_t* numels, int32_t dtype,
+                   double lr, double beta1, double beta2, double weight_decay, double eps, const void* grad_scale,
+                   void* stream);
+
 /* Sum of squares of n device tensors (f32 or bf16) accumulated into *out (device f64).
  * *out is overwritten. */
 int prl_grad_sqnorm(const void* const* srcs, const int32_t* dtypes, const int64_t* numels,

@@ -25,7 +25,7 @@ COMM_LIB = PKG / "libprl_comm.so"
 GEMM_LIB = PKG / "libprl_gemm.so"
 DATA_LIB = PKG / "libprl_data.so"
 ARCH = "gfx950"
-SOURCES = ["grpo_loss.hip", "flat_pack.hip", "model_ops.hip", "attn_bwd.hip"]
+SOURCES = ["grpo_loss.hip", "flat_pack.hip", "model_ops.hip", "attn_bwd.hip", "adamw.hip"]
 
 
 def hipcc() -> str:

@@ -42,7 +42,7 @@ import torch.distributed as dist
 from .finetune.checkpoints import (load_model, load_tokenizer, load_training_state, remove_results,
                                    save_model_and_tokenizer, save_training_state)
 from .finetune.grad_sync import GradBuckets
-from .finetune.optim import get_optimizer
+from .finetune.optim import clip_grad_norm, get_optimizer
 from .finetune.rl import RLConfig, RLStats, rl_step
 from .finetune.rl.utils import aggregate_rl_stats
 from .finetune.sharding import fsdp_requested, set_gradient_sync, shard_model
@@ -416,7 +416,8 @@ def rl_finetuning_worker(args, ctx: Dist, model, optimizer, lr_scheduler, grads:
             grads.finish()
         trace.mark("allreduce_wait")
         clip = args.get("gradient_clipping_threshold")
-        gn = torch.nn.utils.clip_grad_norm_(model.parameters(), clip if clip else float("inf"))
+        # torch's clip_grad_norm_; with the HIP AdamW the multiply runs inside its step (optim.py)
+        gn = clip_grad_norm(model.parameters(), clip if clip else float("inf"), optimizer)
         trace.mark("clip")
         if wum is not None:
             wum.poll()  # a failed update (actor error / timeout) ends training here

@@ -152,6 +152,7 @@ class TrainerStep:
         freeze_setup_heap()  # as the loop does before its first step
 
     def step(self, wum=None, version: int = 0) -> None:
+        from .finetune.optim import clip_grad_norm
         from .finetune.sharding import set_gradient_sync
 
         for i, b in enumerate(self.batches):
@@ -168,7 +169,7 @@ class TrainerStep:
                 loss.backward()
         if self.grads is not None:
             self.grads.finish()
-        torch.nn.utils.clip_grad_norm_(self.model.parameters(), 0.3)
+        clip_grad_norm(self.model.parameters(), 0.3, self.opt)
         if wum is not None:
             wum.before_optimizer_step()  # the previous snapshot is read before params change
         self.opt.step()

@@ -240,3 +240,27 @@ def test_freeze_setup_heap(monkeypatch):
         assert gc.collect() >= 2
     finally:
         gc.unfreeze()
+
+
+def test_prl_adamw_cpu_falls_back_to_torch():
+    """PrlAdamW on CPU parameters takes torch's fused step, with clip_grad_norm's deferred
+    multiply applied first: identical to clip_grad_norm_ + torch.optim.AdamW(fused=True)."""
+    from pipelinerl_amd.finetune.optim import PrlAdamW, clip_grad_norm
+
+    g = torch.Generator().manual_seed(0)
+    pa = [torch.nn.Parameter(torch.randn(s, generator=g)) for s in ((5, 7), (11,))]
+    pb = [torch.nn.Parameter(p.detach().clone()) for p in pa]
+    ref = torch.optim.AdamW(pa, lr=1e-2, fused=True)
+    opt = PrlAdamW(pb, lr=1e-2)
+    for step in range(3):
+        grads = [torch.randn(p.shape, generator=g) * 5 for p in pa]
+        for p, q, gr in zip(pa, pb, grads):
+            p.grad, q.grad = gr.clone(), gr.clone()
+        na = torch.nn.utils.clip_grad_norm_(pa, 0.3)
+        nb = clip_grad_norm(pb, 0.3, opt)
+        assert torch.equal(na, nb)
+        ref.step()
+        opt.step()
+    for p, q in zip(pa, pb):
+        assert torch.equal(p, q)
+    assert isinstance(clip_grad_norm(pa, 1.0, ref), torch.Tensor)  # any other optimizer: torch's clip
