@@ -51,8 +51,10 @@ def has_weights(d: Path) -> bool:
     return any((Path(d) / f).exists() for f in WEIGHT_FILES)
 
 
-def load_model(args, model_class: str, current_dir: Path, device: torch.device):
-    """HF causal LM from ``current_dir`` (resume) or ``args.config_name``; optional value head."""
+def load_model(args, model_class: str, current_dir: Path, device: torch.device, shard_world: int = 1):
+    """HF causal LM from ``current_dir`` (resume) or ``args.config_name``; optional value head.
+    Gradient checkpointing as the config asks, unless its activations fit the device
+    (``gradient_checkpointing_policy``, finetune/recompute.py; ``shard_world``: the FSDP world)."""
     from transformers import AutoConfig, AutoModelForCausalLM
 
     src = str(current_dir) if has_weights(current_dir) else args.config_name
@@ -75,7 +77,12 @@ def load_model(args, model_class: str, current_dir: Path, device: torch.device):
         from .model_ops import patch_model
 
         patch_model(model)
+    from .recompute import plan_gradient_checkpointing
+
+    plan = plan_gradient_checkpointing(args, model, device, shard_world)
     if args.get("gradient_checkpointing", False):
+        logger.info(f"gradient checkpointing: {plan.as_dict()}")
+    if plan.checkpoint:
         model.gradient_checkpointing_enable(
             gradient_checkpointing_kwargs={"use_reentrant": bool(args.get("reentrant_checkpointing", False))})
     if model_class == "causal-language-modeling-with-value-head":

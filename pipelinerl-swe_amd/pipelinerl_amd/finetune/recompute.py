@@ -1,0 +1,100 @@
+"""Whether to recompute activations (gradient checkpointing), sized for the device's HBM.
+
+The reference's trainer config turns HF gradient checkpointing on unconditionally
+(conf/finetune/base.yaml:44-48, "to reduce memory footprint"; applied by
+finetune/checkpoints.py when the model is loaded): every decoder layer's forward runs twice,
+about a third more compute per micro-batch.  On a 288 GB MI355X the activations of a whole
+packed micro-batch usually fit beside the weights, gradients and optimizer state, and
+recomputing them only costs time.  The results are the same either way (the recomputed
+forward is the same deterministic kernels on the same inputs).
+
+``finetune.gradient_checkpointing_policy`` (build-only key):
+  ``auto`` (default)  checkpoint only when the estimate below does not fit the device
+  ``always``          the reference's behaviour: checkpoint whenever gradient_checkpointing is set
+
+The estimate is deliberately conservative (upper bounds, measured against the trainer probes'
+peak memory in DESIGN.md): model state = parameters x (weight + gradient + two AdamW moments),
+divided by the FSDP world when sharded; activations = the tensors a patched Qwen2-style decoder
+layer keeps for its backward per token (the normed inputs of the q/k/v and gate/up GEMMs, q, k,
+v, the attention output, the residual stream, gate, up and the SwiGLU output), times
+``seq_length`` tokens, times the layers, times a 1.25 allowance for backward temporaries; one
+label-row logits chunk; 5 % of the device plus 4 GiB of headroom.
+"""
+
+from __future__ import annotations
+
+import logging
+from dataclasses import dataclass
+
+import torch
+
+logger = logging.getLogger(__name__)
+
+ACT_ALLOWANCE = 1.25
+HEADROOM_FRAC = 0.05
+HEADROOM_BYTES = 4 << 30
+
+
+@dataclass
+class RecomputePlan:
+    checkpoint: bool
+    reason: str
+    state_bytes: int = 0
+    activation_bytes: int = 0
+    logits_bytes: int = 0
+    device_bytes: int = 0
+
+    def as_dict(self) -> dict:
+        return {"checkpoint": self.checkpoint, "reason": self.reason, "state_gb": round(self.state_bytes / 1e9, 2),
+                "activation_gb": round(self.activation_bytes / 1e9, 2), "logits_gb": round(self.logits_bytes / 1e9, 2),
+                "device_gb": round(self.device_bytes / 1e9, 2)}
+
+
+def activation_bytes_per_token(config, dtype_bytes: int = 2) -> int:
+    """Bytes one token keeps for the backward across every decoder layer (upper bound)."""
+    H = int(config.hidden_size)
+    inter = int(getattr(config, "intermediate_size", 4 * H))
+    heads = int(getattr(config, "num_attention_heads", 1))
+    kv_heads = int(getattr(config, "num_key_value_heads", None) or heads)
+    head_dim = int(getattr(config, "head_dim", None) or H // heads)
+    kv = kv_heads * head_dim
+    layers = int(config.num_hidden_layers)
+    # residual in, normed (attention), q, attention out, residual mid, normed (MLP): 6 H;
+    # k, v: 2 kv; gate, up, SwiGLU out: 3 I; per-row statistics (rstd, lse) are negligible
+    per_layer = 6 * H + 2 * kv + 3 * inter
+    return per_layer * layers * dtype_bytes
+
+
+def plan_gradient_checkpointing(args, model, device: torch.device, shard_world: int = 1,
+                                device_bytes: int | None = None) -> RecomputePlan:
+    """The decision for ``model`` (already built) under the trainer config ``args``;
+    ``device_bytes``: the device's memory (default: queried from the HIP device)."""
+    if not args.get("gradient_checkpointing", False):
+        return RecomputePlan(False, "gradient_checkpointing is off")
+    policy = str(args.get("gradient_checkpointing_policy", "auto"))
+    if policy not in ("auto", "always"):
+        raise ValueError(f"gradient_checkpointing_policy must be 'auto' or 'always', got {policy!r}")
+    if policy == "always":
+        return RecomputePlan(True, "policy always (the reference's behaviour)")
+    if device_bytes is None and device.type != "cuda":
+        return RecomputePlan(True, "not a HIP device: the reference's behaviour")
+    seq = args.get("seq_length")
+    config = getattr(model, "config", None)
+    if not seq or config is None or not hasattr(config, "hidden_size") or not hasattr(config, "num_hidden_layers"):
+        return RecomputePlan(True, "no seq_length / decoder shape to size the activations: the reference's behaviour")
+    total = int(device_bytes) if device_bytes is not None else int(torch.cuda.get_device_properties(device).total_memory)
+    params = list(model.parameters())
+    n = sum(p.numel() for p in params)
+    pbytes = params[0].element_size() if params else 2
+    # weight + gradient + exp_avg + exp_avg_sq, all in the parameter dtype (torch / PrlAdamW)
+    state = 4 * n * pbytes // max(1, int(shard_world))
+    act = int(ACT_ALLOWANCE * int(seq) * activation_bytes_per_token(config, pbytes))
+    vocab = int(getattr(config, "vocab_size", 0))
+    rl = args.get("rl", None) or {}
+    chunk = min(int(seq), int(rl.get("lm_head_chunk_rows", 65536) or 65536))  # RLConfig default
+    logits = chunk * vocab * pbytes
+    need = state + act + logits + int(HEADROOM_FRAC * total) + HEADROOM_BYTES
+    keep = need <= total
+    plan = RecomputePlan(not keep, ("activations fit: no recompute" if keep else "activations do not fit: recompute"),
+                         state, act, logits, total)
+    return plan

@@ -200,11 +200,11 @@ def run_finetuning_loop(cfg, step_fn: Callable = rl_step, model=None, tokenizer=
     setup_logging(log_dir, ctx.rank)
     update_stream = SingleStreamSpec(exp_path=exp_root, topic=TRAINER_TOPIC)
 
+    sharded = fsdp_requested(cfg, args) and ctx.initialized
     if model is None:
-        model = load_model(args, args.model_class, current_dir, ctx.device)
+        model = load_model(args, args.model_class, current_dir, ctx.device, shard_world=ctx.world if sharded else 1)
     if tokenizer is None:
         tokenizer = load_tokenizer(args.config_name, getattr(getattr(model, "config", None), "eos_token_id", None))
-    sharded = fsdp_requested(cfg, args) and ctx.initialized
     if sharded:  # before the optimizer: it must see the sharded parameters
         model = shard_model(model, cfg.get("fsdp"), grad_reduce=args.get("grad_reduce", "mean"))
     data_stream = SingleStreamSpec(exp_path=exp_root, topic=args.input, instance=0, partition=ctx.rank)

@@ -1,0 +1,86 @@
+"""Gradient-checkpointing plan (finetune/recompute.py): the reference config sets
+gradient_checkpointing (conf/finetune/base.yaml:44-48); the build skips the recompute when the
+micro-batch's activations fit the device.  Models are built on the meta device at the published
+Qwen2.5 shapes (no memory), the device size is given."""
+
+import types
+
+import pytest
+import torch
+
+GB = 10 ** 9
+
+
+def _meta_model(name):
+    from transformers import AutoModelForCausalLM, Qwen2Config
+
+    from pipelinerl_amd.trainer_probe import QWEN
+
+    with torch.device("meta"):
+        return AutoModelForCausalLM.from_config(Qwen2Config(**QWEN[name]), dtype=torch.bfloat16)
+
+
+def _args(**kw):
+    d = dict(gradient_checkpointing=True, seq_length=12000)
+    d.update(kw)
+
+    class A(dict):
+        def __getattr__(self, k):
+            return self[k]
+
+    return A(d)
+
+
+@pytest.fixture(scope="module")
+def m7b():
+    return _meta_model("7b")
+
+
+def test_7b_c3_fits_mi355x(m7b):
+    from pipelinerl_amd.finetune.recompute import plan_gradient_checkpointing
+
+    p = plan_gradient_checkpointing(_args(), m7b, torch.device("cuda"), device_bytes=288 * GB)
+    assert not p.checkpoint, p.as_dict()
+    # 7.6 B bf16 parameters x (weight, grad, 2 moments); activations of 12 000 tokens over 28 layers
+    assert 60 * GB < p.state_bytes < 62 * GB
+    assert 60 * GB < p.activation_bytes < 75 * GB
+    # the same micro-batch on an 80 GB card recomputes
+    assert plan_gradient_checkpointing(_args(), m7b, torch.device("cuda"), device_bytes=80 * GB).checkpoint
+
+
+def test_policy_and_reference_fallbacks(m7b):
+    from pipelinerl_amd.finetune.recompute import plan_gradient_checkpointing
+
+    cuda = torch.device("cuda")
+    assert plan_gradient_checkpointing(_args(gradient_checkpointing_policy="always"), m7b, cuda,
+                                       device_bytes=288 * GB).checkpoint
+    assert not plan_gradient_checkpointing(_args(gradient_checkpointing=False), m7b, cuda,
+                                           device_bytes=288 * GB).checkpoint
+    # off the GPU, without a seq_length or without a decoder config: as the reference does
+    assert plan_gradient_checkpointing(_args(), m7b, torch.device("cpu")).checkpoint
+    assert plan_gradient_checkpointing(_args(seq_length=None), m7b, cuda, device_bytes=288 * GB).checkpoint
+    assert plan_gradient_checkpointing(_args(), types.SimpleNamespace(parameters=lambda: iter(())), cuda,
+                                       device_bytes=288 * GB).checkpoint
+    with pytest.raises(ValueError):
+        plan_gradient_checkpointing(_args(gradient_checkpointing_policy="never"), m7b, cuda, device_bytes=288 * GB)
+
+
+def test_32b_needs_sharding():
+    from pipelinerl_amd.finetune.recompute import plan_gradient_checkpointing
+
+    m = _meta_model("32b")
+    args = _args(seq_length=4096)
+    cuda = torch.device("cuda")
+    # unsharded, the model state alone (262 GB) leaves no room; FSDP over 4 trainer GPUs does
+    assert plan_gradient_checkpointing(args, m, cuda, shard_world=1, device_bytes=288 * GB).checkpoint
+    p = plan_gradient_checkpointing(args, m, cuda, shard_world=4, device_bytes=288 * GB)
+    assert not p.checkpoint, p.as_dict()
+
+
+def test_label_row_chunk_sizes_the_logits(m7b):
+    from pipelinerl_amd.finetune.recompute import plan_gradient_checkpointing
+
+    cuda = torch.device("cuda")
+    a = plan_gradient_checkpointing(_args(), m7b, cuda, device_bytes=288 * GB)
+    b = plan_gradient_checkpointing(_args(rl={"lm_head_chunk_rows": 4096}), m7b, cuda, device_bytes=288 * GB)
+    assert a.logits_bytes == 12000 * 152064 * 2 and b.logits_bytes == 4096 * 152064 * 2

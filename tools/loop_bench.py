@@ -72,6 +72,10 @@ def main():
     ap.add_argument("--dist", choices=["uniform", "c3"], default="uniform",
                     help="rollout lengths: uniform around --mean-len, or configs[2]'s U{64..512} + U{256..8192}")
     ap.add_argument("--eager-ops", action="store_true", help="HF element-wise chains instead of the HIP model ops")
+    ap.add_argument("--grad-ckpt", action="store_true",
+                    help="gradient_checkpointing: true, as the reference config sets it (conf/finetune/base.yaml:45)")
+    ap.add_argument("--ckpt-policy", choices=["auto", "always"], default="auto",
+                    help="gradient_checkpointing_policy (finetune/recompute.py)")
     ap.add_argument("--workdir", default=None)
     a = ap.parse_args()
 
@@ -106,7 +110,8 @@ def main():
         os.environ.pop(k, None)
     ft = dict(
         config_name=str(model_dir), model_class="causal-language-modeling", output_dir=str(exp / "finetune"),
-        load_as_bf16=True, attn_implementation="flash_attention_2", gradient_checkpointing=False, optim="adamw_torch",
+        load_as_bf16=True, attn_implementation="flash_attention_2", gradient_checkpointing=a.grad_ckpt,
+        gradient_checkpointing_policy=a.ckpt_policy, seq_length=a.seq_length, optim="adamw_torch",
         learning_rate=1e-6, weight_decay=0.01, lr_scheduler_type="cosine", num_warmup_steps=0,
         max_train_steps=a.steps, interrupt_train_steps=-1, gradient_accumulation_passes=a.samples_per_step,
         train_batch_size=1, seq_parallel=1, seed=42, gradient_clipping_threshold=0.3, input="training_data",
@@ -143,6 +148,7 @@ def main():
     out = {"tool": "loop_bench", "model": f"Qwen2.5-{a.model} shapes (random init, bf16)",
            "seq_length": a.seq_length, "samples_per_step": a.samples_per_step, "mean_rollout_len": a.mean_len, "length_dist": a.dist,
            "fused_lm_head": not a.full_logits, "fused_model_ops": not a.eager_ops, "steps": m.completed_steps,
+           "gradient_checkpointing": a.grad_ckpt, "checkpointing_policy": a.ckpt_policy,
            "micro_batches_per_step": [x["throughput/micro_batches_per_step"] for x in lines],
            "tokens_per_step": [x["throughput/tokens_per_step"] for x in lines],
            "step_wall_s": [round(b - a_, 3) for a_, b in zip(stamps, stamps[1:])],
