@@ -87,6 +87,9 @@ constexpr int kLoadAux = PRL_LOAD_AUX;
 constexpr int kStoreAux = PRL_STORE_AUX;
 constexpr uint32_t kPadBf16x2 = 0xF1CAF1CAu;  // two bf16 -1.0e30: contributes 2^-huge = 0
 
+#ifndef PRL_PHASED
+#define PRL_PHASED 0  // A/B (tools/build_variants.py phased): stores of a row, then the next row's loads
+#endif
 #ifndef PRL_ROW_PERMUTE
 #define PRL_ROW_PERMUTE 1  // A/B (tools/build_variants.py row_permute): 7.40 vs 7.46 ms per C2 launch, same box
 #endif
@@ -219,8 +222,18 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
         }
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, o),
                                                ws, voff, k * VSTRIDE, kStoreAux);
+#if !PRL_PHASED
         buf[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rn, voff, k * VSTRIDE, kLoadAux));
+#endif
       }
+#if PRL_PHASED
+      // A/B: the whole row's stores retire before the next row's loads start (no mixed traffic
+      // from this CU); tools/hbm/phased_copy.hip measures the same schedule on a plain copy
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int k = 0; k < NV; ++k)
+        buf[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rn, voff, k * VSTRIDE, kLoadAux));
+#endif
     } else {
 #pragma unroll
       for (int k = 0; k < NV; ++k)
