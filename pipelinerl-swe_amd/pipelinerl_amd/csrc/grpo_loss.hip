@@ -6,9 +6,10 @@
 //   grpo_fwd_resident<NV>  bf16 logits, V % 8 == 0 (Qwen2.5: V = 151936 / 152064).
 //       Persistent grid, one 1024-thread workgroup per CU, one vocab row per iteration.
 //       The whole row (V*2 B = 297 KiB) is held in VGPRs (NV x 16 B per lane), so the
-//       gradient pass re-reads nothing.  Software pipeline: while the gradient of row r is
-//       written, vector k of row r+grid is loaded into the register that vector k of row r
-//       just vacated, so every CU keeps ~300 KiB of loads in flight across the row seam.
+//       gradient pass re-reads nothing.  Read / write phases: the row's dlogits stores retire,
+//       then the whole next row (~300 KiB per CU) is loaded at once, so a CU never mixes HBM
+//       reads and writes (3-4 % faster than loading vector k of row r+grid right behind the
+//       store of vector k of row r; PRL_PHASED below).
 //       Row reduction: per-lane online (max, sum 2^y, sum 2^y y) with lazy rebase, wave
 //       shuffles, then one LDS exchange (double-buffered by row parity: one barrier/row).
 //   grpo_fwd_stream<T,VEC> any dtype / V: same math, row re-read for the gradient pass.
@@ -88,8 +89,18 @@ constexpr int kStoreAux = PRL_STORE_AUX;
 constexpr uint32_t kPadBf16x2 = 0xF1CAF1CAu;  // two bf16 -1.0e30: contributes 2^-huge = 0
 
 #ifndef PRL_PHASED
-#define PRL_PHASED 0  // A/B (tools/build_variants.py phased): stores of a row, then the next row's loads
+// 1: a row's stores retire (vmcnt(0)) before the next row's loads are issued, so this CU never
+// mixes reads and writes: 7.50 -> 7.24 ms per C2 launch on one box (profiles/r02_loss_phase_ab.jsonl;
+// the same schedule on a plain 20 GB copy: profiles/r02_phased_copy.jsonl).  0: the next row's
+// vector k is loaded right behind the store of vector k (round-1 schedule).  2: phased, no wait.
+#define PRL_PHASED 1
 #endif
+// The phased schedule keeps pass 2's gradient vectors and the row in registers at once: above
+// NV = 20 (V > 163 840) it spills row vectors to scratch, and at NV = 24 its dlogits were wrong
+// on the GPU (tests/test_grpo_edge_gpu.py::test_vocab_size_limits; the interleaved schedule
+// passes it; cause not found), so rows that large keep the interleaved schedule.  Qwen2.5's
+// vocabularies are NV = 19, covered by tests/test_grpo_edge_gpu.py::test_multi_row_per_workgroup.
+constexpr int kPhasedMaxNV = 20;
 #ifndef PRL_ROW_PERMUTE
 #define PRL_ROW_PERMUTE 1  // A/B (tools/build_variants.py row_permute): 7.40 vs 7.46 ms per C2 launch, same box
 #endif
@@ -110,6 +121,7 @@ template <int NV>
 __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
   constexpr int BLOCK = 1024, NW = BLOCK / 64;
   constexpr int VSTRIDE = BLOCK * 16;  // bytes between a lane's consecutive vectors
+  constexpr bool kPhased = PRL_PHASED != 0 && NV <= kPhasedMaxNV;
   __shared__ float red[2][NW][3];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int64_t nrows = fwd_rows(a);
@@ -222,18 +234,18 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
         }
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, o),
                                                ws, voff, k * VSTRIDE, kStoreAux);
-#if !PRL_PHASED
-        buf[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rn, voff, k * VSTRIDE, kLoadAux));
-#endif
+        if constexpr (!kPhased)
+          buf[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rn, voff, k * VSTRIDE, kLoadAux));
       }
-#if PRL_PHASED
-      // A/B: the whole row's stores retire before the next row's loads start (no mixed traffic
-      // from this CU); tools/hbm/phased_copy.hip measures the same schedule on a plain copy
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if constexpr (kPhased) {
+        // the whole row's stores retire before the next row's loads start (PRL_PHASED above)
+        if constexpr (PRL_PHASED == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (has_next) {
 #pragma unroll
-      for (int k = 0; k < NV; ++k)
-        buf[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rn, voff, k * VSTRIDE, kLoadAux));
-#endif
+          for (int k = 0; k < NV; ++k)
+            buf[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rn, voff, k * VSTRIDE, kLoadAux));
+        }
+      }
     } else {
 #pragma unroll
       for (int k = 0; k < NV; ++k)

@@ -163,3 +163,17 @@ def test_unpacked_bf16_value_head_ragged():
     lg = synth.to_bf16(rng.normal(0, 2, (B, L, V))).astype(np.float32)
     values = f(rng.normal(0.2, 0.3, (B, L)))
     _cmp(lg, b, dict(CFG, value_loss_coef=0.1), values=values)
+
+
+def test_multi_row_per_workgroup():
+    """Qwen2.5's vocab (the resident kernel's NV = 19, read / write phased schedule) with ~2.3 rows
+    per workgroup of the persistent grid, so rows with and without a next row are both taken: every
+    row's dlogits and every statistic against the oracle, and two runs bitwise identical."""
+    V = 151936
+    lens = [150, 200, 251]
+    T = sum(lens)
+    b = _batch(T, V, seed=9, lens=lens, prompts=[20, 30, 40])
+    lg = synth.to_bf16(np.random.default_rng(9).normal(0, 2.5, (1, T, V))).astype(np.float32)
+    _, d1 = _cmp(lg, b)
+    _, _, d2 = _run(lg, b)
+    assert np.array_equal(d1, d2)

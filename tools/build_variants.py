@@ -31,7 +31,8 @@ VARIANTS = {
     "norm_grid2048": {"PRL_NORM_GRID": "2048"},
     "norm_fwd2048": {"PRL_NORM_FWD_GRID": "2048"},
     "bf16_sw": {"PRL_HW_BF16": "0"},
-    "phased": {"PRL_PHASED": "1"},
+    "unphased": {"PRL_PHASED": "0"},
+    "phased_nowait": {"PRL_PHASED": "2"},
 }
 
 if __name__ == "__main__":
