@@ -77,24 +77,32 @@ __device__ __forceinline__ bf16x8 tr_operand(const char* base, int lane, int dc,
   return bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 }
 
-// register staging of a 64-row stage of X[T, H, D] (rows r0.., head h): 4 chunks per thread
-constexpr int kStageChunks = STAGE * 16 / 256;
-struct Stage {
-  u32x4 x[kStageChunks];
+// register staging of a ROWS-row stage of X[T, H, D] (rows r0.., head h): ROWS / 16 chunks per thread
+template <int ROWS>
+struct StageT {
+  u32x4 x[ROWS * 16 / 256];
 };
-__device__ __forceinline__ Stage stage_load(const __bf16* __restrict__ X, int64_t rs, int h, int r0, int r1, int tid) {
-  Stage st;
+typedef StageT<STAGE> Stage;
+#ifndef PRL_ATTN_BSTAGE
+#define PRL_ATTN_BSTAGE 64  // rows per backward stage; 32 halves the staging registers (A/B)
+#endif
+constexpr int BSTAGE = PRL_ATTN_BSTAGE;
+template <int ROWS = STAGE>
+__device__ __forceinline__ StageT<ROWS> stage_load(const __bf16* __restrict__ X, int64_t rs, int h, int r0, int r1,
+                                                    int tid) {
+  StageT<ROWS> st;
 #pragma unroll
-  for (int j = 0; j < kStageChunks; ++j) {
+  for (int j = 0; j < ROWS * 16 / 256; ++j) {
     const int c = tid + 256 * j;
     const int t = r0 + (c >> 4);
     st.x[j] = t < r1 ? *reinterpret_cast<const u32x4*>(X + (int64_t)t * rs + h * D + (c & 15) * 8) : u32x4{0, 0, 0, 0};
   }
   return st;
 }
-__device__ __forceinline__ void stage_store(const Stage& st, char* base, int tid) {
+template <int ROWS>
+__device__ __forceinline__ void stage_store(const StageT<ROWS>& st, char* base, int tid) {
 #pragma unroll
-  for (int j = 0; j < kStageChunks; ++j) {
+  for (int j = 0; j < ROWS * 16 / 256; ++j) {
     const int c = tid + 256 * j;
     *reinterpret_cast<u32x4*>(base + toff(c >> 4, c & 15)) = st.x[j];
   }
@@ -147,14 +155,14 @@ __device__ __forceinline__ bool dkdv_live(int kw, int q0, int s1) {  // wave-uni
 #ifndef PRL_ATTN_KV_LDS
 #define PRL_ATTN_KV_LDS 0  // A/B: 1 (K/V, Q/dO from LDS, 182 VGPRs) measured 8-12 % slower (profiles/r02_attn_regs_ab.jsonl)
 #endif
-#if PRL_ATTN_KV_LDS
-typedef const char* KvRef;
-__device__ __forceinline__ bf16x8 kv_frag(KvRef base, int l32, int c, int hi) { return row_read(base, l32, 2 * c + hi); }
-#else
-typedef const bf16x8* KvRef;
-__device__ __forceinline__ bf16x8 kv_frag(KvRef f, int, int c, int) { return f[c]; }
-#endif
-__device__ __forceinline__ void dkdv_scores(const char* tQ, const char* tdO, KvRef kf, KvRef vf, int l32, int hi,
+// 2: K (Q in the dQ role) in registers, V (dO) from an LDS image of the block: 32 KiB, so two
+// workgroups fit a CU (with PRL_ATTN_BWD_MINB = 2)
+typedef const char* LdsRef;    // rows of a swizzled LDS image
+typedef const bf16x8* RegRef;  // the lane's fragments in registers
+__device__ __forceinline__ bf16x8 kv_frag(LdsRef base, int l32, int c, int hi) { return row_read(base, l32, 2 * c + hi); }
+__device__ __forceinline__ bf16x8 kv_frag(RegRef f, int, int c, int) { return f[c]; }
+template <typename KR, typename VR>
+__device__ __forceinline__ void dkdv_scores(const char* tQ, const char* tdO, KR kf, VR vf, int l32, int hi,
                                             f32x16& S, f32x16& dP) {
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
@@ -198,8 +206,9 @@ __device__ __forceinline__ void dkdv_acc(const char* tQ, const char* tdO, int la
     }
 }
 // one tile, masked (the diagonal and ragged ends)
+template <typename KR, typename VR>
 __device__ __forceinline__ void dkdv_tile(const char* tQ, const char* tdO, const float* tL, const float* tDl, int q0,
-                                          KvRef kf, KvRef vf, int key, bool kval, int s1, int lane,
+                                          KR kf, VR vf, int key, bool kval, int s1, int lane,
                                           float c2, f32x16* dKt, f32x16* dVt) {
   const int hi = lane >> 5, l32 = lane & 31;
   f32x16 S = f32x16{}, dP = f32x16{};
@@ -209,8 +218,9 @@ __device__ __forceinline__ void dkdv_tile(const char* tQ, const char* tdO, const
   dkdv_acc(tQ, tdO, lane, pb, sb, dKt, dVt);
 }
 // two unmasked tiles (a = the stage's first 32 rows, b = the next 32), interleaved
+template <typename KR, typename VR>
 __device__ __forceinline__ void dkdv_pair(const char* tQ, const char* tdO, const float* tL, const float* tDl,
-                                          KvRef kf, KvRef vf, int key, bool kval, int s1, int lane,
+                                          KR kf, VR vf, int key, bool kval, int s1, int lane,
                                           float c2, f32x16* dKt, f32x16* dVt) {
   const int hi = lane >> 5, l32 = lane & 31;
   const char *tQb = tQ + TILE * 256, *tdOb = tdO + TILE * 256;
@@ -248,7 +258,7 @@ __device__ __forceinline__ void attn_bwd_dkdv(const __bf16* __restrict__ q, cons
   const int kw = kb + 32 * w;
   const int key = kw + l32;
   const bool kval = key < s1;
-#if PRL_ATTN_KV_LDS
+#if PRL_ATTN_KV_LDS == 1
   {  // the block's 128 K and V rows into two swizzled images (visible after the loop's first barriers)
     const Stage k0 = stage_load(k, rsk, g, kb, s1, tid), k1 = stage_load(k, rsk, g, kb + STAGE, s1, tid);
     const Stage v0 = stage_load(v, rsk, g, kb, s1, tid), v1 = stage_load(v, rsk, g, kb + STAGE, s1, tid);
@@ -257,7 +267,17 @@ __device__ __forceinline__ void attn_bwd_dkdv(const __bf16* __restrict__ q, cons
     stage_store(v0, sKV + 128 * 256, tid);
     stage_store(v1, sKV + 128 * 256 + STAGE * 256, tid);
   }
-  const KvRef kf = sKV + 32 * w * 256, vf = sKV + 128 * 256 + 32 * w * 256;
+  const LdsRef kf = sKV + 32 * w * 256, vf = sKV + 128 * 256 + 32 * w * 256;
+#elif PRL_ATTN_KV_LDS == 2
+  {  // the block's 128 V rows into a swizzled image (visible after the loop's first barriers)
+    const Stage v0 = stage_load(v, rsk, g, kb, s1, tid), v1 = stage_load(v, rsk, g, kb + STAGE, s1, tid);
+    stage_store(v0, sKV, tid);
+    stage_store(v1, sKV + STAGE * 256, tid);
+  }
+  bf16x8 kf[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) kf[c] = kval ? ld8(k + (int64_t)key * rsk + g * D + 16 * c + 8 * hi) : zero8();
+  const LdsRef vf = sKV + 32 * w * 256;
 #else
   bf16x8 kf[8], vf[8];
 #pragma unroll
@@ -274,36 +294,36 @@ __device__ __forceinline__ void attn_bwd_dkdv(const __bf16* __restrict__ q, cons
   }
 #pragma unroll 1
   for (int h = g * rep; h < (g + 1) * rep; ++h) {
-  Stage nq = stage_load(q, rsq, h, kb, s1, tid), nd = stage_load(dout, rsq, h, kb, s1, tid);
+  StageT<BSTAGE> nq = stage_load<BSTAGE>(q, rsq, h, kb, s1, tid), nd = stage_load<BSTAGE>(dout, rsq, h, kb, s1, tid);
   float nl = 0.f, ndl = 0.f;
-  if (tid < STAGE && kb + tid < s1) {
+  if (tid < BSTAGE && kb + tid < s1) {
     nl = lse2[(int64_t)h * T + kb + tid];
     ndl = delta[(int64_t)h * T + kb + tid];
   }
-  for (int q00 = kb; q00 < s1; q00 += STAGE) {
+  for (int q00 = kb; q00 < s1; q00 += BSTAGE) {
     __syncthreads();  // every wave is done with the previous stage
     stage_store(nq, sQ, tid);
     stage_store(nd, sdO, tid);
-    if (tid < STAGE) {
+    if (tid < BSTAGE) {
       sL[tid] = nl;
       sDl[tid] = ndl;
     }
     __syncthreads();
-    const int qn = q00 + STAGE;  // prefetch the next stage behind this stage's MFMAs
+    const int qn = q00 + BSTAGE;  // prefetch the next stage behind this stage's MFMAs
     if (qn < s1 && !PRL_ATTN_EXP_NOLOAD) {
-      nq = stage_load(q, rsq, h, qn, s1, tid);
-      nd = stage_load(dout, rsq, h, qn, s1, tid);
-      if (tid < STAGE && qn + tid < s1) {
+      nq = stage_load<BSTAGE>(q, rsq, h, qn, s1, tid);
+      nd = stage_load<BSTAGE>(dout, rsq, h, qn, s1, tid);
+      if (tid < BSTAGE && qn + tid < s1) {
         nl = lse2[(int64_t)h * T + qn + tid];
         ndl = delta[(int64_t)h * T + qn + tid];
       }
     }
-    if (PRL_ATTN_INTERLEAVE && kw < s1 && q00 >= kw + TILE - 1 && q00 + TILE < s1) {  // wave-uniform
+    if (PRL_ATTN_INTERLEAVE && BSTAGE == 2 * TILE && kw < s1 && q00 >= kw + TILE - 1 && q00 + TILE < s1) {  // wave-uniform
       dkdv_pair(sQ, sdO, sL, sDl, kf, vf, key, kval, s1, lane, c2, dKt, dVt);
       continue;
     }
 #pragma unroll 1
-    for (int half = 0; half < STAGE / TILE; ++half) {
+    for (int half = 0; half < BSTAGE / TILE; ++half) {
       const int q0 = q00 + TILE * half;
       if (!dkdv_live(kw, q0, s1)) continue;  // wave-uniform
       dkdv_tile(sQ + half * TILE * 256, sdO + half * TILE * 256, sL + half * TILE, sDl + half * TILE, q0, kf, vf, key,
@@ -329,7 +349,8 @@ __device__ __forceinline__ void attn_bwd_dkdv(const __bf16* __restrict__ q, cons
 __device__ __forceinline__ bool dq_live(int qw, int k0, int s1, int kend) {  // wave-uniform
   return !(qw >= s1 || k0 > qw + TILE - 1 || k0 >= kend);
 }
-__device__ __forceinline__ void dq_scores(const char* tK, const char* tV, KvRef qf, KvRef of, int l32, int hi,
+template <typename KR, typename VR>
+__device__ __forceinline__ void dq_scores(const char* tK, const char* tV, KR qf, VR of, int l32, int hi,
                                           f32x16& St, f32x16& dPt) {
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
@@ -359,7 +380,8 @@ __device__ __forceinline__ void dq_acc(const char* tK, int lane, const bf16x8* s
     for (int ks = 0; ks < 2; ++ks) dQt[dc] = mfma(tr_operand(tK, lane, dc, ks), sb[ks], dQt[dc]);
 }
 // one tile, masked
-__device__ __forceinline__ void dq_tile(const char* tK, const char* tV, int k0, KvRef qf, KvRef of,
+template <typename KR, typename VR>
+__device__ __forceinline__ void dq_tile(const char* tK, const char* tV, int k0, KR qf, VR of,
                                         int qq, bool qval, int s1, int lane, float c2, float lq, float dq_delta,
                                         f32x16* dQt) {
   const int hi = lane >> 5, l32 = lane & 31;
@@ -370,7 +392,8 @@ __device__ __forceinline__ void dq_tile(const char* tK, const char* tV, int k0, 
   dq_acc(tK, lane, sb, dQt);
 }
 // two unmasked tiles, interleaved as in dkdv_pair
-__device__ __forceinline__ void dq_pair(const char* tK, const char* tV, KvRef qf, KvRef of, int qq,
+template <typename KR, typename VR>
+__device__ __forceinline__ void dq_pair(const char* tK, const char* tV, KR qf, VR of, int qq,
                                         bool qval, int s1, int lane, float c2, float lq, float dq_delta, f32x16* dQt) {
   const int hi = lane >> 5, l32 = lane & 31;
   const char *tKb = tK + TILE * 256, *tVb = tV + TILE * 256;
@@ -403,7 +426,7 @@ __device__ __forceinline__ void attn_bwd_dq(const __bf16* __restrict__ q, const 
   const int qw = qb + 32 * w;
   const int qq = qw + l32;
   const bool qval = qq < s1;
-#if PRL_ATTN_KV_LDS
+#if PRL_ATTN_KV_LDS == 1
   {  // the block's 128 Q and dO rows into two swizzled images (visible after the loop's barriers)
     const Stage q0 = stage_load(q, rs, h, qb, s1, tid), q1 = stage_load(q, rs, h, qb + STAGE, s1, tid);
     const Stage o0 = stage_load(dout, rs, h, qb, s1, tid), o1 = stage_load(dout, rs, h, qb + STAGE, s1, tid);
@@ -412,7 +435,17 @@ __device__ __forceinline__ void attn_bwd_dq(const __bf16* __restrict__ q, const 
     stage_store(o0, sQO + 128 * 256, tid);
     stage_store(o1, sQO + 128 * 256 + STAGE * 256, tid);
   }
-  const KvRef qf = sQO + 32 * w * 256, of = sQO + 128 * 256 + 32 * w * 256;
+  const LdsRef qf = sQO + 32 * w * 256, of = sQO + 128 * 256 + 32 * w * 256;
+#elif PRL_ATTN_KV_LDS == 2
+  {  // the block's 128 dO rows into a swizzled image (visible after the loop's barriers)
+    const Stage o0 = stage_load(dout, rs, h, qb, s1, tid), o1 = stage_load(dout, rs, h, qb + STAGE, s1, tid);
+    stage_store(o0, sQO, tid);
+    stage_store(o1, sQO + STAGE * 256, tid);
+  }
+  bf16x8 qf[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) qf[c] = qval ? ld8(q + (int64_t)qq * rs + h * D + 16 * c + 8 * hi) : zero8();
+  const LdsRef of = sQO + 32 * w * 256;
 #else
   bf16x8 qf[8], of[8];
 #pragma unroll
@@ -427,22 +460,22 @@ __device__ __forceinline__ void attn_bwd_dq(const __bf16* __restrict__ q, const 
 #pragma unroll
   for (int i = 0; i < 4; ++i) dQt[i] = f32x16{};
   const int kend = (qb + 128 < s1 ? qb + 128 : s1);  // causal: keys <= the block's last query
-  Stage nk = stage_load(k, rsk, g, s0, s1, tid), nv = stage_load(v, rsk, g, s0, s1, tid);
-  for (int k00 = s0; k00 < kend; k00 += STAGE) {
+  StageT<BSTAGE> nk = stage_load<BSTAGE>(k, rsk, g, s0, s1, tid), nv = stage_load<BSTAGE>(v, rsk, g, s0, s1, tid);
+  for (int k00 = s0; k00 < kend; k00 += BSTAGE) {
     __syncthreads();
     stage_store(nk, sK, tid);
     stage_store(nv, sV, tid);
     __syncthreads();
-    if (k00 + STAGE < kend && !PRL_ATTN_EXP_NOLOAD) {
-      nk = stage_load(k, rsk, g, k00 + STAGE, s1, tid);
-      nv = stage_load(v, rsk, g, k00 + STAGE, s1, tid);
+    if (k00 + BSTAGE < kend && !PRL_ATTN_EXP_NOLOAD) {
+      nk = stage_load<BSTAGE>(k, rsk, g, k00 + BSTAGE, s1, tid);
+      nv = stage_load<BSTAGE>(v, rsk, g, k00 + BSTAGE, s1, tid);
     }
-    if (PRL_ATTN_INTERLEAVE && qw < s1 && k00 + STAGE - 1 <= qw && k00 + STAGE <= s1) {  // wave-uniform
+    if (PRL_ATTN_INTERLEAVE && BSTAGE == 2 * TILE && qw < s1 && k00 + BSTAGE - 1 <= qw && k00 + BSTAGE <= s1) {  // wave-uniform
       dq_pair(sK, sV, qf, of, qq, qval, s1, lane, c2, lq, dq_delta, dQt);
       continue;
     }
 #pragma unroll 1
-    for (int half = 0; half < STAGE / TILE; ++half) {
+    for (int half = 0; half < BSTAGE / TILE; ++half) {
       const int k0 = k00 + TILE * half;
       if (!dq_live(qw, k0, s1, kend)) continue;  // wave-uniform
       dq_tile(sK + half * TILE * 256, sV + half * TILE * 256, k0, qf, of, qq, qval, s1, lane, c2, lq, dq_delta, dQt);
@@ -480,7 +513,10 @@ __device__ __forceinline__ int xcd_group_remap(int b, int n, int G) {
 
 // One launch for both roles: workgroups [0, n_kv * Hkv) compute dK/dV of a (key block, kv head),
 // the rest dQ of a (query block, query head), so the lighter dQ workgroups fill the causal tail.
-__global__ __launch_bounds__(256) void attn_bwd_fused(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
+#ifndef PRL_ATTN_BWD_MINB
+#define PRL_ATTN_BWD_MINB 1  // A/B: 2 = two workgroups per CU (<= 256 registers per lane)
+#endif
+__global__ __launch_bounds__(256, PRL_ATTN_BWD_MINB) void attn_bwd_fused(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
                                                       const __bf16* __restrict__ v, const __bf16* __restrict__ dout,
                                                       const float* __restrict__ lse2, const float* __restrict__ delta,
                                                       const int32_t* __restrict__ kv_items, int n_kv,
@@ -490,7 +526,8 @@ __global__ __launch_bounds__(256) void attn_bwd_fused(const __bf16* __restrict__
   __shared__ __attribute__((aligned(16))) char s0[STAGE * D * 2], s1[STAGE * D * 2];
   __shared__ __attribute__((aligned(16))) float sL[STAGE], sDl[STAGE];
 #if PRL_ATTN_KV_LDS
-  __shared__ __attribute__((aligned(16))) char sKV[2 * 128 * D * 2];  // K and V images of the key block
+  // K and V (mode 2: V) images of the key block; the dQ role's Q and dO (dO)
+  __shared__ __attribute__((aligned(16))) char sKV[(PRL_ATTN_KV_LDS == 1 ? 2 : 1) * 128 * D * 2];
 #else
   char* sKV = nullptr;
 #endif
