@@ -302,6 +302,16 @@ int prl_attn_bwd(const void* q, const void* k, const void* v, const void* dout, 
                  const float* delta, const int32_t* kv_items, int32_t n_kv_items, const int32_t* q_items,
                  int32_t n_q_items, void* dq, void* dk, void* dv, int64_t tokens, int32_t heads,
                  int32_t kv_heads, int32_t head_dim, float scale, void* stream);
+/* prl_attn_bwd with heavy dK/dV work split over the query heads of its group: split_units are
+ * int32 7-tuples (seq_start, seq_end, block_start, kv_head, head_lo, head_hi, slot) run before the
+ * kv_items (which must then leave those key blocks out); each writes fp32 partial dK / dV to
+ * parts + slot * 2 * 128 * 128; split_groups are int32 5-tuples (seq_end, block_start, kv_head,
+ * first_slot, n_parts) summed in part order into bf16 dk / dv by a second launch (deterministic). */
+int prl_attn_bwd_split(const void* q, const void* k, const void* v, const void* dout, const float* lse2,
+                       const float* delta, const int32_t* kv_items, int32_t n_kv_items, const int32_t* q_items,
+                       int32_t n_q_items, const int32_t* split_units, int32_t n_split, const int32_t* split_groups,
+                       int32_t n_groups, float* parts, void* dq, void* dk, void* dv, int64_t tokens, int32_t heads,
+                       int32_t kv_heads, int32_t head_dim, float scale, void* stream);
 
 #ifdef __cplusplus
 }

@@ -112,6 +112,9 @@ _SIGNATURES = {
     "prl_attn_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,
                              c_int32, c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32, c_int32, c_float,
                              c_void_p]),
+    "prl_attn_bwd_split": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32,
+                                   c_void_p, c_int32, c_void_p, c_int32, c_void_p, c_int32, c_void_p, c_void_p,
+                                   c_void_p, c_void_p, c_int64, c_int32, c_int32, c_int32, c_float, c_void_p]),
 }
 
 _lib = None

@@ -243,15 +243,17 @@ __device__ __forceinline__ void dkdv_pair(const char* tQ, const char* tdO, const
 // GQA: k / v / dk / dv have Hkv heads, q / dout / dq have H = rep * Hkv; the dK/dV role of kv head
 // g sweeps the query heads g*rep .. g*rep+rep-1 (all of its group), so dK / dV are complete sums
 // in registers with no atomics.
+// h0 .. h1-1: the query heads this workgroup sweeps (all of the group, or a part of it for a split
+// heavy key block); part != null: write the unscaled fp32 accumulators there ([2][128][128],
+// dK then dV, row = key - kb) for attn_bwd_dkdv_reduce instead of bf16 dk / dv.
 __device__ __forceinline__ void attn_bwd_dkdv(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
                                               const __bf16* __restrict__ v, const __bf16* __restrict__ dout,
                                               const float* __restrict__ lse2, const float* __restrict__ delta,
-                                              const int32_t* __restrict__ items, __bf16* __restrict__ dk,
-                                              __bf16* __restrict__ dv, int64_t T, int H, int Hkv, float c2,
-                                              float scale, int it, int g, char* sQ, char* sdO, float* sL,
+                                              int s1, int kb, int h0, int h1, __bf16* __restrict__ dk,
+                                              __bf16* __restrict__ dv, float* __restrict__ part, int64_t T, int H,
+                                              int Hkv, float c2, float scale, int g, char* sQ, char* sdO, float* sL,
                                               float* sDl, char* sKV) {
   const int tid = threadIdx.x;
-  const int s1 = items[3 * it + 1], kb = items[3 * it + 2];
   const int lane = tid & 63, w = tid >> 6, hi = lane >> 5, l32 = lane & 31;
   const int64_t rsq = (int64_t)H * D, rsk = (int64_t)Hkv * D;
   const int rep = H / Hkv;
@@ -293,7 +295,7 @@ __device__ __forceinline__ void attn_bwd_dkdv(const __bf16* __restrict__ q, cons
     dVt[i] = f32x16{};
   }
 #pragma unroll 1
-  for (int h = g * rep; h < (g + 1) * rep; ++h) {
+  for (int h = h0; h < h1; ++h) {
   StageT<BSTAGE> nq = stage_load<BSTAGE>(q, rsq, h, kb, s1, tid), nd = stage_load<BSTAGE>(dout, rsq, h, kb, s1, tid);
   float nl = 0.f, ndl = 0.f;
   if (tid < BSTAGE && kb + tid < s1) {
@@ -332,6 +334,21 @@ __device__ __forceinline__ void attn_bwd_dkdv(const __bf16* __restrict__ q, cons
   }
   }
   if (!kval) return;
+  if (part) {
+    float* pk = part + (int64_t)(key - kb) * D;
+    float* pv = pk + 128 * D;
+#pragma unroll
+    for (int dc = 0; dc < 4; ++dc)
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        const int d0 = 32 * dc + 8 * gg + 4 * hi;
+        *reinterpret_cast<f32x4*>(pk + d0) = f32x4{dKt[dc][4 * gg], dKt[dc][4 * gg + 1], dKt[dc][4 * gg + 2],
+                                                   dKt[dc][4 * gg + 3]};
+        *reinterpret_cast<f32x4*>(pv + d0) = f32x4{dVt[dc][4 * gg], dVt[dc][4 * gg + 1], dVt[dc][4 * gg + 2],
+                                                   dVt[dc][4 * gg + 3]};
+      }
+    return;
+  }
   __bf16* dkr = dk + (int64_t)key * rsk + g * D;
   __bf16* dvr = dv + (int64_t)key * rsk + g * D;
 #pragma unroll
@@ -511,8 +528,11 @@ __device__ __forceinline__ int xcd_group_remap(int b, int n, int G) {
   return ((sl / G) * 8 + x) * G + sl % G;
 }
 
-// One launch for both roles: workgroups [0, n_kv * Hkv) compute dK/dV of a (key block, kv head),
-// the rest dQ of a (query block, query head), so the lighter dQ workgroups fill the causal tail.
+// One launch for both roles: workgroups [0, n_split) are the parts of split heavy dK/dV work
+// (split units: int32 (seq_start, seq_end, block_start, kv head, h0, h1, slot), each writing fp32
+// partials to parts + slot * 2 * 128 * 128), [n_split, n_split + n_kv * Hkv) compute dK/dV of a
+// (key block, kv head) over the whole query-head group, the rest dQ of a (query block, query
+// head), so the lighter dQ workgroups fill the causal tail.
 #ifndef PRL_ATTN_BWD_MINB
 #define PRL_ATTN_BWD_MINB 1  // A/B: 2 = two workgroups per CU (<= 256 registers per lane)
 #endif
@@ -522,7 +542,9 @@ __global__ __launch_bounds__(256, PRL_ATTN_BWD_MINB) void attn_bwd_fused(const _
                                                       const int32_t* __restrict__ kv_items, int n_kv,
                                                       const int32_t* __restrict__ q_items, __bf16* __restrict__ dq,
                                                       __bf16* __restrict__ dk, __bf16* __restrict__ dv, int64_t T,
-                                                      int H, int Hkv, float c2, float scale) {
+                                                      int H, int Hkv, float c2, float scale,
+                                                      const int32_t* __restrict__ split_units, int n_split,
+                                                      float* __restrict__ parts) {
   __shared__ __attribute__((aligned(16))) char s0[STAGE * D * 2], s1[STAGE * D * 2];
   __shared__ __attribute__((aligned(16))) float sL[STAGE], sDl[STAGE];
 #if PRL_ATTN_KV_LDS
@@ -532,13 +554,53 @@ __global__ __launch_bounds__(256, PRL_ATTN_BWD_MINB) void attn_bwd_fused(const _
   char* sKV = nullptr;
 #endif
   const int b = blockIdx.x;
-  if (b < n_kv * Hkv)
-    attn_bwd_dkdv(q, k, v, dout, lse2, delta, kv_items, dk, dv, T, H, Hkv, c2, scale, b / Hkv, b % Hkv, s0, s1, sL,
-                  sDl, sKV);
-  else {
-    const int lq = xcd_group_remap(b - n_kv * Hkv, (int)gridDim.x - n_kv * Hkv, H / Hkv);
+  const int rep = H / Hkv;
+  if (b < n_split) {
+    const int32_t* u = split_units + 7 * b;
+    attn_bwd_dkdv(q, k, v, dout, lse2, delta, u[1], u[2], u[4], u[5], dk, dv, parts + (int64_t)u[6] * 2 * 128 * D, T,
+                  H, Hkv, c2, scale, u[3], s0, s1, sL, sDl, sKV);
+  } else if (b < n_split + n_kv * Hkv) {
+    const int it = (b - n_split) / Hkv, g = (b - n_split) % Hkv;
+    attn_bwd_dkdv(q, k, v, dout, lse2, delta, kv_items[3 * it + 1], kv_items[3 * it + 2], g * rep, (g + 1) * rep, dk,
+                  dv, nullptr, T, H, Hkv, c2, scale, g, s0, s1, sL, sDl, sKV);
+  } else {
+    const int nd = n_split + n_kv * Hkv;
+    const int lq = xcd_group_remap(b - nd, (int)gridDim.x - nd, rep);
     attn_bwd_dq(q, k, v, dout, lse2, delta, q_items, dq, T, H, Hkv, c2, scale, lq / H, lq % H, s0, s1, sKV);
   }
+}
+
+// dK / dV of split key blocks: the parts' fp32 partials summed in part order (deterministic),
+// dK scaled, rounded to bf16.  groups: int32 (seq_end, block_start, kv head, first slot, parts);
+// one thread per (key, 8 head-dim columns), 16 keys per 256-thread workgroup.
+__global__ __launch_bounds__(256) void attn_bwd_dkdv_reduce(const float* __restrict__ parts,
+                                                            const int32_t* __restrict__ groups,
+                                                            __bf16* __restrict__ dk, __bf16* __restrict__ dv, int Hkv,
+                                                            float scale) {
+  const int gi = blockIdx.x >> 3;  // 8 workgroups x 16 keys per 128-key block
+  const int32_t* gr = groups + 5 * gi;
+  const int s1 = gr[0], kb = gr[1], g = gr[2], slot0 = gr[3], np = gr[4];
+  const int r = ((blockIdx.x & 7) << 4) + (threadIdx.x >> 4), c8 = (threadIdx.x & 15) * 8;
+  const int key = kb + r;
+  if (key >= s1) return;
+  float ak[8] = {}, av[8] = {};
+  for (int p = 0; p < np; ++p) {
+    const float* pk = parts + (int64_t)(slot0 + p) * 2 * 128 * D + (int64_t)r * D + c8;
+    const f32x4 k0 = *reinterpret_cast<const f32x4*>(pk), k1 = *reinterpret_cast<const f32x4*>(pk + 4);
+    const f32x4 v0 = *reinterpret_cast<const f32x4*>(pk + 128 * D), v1 = *reinterpret_cast<const f32x4*>(pk + 128 * D + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      ak[j] += k0[j];
+      ak[4 + j] += k1[j];
+      av[j] += v0[j];
+      av[4 + j] += v1[j];
+    }
+  }
+  const int64_t o = (int64_t)key * Hkv * D + (int64_t)g * D + c8;
+  st4(dk + o, scale * ak[0], scale * ak[1], scale * ak[2], scale * ak[3]);
+  st4(dk + o + 4, scale * ak[4], scale * ak[5], scale * ak[6], scale * ak[7]);
+  st4(dv + o, av[0], av[1], av[2], av[3]);
+  st4(dv + o + 4, av[4], av[5], av[6], av[7]);
 }
 
 // Forward (same structure as the dQ role): one workgroup = 128 queries of one query head, each
@@ -755,23 +817,52 @@ int prl_attn_bwd_delta(const void* out, const void* dout, float* delta, int64_t 
   return (int)hipGetLastError();
 }
 
+static int attn_bwd_launch(const void* q, const void* k, const void* v, const void* dout, const float* lse2,
+                           const float* delta, const int32_t* kv_items, int32_t n_kv_items, const int32_t* q_items,
+                           int32_t n_q_items, const int32_t* split_units, int32_t n_split,
+                           const int32_t* split_groups, int32_t n_groups, float* parts, void* dq, void* dk, void* dv,
+                           int64_t tokens, int32_t heads, int32_t kv_heads, int32_t head_dim, float scale,
+                           void* stream) {
+  if (!q || !k || !v || !dout || !lse2 || !delta || !dq || !dk || !dv || tokens < 0 || heads <= 0 || kv_heads <= 0 ||
+      heads % kv_heads || n_kv_items < 0 || n_q_items < 0 || (n_kv_items && !kv_items) || (n_q_items && !q_items) ||
+      n_split < 0 || n_groups < 0 || (n_split && (!split_units || !parts)) || (n_groups && (!split_groups || !parts)))
+    return PRL_E_INVALID;
+  if (head_dim != D) return PRL_E_UNSUPPORTED;
+  const int64_t blocks = (int64_t)n_split + (int64_t)n_kv_items * kv_heads + (int64_t)n_q_items * heads;
+  if (blocks > 0x7FFFFFFF || (int64_t)n_groups * 8 > 0x7FFFFFFF) return PRL_E_UNSUPPORTED;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const float c2 = scale * 1.4426950408889634f;
+  if (blocks > 0) {
+    hipLaunchKernelGGL(attn_bwd_fused, dim3((unsigned)blocks), dim3(256), 0, s, (const __bf16*)q, (const __bf16*)k,
+                       (const __bf16*)v, (const __bf16*)dout, lse2, delta, kv_items, (int)n_kv_items, q_items,
+                       (__bf16*)dq, (__bf16*)dk, (__bf16*)dv, tokens, (int)heads, (int)kv_heads, c2, scale,
+                       split_units, (int)n_split, parts);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+  }
+  if (n_groups > 0) {
+    hipLaunchKernelGGL(attn_bwd_dkdv_reduce, dim3((unsigned)(8 * n_groups)), dim3(256), 0, s, parts, split_groups,
+                       (__bf16*)dk, (__bf16*)dv, (int)kv_heads, scale);
+    return (int)hipGetLastError();
+  }
+  return PRL_OK;
+}
+
 int prl_attn_bwd(const void* q, const void* k, const void* v, const void* dout, const float* lse2, const float* delta,
                  const int32_t* kv_items, int32_t n_kv_items, const int32_t* q_items, int32_t n_q_items, void* dq,
                  void* dk, void* dv, int64_t tokens, int32_t heads, int32_t kv_heads, int32_t head_dim, float scale,
                  void* stream) {
-  if (!q || !k || !v || !dout || !lse2 || !delta || !dq || !dk || !dv || tokens < 0 || heads <= 0 || kv_heads <= 0 ||
-      heads % kv_heads || n_kv_items < 0 || n_q_items < 0 || (n_kv_items && !kv_items) || (n_q_items && !q_items))
-    return PRL_E_INVALID;
-  if (head_dim != D) return PRL_E_UNSUPPORTED;
-  const int64_t blocks = (int64_t)n_kv_items * kv_heads + (int64_t)n_q_items * heads;
-  if (blocks > 0x7FFFFFFF) return PRL_E_UNSUPPORTED;
-  if (blocks == 0) return PRL_OK;
-  const float c2 = scale * 1.4426950408889634f;
-  hipLaunchKernelGGL(attn_bwd_fused, dim3((unsigned)blocks), dim3(256), 0, static_cast<hipStream_t>(stream),
-                     (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, (const __bf16*)dout, lse2, delta, kv_items,
-                     (int)n_kv_items, q_items, (__bf16*)dq, (__bf16*)dk, (__bf16*)dv, tokens, (int)heads,
-                     (int)kv_heads, c2, scale);
-  return (int)hipGetLastError();
+  return attn_bwd_launch(q, k, v, dout, lse2, delta, kv_items, n_kv_items, q_items, n_q_items, nullptr, 0, nullptr, 0,
+                         nullptr, dq, dk, dv, tokens, heads, kv_heads, head_dim, scale, stream);
+}
+
+int prl_attn_bwd_split(const void* q, const void* k, const void* v, const void* dout, const float* lse2,
+                       const float* delta, const int32_t* kv_items, int32_t n_kv_items, const int32_t* q_items,
+                       int32_t n_q_items, const int32_t* split_units, int32_t n_split, const int32_t* split_groups,
+                       int32_t n_groups, float* parts, void* dq, void* dk, void* dv, int64_t tokens, int32_t heads,
+                       int32_t kv_heads, int32_t head_dim, float scale, void* stream) {
+  return attn_bwd_launch(q, k, v, dout, lse2, delta, kv_items, n_kv_items, q_items, n_q_items, split_units, n_split,
+                         split_groups, n_groups, parts, dq, dk, dv, tokens, heads, kv_heads, head_dim, scale, stream);
 }
 
 }  // extern "C"

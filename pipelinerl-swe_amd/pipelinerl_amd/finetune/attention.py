@@ -48,6 +48,63 @@ def _items(bounds: list[int], device) -> tuple:
     return hit
 
 
+_SPLITS: dict[tuple, tuple] = {}
+SPLIT_MIN_RATIO = 1.2
+
+
+def split_plan(bounds: list[int], heads: int, kv_heads: int, cus: int) -> tuple[list, list, list, int]:
+    """Which dK/dV key blocks to split over the query heads of their group (host arithmetic only).
+
+    A dK/dV workgroup sweeps all ``rep = heads / kv_heads`` query heads over every query after its
+    key block: for the first blocks of a long sequence that is far more than a CU's share of the
+    launch (a lone 4 096-token sequence at 28 / 4 heads: its first workgroup alone runs as long as
+    two whole sequences, profiles/r02_attn_ragged.jsonl).  Work is counted in MFMAs per wave (one
+    wave per SIMD: a workgroup's duration follows it): dK/dV 32 per 32-query tile per query head,
+    dQ 24 per 32-key tile.  Key blocks whose workgroup exceeds 1.2 x target, target = max(the
+    per-SIMD average, the largest dQ workgroup), are cut into min(rep, ceil(work / target))
+    contiguous head ranges (below 1.2 the split measured no faster: profiles/r02_attn_split_ab.jsonl).
+
+    Returns (kv_rows, split_units, split_groups, slots): the unsplit (seq_start, seq_end,
+    block_start) rows, the 7-tuples and 5-tuples of prl_attn_bwd_split, and the partial slots."""
+    rep = heads // kv_heads
+    rows = [(a, b, x) for a, b in zip(bounds[:-1], bounds[1:]) for x in range(a, b, BLOCK)]
+    w_kv = {r: rep * 32 * -(-(r[1] - r[2]) // 32) for r in rows}
+    w_q = [24 * -(-(min(r[2] + BLOCK, r[1]) - r[0]) // 32) for r in rows]
+    total = 4 * (kv_heads * sum(w_kv.values()) + heads * sum(w_q))
+    target = max(total / (4 * max(1, cus)), max(w_q, default=0), 1)
+    kv_rows, units, groups, slot = [], [], [], 0
+    for r in rows:
+        parts = min(rep, -(-w_kv[r] // int(target))) if w_kv[r] > SPLIT_MIN_RATIO * target else 1
+        if parts <= 1:
+            kv_rows.append(r)
+            continue
+        cuts = [rep * i // parts for i in range(parts + 1)]
+        for g in range(kv_heads):
+            groups.append((r[1], r[2], g, slot, parts))
+            for p in range(parts):
+                units.append((r[0], r[1], r[2], g, g * rep + cuts[p], g * rep + cuts[p + 1], slot))
+                slot += 1
+    units.sort(key=lambda u: -(u[5] - u[4]) * (u[1] - u[2]))  # heaviest first
+    return kv_rows, units, groups, slot
+
+
+def _split_items(bounds: list[int], heads: int, kv_heads: int, device) -> tuple:
+    """Device tensors of split_plan (cached per packing): (kv_items, n_kv, units, n_units, groups,
+    n_groups, slots)."""
+    key = (tuple(bounds), heads, kv_heads, str(device))
+    hit = _SPLITS.get(key)
+    if hit is None:
+        cus = torch.cuda.get_device_properties(device).multi_processor_count
+        kv_rows, units, groups, slots = split_plan(bounds, heads, kv_heads, cus)
+        kv_rows = sorted(kv_rows, key=lambda r: -(r[1] - r[2]))
+        mk = lambda rr, w: torch.tensor(rr if rr else [(0,) * w], dtype=torch.int32).to(device)  # noqa: E731
+        hit = (mk(kv_rows, 3), len(kv_rows), mk(units, 7), len(units), mk(groups, 5), len(groups), slots)
+        if len(_SPLITS) > 64:
+            _SPLITS.clear()
+        _SPLITS[key] = hit
+    return hit
+
+
 class PackedCausalAttention(torch.autograd.Function):
     """HIP flash-attention forward (prl_attn_fwd; PRL_ATTN_FWD=torch: torch's varlen forward, its
     log-sum-exp converted) and HIP backward (prl_attn_bwd; tools/attn_backend_probe.py,
@@ -100,6 +157,15 @@ class PackedCausalAttention(torch.autograd.Function):
                                                       T, H, D, st), "prl_attn_bwd_preprocess")
         kv_items, q_items, n = _items(ctx.bounds, q.device)
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        if os.environ.get("PRL_ATTN_SPLIT", "1") != "0":  # heavy key blocks split over query heads
+            kv_s, n_kv, units, n_units, groups, n_groups, slots = _split_items(ctx.bounds, H, k.shape[1], q.device)
+            parts = torch.empty((max(slots, 1), 2, BLOCK, D), dtype=torch.float32, device=q.device)
+            _native.check(lib.prl_attn_bwd_split(
+                q.data_ptr(), k.data_ptr(), v.data_ptr(), dout.data_ptr(), lse2.data_ptr(), delta.data_ptr(),
+                kv_s.data_ptr(), n_kv, q_items.data_ptr(), n, units.data_ptr(), n_units, groups.data_ptr(), n_groups,
+                parts.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), T, H, k.shape[1], D, D ** -0.5, st),
+                "prl_attn_bwd_split")
+            return dq, dk, dv, None, None, None
         _native.check(lib.prl_attn_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), dout.data_ptr(), lse2.data_ptr(),
                                        delta.data_ptr(), kv_items.data_ptr(), n, q_items.data_ptr(), n, dq.data_ptr(),
                                        dk.data_ptr(), dv.data_ptr(), T, H, k.shape[1], D, D ** -0.5, st),

@@ -76,3 +76,35 @@ def test_hip_backward_matches(bounds, fwd, monkeypatch):
         assert err_ours <= max(1e-2, 2 * err_lib), (name, err_ours, err_lib)
     c = _run(ours, q, k, v, do)  # deterministic: no atomics
     assert all(torch.equal(x, y) for x, y in zip(a[1:], c[1:]))
+
+
+@pytest.mark.parametrize("heads", [(12, 2), (28, 4)])
+@pytest.mark.parametrize("bounds", [[0, 4096], [0, 3000, 3400, 3500], [0, 3160, 6443]])
+def test_split_heavy_key_blocks(bounds, heads, monkeypatch):
+    """Heavy dK/dV key blocks split over query heads (prl_attn_bwd_split, the default): dq
+    bit-identical to the unsplit launch, dk / dv within the unsplit kernel's error of the fp32
+    reference (the partial sums change the fp32 summation order), runs bitwise repeatable, and the
+    plan does split these packings."""
+    from pipelinerl_amd.finetune.attention import PackedCausalAttention, split_plan
+
+    assert split_plan(bounds, *heads, torch.cuda.get_device_properties(0).multi_processor_count)[1]
+    q, k, v, do = _inputs(bounds, *heads, seed=4)
+    cu = torch.tensor(bounds, dtype=torch.int32, device=DEV)
+    mx = max(b - a for a, b in zip(bounds[:-1], bounds[1:]))
+
+    def ours(qq, kk, vv):
+        return PackedCausalAttention.apply(qq, kk, vv, cu, mx, bounds)
+
+    monkeypatch.setenv("PRL_ATTN_SPLIT", "0")
+    a = _run(ours, q, k, v, do)
+    monkeypatch.setenv("PRL_ATTN_SPLIT", "1")
+    b = _run(ours, q, k, v, do)
+    c = _run(ours, q, k, v, do)
+    ref = _fp32_ref(q, k, v, do, bounds)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])  # out, dq
+    for name, x, y, r in zip(("dk", "dv"), a[2:], b[2:], ref[2:]):
+        scale = float(r.abs().max())
+        err_split = float((y.float() - r).abs().max()) / scale
+        err_one = float((x.float() - r).abs().max()) / scale
+        assert err_split <= max(1e-2, 1.5 * err_one), (name, err_split, err_one)
+    assert all(torch.equal(x, y) for x, y in zip(b, c))
