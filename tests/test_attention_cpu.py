@@ -60,3 +60,31 @@ def check(tmp_path, device):
 
 def test_varlen_fallback_cpu(tmp_path):
     check(tmp_path, "cpu")
+
+
+def test_split_plan_covers_every_block_once():
+    """split_plan (host side of prl_attn_bwd_split): every (key block, kv head) is computed exactly
+    once — unsplit, or as parts whose query-head ranges tile the group in order — the slots are
+    0..n-1, groups point at their parts, heavy blocks of a lone sequence are split and a packing
+    of many equal sequences is not (below the 1.2 x target threshold)."""
+    from pipelinerl_amd.finetune.attention import BLOCK, split_plan
+
+    for bounds, heads, kv in (([0, 4096], 28, 4), ([0, 6122], 12, 2), ([0, 3000, 3400, 3500], 28, 4),
+                              ([0, 8192, 16384], 28, 4), ([0, 1, 37, 300, 531, 1024, 1151], 12, 2)):
+        rep = heads // kv
+        kv_rows, units, groups, slots = split_plan(bounds, heads, kv, 256)
+        blocks = {(a, b, x) for a, b in zip(bounds[:-1], bounds[1:]) for x in range(a, b, BLOCK)}
+        split_blocks = {(u[0], u[1], u[2]) for u in units}
+        assert set(kv_rows) | split_blocks == blocks and not (set(kv_rows) & split_blocks)
+        assert sorted(u[6] for u in units) == list(range(slots))
+        by_slot = {u[6]: u for u in units}
+        for s1, kb, g, slot0, n in groups:
+            parts = [by_slot[slot0 + p] for p in range(n)]
+            assert all(p[1] == s1 and p[2] == kb and p[3] == g for p in parts)
+            assert [p[4] for p in parts] == [g * rep] + [p[5] for p in parts[:-1]]  # contiguous, in order
+            assert parts[-1][5] == (g + 1) * rep and 2 <= n <= rep
+        assert len(groups) == len({(u[0], u[1], u[2], u[3]) for u in units})
+        if bounds in ([0, 4096], [0, 6122]):
+            assert units
+        if bounds == [0, 8192, 16384]:
+            assert not units
