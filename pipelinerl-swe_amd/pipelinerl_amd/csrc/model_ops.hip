@@ -448,6 +448,142 @@ __global__ __launch_bounds__(256) void swiglu_bwd(const u32x4* __restrict__ dh, 
   }
 }
 
+// Read / write phased SwiGLU (PRL_SWIGLU_PHASED, the loss head's schedule: csrc/grpo_loss.hip):
+// one 1024-thread workgroup per CU walks chunks of 1024 x UP vectors; per chunk every thread loads
+// all of its inputs, computes, stores, and waits for its stores to retire before the next chunk's
+// loads, so a CU never mixes HBM reads and writes.  Same per-element arithmetic (bit-identical).
+#ifndef PRL_SWIGLU_PHASED
+// contiguous kernels (micro-batches above the fused gate/up limit, e.g. C2's 65 536 tokens):
+// fwd 0.81 -> 0.74-0.77 ms, bwd 1.29-1.33 -> 1.07-1.08 ms at 65 536 x 8 960 (profiles/r02_swiglu_phased_ab.jsonl)
+#define PRL_SWIGLU_PHASED 1
+#endif
+#ifndef PRL_SWIGLU_ROWS_PHASED
+// row-strided kernels (fused gate/up, C3): the C3 step measured no gain (1477-1481 vs 1480-1483 ms)
+#define PRL_SWIGLU_ROWS_PHASED 0
+#endif
+constexpr int kPhFwdU = 8, kPhBwdU = 6;
+__global__ __launch_bounds__(1024) void swiglu_fwd_phased(const u32x4* __restrict__ g, const u32x4* __restrict__ u,
+                                                         u32x4* __restrict__ h, int64_t n8) {
+  constexpr int U = kPhFwdU;
+  const int64_t chunk = 1024 * U;
+  for (int64_t base = (int64_t)blockIdx.x * chunk; base < n8; base += (int64_t)gridDim.x * chunk) {
+    u32x4 gv[U], uv[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const int64_t i = base + k * 1024 + threadIdx.x;
+      gv[k] = i < n8 ? __builtin_nontemporal_load(g + i) : u32x4{0, 0, 0, 0};
+      uv[k] = i < n8 ? __builtin_nontemporal_load(u + i) : u32x4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const int64_t i = base + k * 1024 + threadIdx.x;
+      if (i < n8) __builtin_nontemporal_store(swiglu_vec(gv[k], uv[k]), h + i);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
+__global__ __launch_bounds__(1024) void swiglu_bwd_phased(const u32x4* __restrict__ dh, const u32x4* __restrict__ g,
+                                                         const u32x4* __restrict__ u, u32x4* __restrict__ dg,
+                                                         u32x4* __restrict__ du, int64_t n8) {
+  constexpr int U = kPhBwdU;
+  const int64_t chunk = 1024 * U;
+  for (int64_t base = (int64_t)blockIdx.x * chunk; base < n8; base += (int64_t)gridDim.x * chunk) {
+    u32x4 dv[U], gv[U], uv[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const int64_t i = base + k * 1024 + threadIdx.x;
+      dv[k] = i < n8 ? __builtin_nontemporal_load(dh + i) : u32x4{0, 0, 0, 0};
+      gv[k] = i < n8 ? __builtin_nontemporal_load(g + i) : u32x4{0, 0, 0, 0};
+      uv[k] = i < n8 ? __builtin_nontemporal_load(u + i) : u32x4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const int64_t i = base + k * 1024 + threadIdx.x;
+      u32x4 og, ou;
+      swiglu_bwd_vec(dv[k], gv[k], uv[k], og, ou);
+      if (i < n8) {
+        __builtin_nontemporal_store(og, dg + i);
+        __builtin_nontemporal_store(ou, du + i);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
+
+// the same for the row-strided forms below: vector i of the [rows, cols8] problem is (i / cols8,
+// i % cols8), a thread's vectors 1024 apart (row / column advanced incrementally)
+__device__ __forceinline__ void rc_of(int64_t i, int cols8, int64_t& r, int& c) {
+  r = i / cols8;
+  c = (int)(i - r * cols8);
+}
+__device__ __forceinline__ void rc_step(int cols8, int64_t& r, int& c) {
+  c += 1024;
+  while (c >= cols8) {
+    c -= cols8;
+    ++r;
+  }
+}
+__global__ __launch_bounds__(1024) void swiglu_fwd_rows_phased(const u32x4* __restrict__ g, const u32x4* __restrict__ u,
+                                                              u32x4* __restrict__ h, int64_t rows, int cols8,
+                                                              int64_t ldg, int64_t ldu, int64_t ldh) {
+  constexpr int U = kPhFwdU;
+  const int64_t n8 = rows * cols8, chunk = 1024 * U;
+  for (int64_t base = (int64_t)blockIdx.x * chunk; base < n8; base += (int64_t)gridDim.x * chunk) {
+    u32x4 gv[U], uv[U];
+    int64_t r;
+    int c;
+    rc_of(base + threadIdx.x, cols8, r, c);
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const bool ok = r < rows;
+      gv[k] = ok ? __builtin_nontemporal_load(g + r * ldg + c) : u32x4{0, 0, 0, 0};
+      uv[k] = ok ? __builtin_nontemporal_load(u + r * ldu + c) : u32x4{0, 0, 0, 0};
+      rc_step(cols8, r, c);
+    }
+    rc_of(base + threadIdx.x, cols8, r, c);
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      if (r < rows) __builtin_nontemporal_store(swiglu_vec(gv[k], uv[k]), h + r * ldh + c);
+      rc_step(cols8, r, c);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
+__global__ __launch_bounds__(1024) void swiglu_bwd_rows_phased(const u32x4* __restrict__ dh, const u32x4* __restrict__ g,
+                                                              const u32x4* __restrict__ u, u32x4* __restrict__ dg,
+                                                              u32x4* __restrict__ du, int64_t rows, int cols8,
+                                                              int64_t lddh, int64_t ldg, int64_t ldu, int64_t lddg,
+                                                              int64_t lddu) {
+  constexpr int U = kPhBwdU;
+  const int64_t n8 = rows * cols8, chunk = 1024 * U;
+  for (int64_t base = (int64_t)blockIdx.x * chunk; base < n8; base += (int64_t)gridDim.x * chunk) {
+    u32x4 dv[U], gv[U], uv[U];
+    int64_t r;
+    int c;
+    rc_of(base + threadIdx.x, cols8, r, c);
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const bool ok = r < rows;
+      dv[k] = ok ? __builtin_nontemporal_load(dh + r * lddh + c) : u32x4{0, 0, 0, 0};
+      gv[k] = ok ? __builtin_nontemporal_load(g + r * ldg + c) : u32x4{0, 0, 0, 0};
+      uv[k] = ok ? __builtin_nontemporal_load(u + r * ldu + c) : u32x4{0, 0, 0, 0};
+      rc_step(cols8, r, c);
+    }
+    rc_of(base + threadIdx.x, cols8, r, c);
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      u32x4 og, ou;
+      swiglu_bwd_vec(dv[k], gv[k], uv[k], og, ou);
+      if (r < rows) {
+        __builtin_nontemporal_store(og, dg + r * lddg + c);
+        __builtin_nontemporal_store(ou, du + r * lddu + c);
+      }
+      rc_step(cols8, r, c);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
+
 // Row-strided SwiGLU for the fused gate/up GEMM (finetune/model_ops.py GateUpSwiGLUFn): gate and up
 // are the two column halves of one [rows, 2 I] GEMM output (row stride ld, 8-element vectors), the
 // backward writes dgate / dup into the two halves of one [rows, 2 I] buffer, which the fused dgrad
@@ -612,6 +748,19 @@ hipError_t norm_bwd_table(int nv, const void* dy, const void* x, const void* w, 
 
 bool a16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 bool a8(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7u) == 0; }
+// one 1024-thread workgroup per CU (x PRL_SWIGLU_PHASED_WG)
+#ifndef PRL_SWIGLU_PHASED_WG
+#define PRL_SWIGLU_PHASED_WG 1
+#endif
+static int phased_grid() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  return cus * PRL_SWIGLU_PHASED_WG;
+}
 int ew_grid(int64_t n8) {
   const int64_t g = (n8 + 255) / 256;
   return (int)(g < 4096 ? (g > 0 ? g : 1) : 4096);
@@ -706,6 +855,13 @@ int prl_swiglu_forward(const void* gate, const void* up, void* out, int64_t n, v
   if (n % 8 || !a16(gate) || !a16(up) || !a16(out)) return PRL_E_UNSUPPORTED;
   if (n == 0) return PRL_OK;
   const int64_t n8 = n / 8;
+  if (PRL_SWIGLU_PHASED) {
+    const int64_t chunks = (n8 + 1024 * kPhFwdU - 1) / (1024 * kPhFwdU);
+    const int grid = (int)(chunks < phased_grid() ? chunks : phased_grid());
+    hipLaunchKernelGGL(swiglu_fwd_phased, dim3(grid), dim3(1024), 0, static_cast<hipStream_t>(stream),
+                       (const u32x4*)gate, (const u32x4*)up, (u32x4*)out, n8);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(swiglu_fwd, dim3(ew_grid(n8)), dim3(256), 0, static_cast<hipStream_t>(stream),
                      (const u32x4*)gate, (const u32x4*)up, (u32x4*)out, n8);
   return (int)hipGetLastError();
@@ -717,6 +873,13 @@ int prl_swiglu_backward(const void* dout, const void* gate, const void* up, void
   if (n % 8 || !a16(dout) || !a16(gate) || !a16(up) || !a16(dgate) || !a16(dup)) return PRL_E_UNSUPPORTED;
   if (n == 0) return PRL_OK;
   const int64_t n8 = n / 8;
+  if (PRL_SWIGLU_PHASED) {
+    const int64_t chunks = (n8 + 1024 * kPhBwdU - 1) / (1024 * kPhBwdU);
+    const int grid = (int)(chunks < phased_grid() ? chunks : phased_grid());
+    hipLaunchKernelGGL(swiglu_bwd_phased, dim3(grid), dim3(1024), 0, static_cast<hipStream_t>(stream),
+                       (const u32x4*)dout, (const u32x4*)gate, (const u32x4*)up, (u32x4*)dgate, (u32x4*)dup, n8);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(swiglu_bwd, dim3(ew_grid(n8)), dim3(256), 0, static_cast<hipStream_t>(stream),
                      (const u32x4*)dout, (const u32x4*)gate, (const u32x4*)up, (u32x4*)dgate, (u32x4*)dup, n8);
   return (int)hipGetLastError();
@@ -732,6 +895,14 @@ int prl_swiglu_forward_rows(const void* gate, const void* up, void* out, int64_t
       cols / 8 > 0x7FFFFFFF)
     return PRL_E_UNSUPPORTED;
   if (rows == 0 || cols == 0) return PRL_OK;
+  if (PRL_SWIGLU_ROWS_PHASED) {
+    const int64_t chunks = (rows * (cols / 8) + 1024 * kPhFwdU - 1) / (1024 * kPhFwdU);
+    const int grid = (int)(chunks < phased_grid() ? chunks : phased_grid());
+    hipLaunchKernelGGL(swiglu_fwd_rows_phased, dim3(grid), dim3(1024), 0, static_cast<hipStream_t>(stream),
+                       (const u32x4*)gate, (const u32x4*)up, (u32x4*)out, rows, (int)(cols / 8), ld_gate / 8,
+                       ld_up / 8, ld_out / 8);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(swiglu_fwd_rows, dim3(rows_grid(rows)), dim3(256), 0, static_cast<hipStream_t>(stream),
                      (const u32x4*)gate, (const u32x4*)up, (u32x4*)out, rows, (int)(cols / 8), ld_gate / 8, ld_up / 8,
                      ld_out / 8);
@@ -748,6 +919,14 @@ int prl_swiglu_backward_rows(const void* dout, const void* gate, const void* up,
       !a16(gate) || !a16(up) || !a16(dgate) || !a16(dup) || cols / 8 > 0x7FFFFFFF)
     return PRL_E_UNSUPPORTED;
   if (rows == 0 || cols == 0) return PRL_OK;
+  if (PRL_SWIGLU_ROWS_PHASED) {
+    const int64_t chunks = (rows * (cols / 8) + 1024 * kPhBwdU - 1) / (1024 * kPhBwdU);
+    const int grid = (int)(chunks < phased_grid() ? chunks : phased_grid());
+    hipLaunchKernelGGL(swiglu_bwd_rows_phased, dim3(grid), dim3(1024), 0, static_cast<hipStream_t>(stream),
+                       (const u32x4*)dout, (const u32x4*)gate, (const u32x4*)up, (u32x4*)dgate, (u32x4*)dup, rows,
+                       (int)(cols / 8), ld_dout / 8, ld_gate / 8, ld_up / 8, ld_dgate / 8, ld_dup / 8);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(swiglu_bwd_rows, dim3(rows_grid(rows)), dim3(256), 0, static_cast<hipStream_t>(stream),
                      (const u32x4*)dout, (const u32x4*)gate, (const u32x4*)up, (u32x4*)dgate, (u32x4*)dup, rows,
                      (int)(cols / 8), ld_dout / 8, ld_gate / 8, ld_up / 8, ld_dgate / 8, ld_dup / 8);

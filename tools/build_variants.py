@@ -32,6 +32,9 @@ VARIANTS = {
     "norm_fwd2048": {"PRL_NORM_FWD_GRID": "2048"},
     "bf16_sw": {"PRL_HW_BF16": "0"},
     "unphased": {"PRL_PHASED": "0"},
+    "swiglu_gridstride": {"PRL_SWIGLU_PHASED": "0"},
+    "swiglu_phased_wg2": {"PRL_SWIGLU_PHASED": "1", "PRL_SWIGLU_PHASED_WG": "2"},
+    "swiglu_rows_phased": {"PRL_SWIGLU_ROWS_PHASED": "1"},
     "attn_2wg": {"PRL_ATTN_BWD_MINB": "2", "PRL_ATTN_KV_LDS": "2", "PRL_ATTN_INTERLEAVE": "0", "PRL_ATTN_BSTAGE": "32"},
     "attn_v_lds": {"PRL_ATTN_KV_LDS": "2"},
     "attn_bstage32": {"PRL_ATTN_INTERLEAVE": "0", "PRL_ATTN_BSTAGE": "32"},
