@@ -8,6 +8,7 @@
 //   sync<K>   phased, plus a grid-wide soft barrier every K rows so every CU reads (and then
 //             writes) at the same time; bounded spin (falls through after ~2^20 polls), so the
 //             grid always drains even if a workgroup is not resident
+//   *_inplace the same schedules writing each row back over itself (out == in)
 // One JSON line per variant (ms per 20 GB copy, GB/s counting read + write).
 //   hipcc -O3 --offload-arch=gfx950 tools/hbm/phased_copy.hip -o tools/hbm/phased_copy.bin
 #include <hip/hip_runtime.h>
@@ -134,5 +135,11 @@ int main(int argc, char** argv) {
     run(nm, [&] { rowcopy<2><<<G, THREADS>>>(I, O, nrows, ctr, K); });
   }
   run("overlap", [&] { rowcopy<0><<<G, THREADS>>>(I, O, nrows, ctr, 1); });
+  // in place (the row written back over the row read: the label-row lm_head's dlogits-over-logits)
+  u32x4* IO = (u32x4*)in;
+  run("phased_inplace", [&] { rowcopy<1><<<G, THREADS>>>(IO, IO, nrows, ctr, 1); });
+  run("overlap_inplace", [&] { rowcopy<0><<<G, THREADS>>>(IO, IO, nrows, ctr, 1); });
+  run("phased", [&] { rowcopy<1><<<G, THREADS>>>(I, O, nrows, ctr, 1); });
+  run("phased_inplace", [&] { rowcopy<1><<<G, THREADS>>>(IO, IO, nrows, ctr, 1); });
   return 0;
 }
