@@ -108,3 +108,29 @@ def test_split_heavy_key_blocks(bounds, heads, monkeypatch):
         err_one = float((x.float() - r).abs().max()) / scale
         assert err_split <= max(1e-2, 1.5 * err_one), (name, err_split, err_one)
     assert all(torch.equal(x, y) for x, y in zip(b, c))
+
+
+@pytest.mark.parametrize("heads", [(14, 2), (40, 8)])
+@pytest.mark.parametrize("bounds", [[0, 4096], [0, 3000, 3400, 3500], [0, 1, 700, 2900, 3100]])
+def test_reference_model_gqa_ratios(bounds, heads):
+    """The query / kv head counts of the other BASELINE models (C1 Qwen2.5-0.5B: 14 / 2, C5
+    Qwen2.5-32B: 40 / 8, a group of 5 — the XCD remap's and the split plan's non-power-of-two
+    case) through the HIP forward and the default (split) backward: within the bf16 error of the
+    fp32 per-sequence reference, and bitwise repeatable."""
+    from pipelinerl_amd.finetune.attention import PackedCausalAttention
+
+    q, k, v, do = _inputs(bounds, *heads, seed=7)
+    cu = torch.tensor(bounds, dtype=torch.int32, device=DEV)
+    mx = max(b - a for a, b in zip(bounds[:-1], bounds[1:]))
+
+    def ours(qq, kk, vv):
+        return PackedCausalAttention.apply(qq, kk, vv, cu, mx, bounds)
+
+    a = _run(ours, q, k, v, do)
+    ref = _fp32_ref(q, k, v, do, bounds)
+    for name, x, r in zip(("out", "dq", "dk", "dv"), a, ref):
+        scale = float(r.abs().max())
+        err = float((x.float() - r).abs().max()) / scale
+        assert err <= 1e-2, (name, err)
+    b = _run(ours, q, k, v, do)
+    assert all(torch.equal(x, y) for x, y in zip(a, b))
