@@ -51,13 +51,14 @@ def test_rmsnorm(H):
     assert ok, err
 
 
-def test_swiglu():
+@pytest.mark.parametrize("shape", [(5, 333, 1024), (1, 77, 4864), (1, 61, 27648)])  # toy, 0.5B, 32B widths
+def test_swiglu(shape):
     from pipelinerl_amd.finetune.model_ops import SwiGLUFn
 
     g0 = torch.Generator(device=DEV).manual_seed(1)
-    gate = (torch.randn((5, 333, 1024), generator=g0, device=DEV) * 3).to(torch.bfloat16)
-    up = torch.randn((5, 333, 1024), generator=g0, device=DEV).to(torch.bfloat16)
-    dh = torch.randn((5, 333, 1024), generator=g0, device=DEV).to(torch.bfloat16)
+    gate = (torch.randn(shape, generator=g0, device=DEV) * 3).to(torch.bfloat16)
+    up = torch.randn(shape, generator=g0, device=DEV).to(torch.bfloat16)
+    dh = torch.randn(shape, generator=g0, device=DEV).to(torch.bfloat16)
     ga, ua = gate.clone().requires_grad_(), up.clone().requires_grad_()
     ha = torch.nn.functional.silu(ga) * ua
     ha.backward(dh)
@@ -70,12 +71,14 @@ def test_swiglu():
     assert ok, err
 
 
-def test_rope_matches_hf():
+@pytest.mark.parametrize("heads", [(12, 2), (14, 2), (28, 4), (40, 8)])  # 1.5B, 0.5B, 7B, 32B
+def test_rope_matches_hf(heads):
     from transformers.models.qwen2 import modeling_qwen2 as mq
 
     from pipelinerl_amd.finetune.model_ops import RopeFn
 
-    B, T, hq, hkv, D = 2, 97, 12, 2, 128
+    B, T, D = 2, 97, 128
+    hq, hkv = heads
     g = torch.Generator(device=DEV).manual_seed(3)
     qp = torch.randn((B, T, hq * D), generator=g, device=DEV).to(torch.bfloat16)
     kp = torch.randn((B, T, hkv * D), generator=g, device=DEV).to(torch.bfloat16)
