@@ -205,7 +205,10 @@ def test_shared_input_linear(bias):
                 assert float((ba[i].grad.float() - ref).abs().max()) <= 1e-2 * float(ref.abs().max())
 
 
-def test_patched_qwen2_matches_eager(tmp_path):
+# toy, then two decoder layers of the 7B (C3 / C4) and 32B (C5) shapes: head dim 128 (the HIP
+# attention), GQA groups of 7 and 5, the wide MLPs
+@pytest.mark.parametrize("shape", [(256, 512, 4, 2), (3584, 18944, 28, 4), (5120, 27648, 40, 8)])
+def test_patched_qwen2_matches_eager(tmp_path, shape):
     from loop_helpers import tiny_model_dir
     from transformers import AutoConfig, AutoModelForCausalLM
 
@@ -213,7 +216,8 @@ def test_patched_qwen2_matches_eager(tmp_path):
     from pipelinerl_amd.finetune.model_ops import patch_model
 
     cfg = AutoConfig.from_pretrained(tiny_model_dir(tmp_path, vocab=512))
-    cfg.hidden_size, cfg.intermediate_size, cfg.num_attention_heads, cfg.num_key_value_heads = 256, 512, 4, 2
+    cfg.hidden_size, cfg.intermediate_size, cfg.num_attention_heads, cfg.num_key_value_heads = shape
+    cfg.num_hidden_layers = 2
     torch.manual_seed(0)
     eager = AutoModelForCausalLM.from_config(cfg, dtype=torch.bfloat16, attn_implementation=register()).to(DEV)
     fused = copy.deepcopy(eager)
