@@ -19,6 +19,25 @@ from .types import PipelineBatchEncoding
 from .utils import create_sentinel_batch
 
 
+def filter_zero_advantage_groups(dataset: list[dict[str, Any]], epsilon: float = 1e-6) -> tuple[list[dict[str, Any]], int]:
+    """Drop every group whose rollouts all have |advantage| <= epsilon on every token
+    (pipelinerl/preprocess.py:287-324; applied to each populated chunk before packing when
+    ``rl.filter_zero_advantage_groups`` is set, :509-513).  Kept groups come out in order of
+    their first appearance, each group's entries in input order; returns (kept, number dropped).
+    A NaN advantage counts as zero (``abs(nan) > epsilon`` is false), as in the reference."""
+    groups: dict[Any, list[dict[str, Any]]] = {}
+    for entry in dataset:
+        groups.setdefault(entry["group_id"], []).append(entry)
+    kept: list[dict[str, Any]] = []
+    dropped = 0
+    for entries in groups.values():
+        if any(abs(a) > epsilon for e in entries for a in e["advantages"]):
+            kept.extend(entries)
+        else:
+            dropped += len(entries)
+    return kept, dropped
+
+
 class MicroBatchPacker:
     def __init__(self, num_trainers: int, seq_length: int, samples_per_lead_per_step: int, tokenizer,
                  seq_parallel: int = 1):

@@ -79,14 +79,20 @@ def rollouts(config: str, n: int, seed: int = 1234, max_completion: int | None =
     return populate_rl_data(data, EOS, RLConfig(divide_advantage_by_std=False))
 
 
-def pack(data: list[dict], seq_length: int, samples_per_step: int, num_trainers: int = 1) -> list[tuple[int, object]]:
+def pack(data: list[dict], seq_length: int, samples_per_step: int, num_trainers: int = 1,
+         filter_zero_advantage_groups: bool = False) -> list[tuple[int, object]]:
     """(trainer_id, PipelineBatchEncoding) writes of the preprocessor's packer (quota + sentinel
-    protocol, preprocess.py:557-626) for ``data``."""
-    from .finetune.packing import MicroBatchPacker
+    protocol, preprocess.py:557-626) for ``data``; with ``filter_zero_advantage_groups`` the
+    chunk first loses its all-zero-advantage groups, as rl.filter_zero_advantage_groups does
+    (preprocess.py:509-513)."""
+    from .finetune import packing
 
-    packer = MicroBatchPacker(num_trainers, seq_length, samples_per_step // num_trainers,
-                              types.SimpleNamespace(eos_token_id=EOS))
-    return packer.feed(copy.deepcopy(data))
+    data = copy.deepcopy(data)
+    if filter_zero_advantage_groups:
+        data, _ = packing.filter_zero_advantage_groups(data)
+    packer = packing.MicroBatchPacker(num_trainers, seq_length, samples_per_step // num_trainers,
+                                      types.SimpleNamespace(eos_token_id=EOS))
+    return packer.feed(data)
 
 
 def micro_batches(config: str, count: int, seed: int = 1234, seq_length: int | None = None) -> list:
