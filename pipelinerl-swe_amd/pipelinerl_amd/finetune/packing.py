@@ -64,9 +64,12 @@ class MicroBatchPacker:
 
     def feed(self, entries: Iterable[dict[str, Any]]) -> list[tuple[int, PipelineBatchEncoding]]:
         """Queue processed samples; return the (trainer_id, micro_batch) writes now possible."""
+        appended = False
         for e in entries:
             self.queue.append(e)
-            self.max_model_version = max(self.max_model_version, int(e.get("model_version", 0)))
+            appended = True
+        if appended:  # preprocess.py:542-546: the max over the entries still queued, after the appends
+            self.max_model_version = max(int(e.get("model_version", 0)) for e in self.queue)
         out: list[tuple[int, PipelineBatchEncoding]] = []
         while self.queue:  # the reference's outer loop re-enters the write loop after each step
             out.extend(self._write_step())
