@@ -444,9 +444,10 @@ def rl_finetuning_worker(args, ctx: Dist, model, optimizer, lr_scheduler, grads:
             md.update(step_metrics(metrics, lag, batch_queue, tokens_processed, passes_took, mb_sizes, ctx.world,
                                    samples_per_step, step_took))
             gathered = defaultdict(list)
-            for per_rank in ctx.gather_object(dict(rl_metrics)):
+            for per_rank in ctx.gather_object(dict(rl_metrics)):  # gather_rl_metrics, finetune_loop.py:62-89
                 for k, vs in per_rank.items():
-                    gathered[k].extend(v for v in vs if np.isfinite(v))
+                    if vs:  # an empty list adds no key; non-finite values are dropped
+                        gathered[k].extend(v for v in vs if np.isfinite(v))
             avg = aggregate_rl_stats(gathered, samples_per_step)
             if avg.get("rl/ratio_new_old_squared_sum") and avg.get("rl/num_output_tokens_sum"):
                 avg["rl/ess"] = (avg["rl/ratio_new_old_sum"] ** 2 / avg["rl/ratio_new_old_squared_sum"]
