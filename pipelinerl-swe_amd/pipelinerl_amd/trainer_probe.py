@@ -128,6 +128,8 @@ class TrainerStep:
         from .finetune.rl import rl_step
 
         self.native_step = step_fn is None or step_fn is rl_step
+        self._tail_events: list = []
+        self._tail_cpu: list[float] = []
         self.step_fn = step_fn if step_fn is not None else rl_step
         self.opt = get_optimizer("adamw_torch", self.model, 1e-6, 0.01)
         self.grads = GradBuckets(list(self.model.parameters()), group=group) \
@@ -169,6 +171,12 @@ class TrainerStep:
                 loss.backward()
         if self.grads is not None:
             self.grads.finish()
+        on_gpu = self.device.type == "cuda"
+        if on_gpu:  # the optimizer tail (clip, AdamW, zero) on the device, end of backward -> done
+            t0 = torch.cuda.Event(enable_timing=True)
+            t0.record()
+        else:
+            c0 = time.perf_counter()
         clip_grad_norm(self.model.parameters(), 0.3, self.opt)
         if wum is not None:
             wum.before_optimizer_step()  # the previous snapshot is read before params change
@@ -177,6 +185,12 @@ class TrainerStep:
             self.grads.zero_()
         else:
             self.opt.zero_grad(set_to_none=True)
+        if on_gpu:
+            t1 = torch.cuda.Event(enable_timing=True)
+            t1.record()
+            self._tail_events.append((t0, t1))
+        else:
+            self._tail_cpu.append(time.perf_counter() - c0)
         if wum is not None:
             wum.send_weight_update(version)  # returns at once: overlapped with the next step
 
@@ -187,6 +201,7 @@ class TrainerStep:
             v += 1
             self.step(wum, v)
         _sync(self.device)
+        self._tail_events, self._tail_cpu = [], []
         if self.world > 1:
             dist.barrier(self.group)
         t0 = time.perf_counter()
@@ -200,6 +215,19 @@ class TrainerStep:
         if self.world > 1:
             dist.all_reduce(dt, op=dist.ReduceOp.MAX, group=self.group)
         return float(dt) / steps
+
+    def optimizer_tail(self) -> float:
+        """Seconds of the last ``timed`` run's optimizer tail (clip_grad_norm, AdamW, zeroing) per
+        step, mean over its steps, max over the group's ranks."""
+        if self._tail_events:
+            _sync(self.device)
+            t = sum(a.elapsed_time(b) for a, b in self._tail_events) / len(self._tail_events) / 1e3
+        else:
+            t = sum(self._tail_cpu) / max(1, len(self._tail_cpu))
+        dt = torch.tensor([t], dtype=torch.float64, device=self.device)
+        if self.world > 1:
+            dist.all_reduce(dt, op=dist.ReduceOp.MAX, group=self.group)
+        return float(dt)
 
     def allreduce_alone(self, iters: int = 3) -> float:
         """Seconds of the bucketed gradient all-reduce over the model's real buckets with no
@@ -282,7 +310,8 @@ def dp_step_probe(config: str = "c3", micro_batches: int = 4, steps: int = 2, wa
     (DP − local) / all-reduce alone.  The real C3 step trains ``samples_per_step`` (4096) samples,
     i.e. ~``samples_per_step / world / samples_per_micro_batch`` micro-batches per rank for ONE
     all-reduce: ``extrapolated_tokens_per_s_per_gpu`` prices that step as (its micro-batches x the
-    measured per-micro-batch time) + the exposed all-reduce + the optimizer tail.
+    measured per-micro-batch time, the optimizer tail taken out) + the exposed all-reduce + one
+    optimizer tail (clip + AdamW + zeroing, timed with device events: ``optimizer_tail_ms``).
     Collective over the default group (every rank calls it).  ``batches`` / ``model`` /
     ``step_fn`` are injectable (gloo tests on CPU)."""
     from . import workloads
@@ -302,6 +331,7 @@ def dp_step_probe(config: str = "c3", micro_batches: int = 4, steps: int = 2, wa
     ts = TrainerStep(spec.model, device=device, fused_head=True, kl_coef=spec.kl_coef, layers=layers,
                      batches=batches, samples_per_step=samples_per_step, local=True, model=model, step_fn=step_fn)
     t_local = ts.timed(steps, warmup)
+    t_tail = ts.optimizer_tail()
     t_dp, t_ar = t_local, 0.0
     if world > 1:
         from .finetune.grad_sync import GradBuckets
@@ -324,11 +354,13 @@ def dp_step_probe(config: str = "c3", micro_batches: int = 4, steps: int = 2, wa
         stats = stats.clone()
     tok_all, samp_all, t_local_max = (float(x) for x in stats.cpu())
     exposed = max(0.0, t_dp - t_local_max)
-    # the real step: samples_per_step samples over all ranks, one all-reduce
+    # the real step: samples_per_step samples over all ranks, one all-reduce, ONE optimizer tail
+    # (finetune_loop.py:700-719 runs clip + AdamW once per samples_per_step, not per micro-batch)
     mb_real = samples_per_step / (samp_all / (micro_batches * world))
-    per_mb = t_local_max / micro_batches
+    t_tail = min(t_tail, t_local_max)
+    per_mb = (t_local_max - t_tail) / micro_batches
     tok_per_mb = tok_all / (micro_batches * world)
-    t_real = (mb_real / world) * per_mb + exposed
+    t_real = (mb_real / world) * per_mb + t_tail + exposed
     return {"config": f"C3: Qwen2.5-{spec.model} shapes{f' ({layers} layers)' if layers else ''} (random init, bf16), "
                       f"math rollouts packed at {spec.seq_length}, label-row lm_head",
             "micro_batches_per_rank": micro_batches, "tokens_per_rank_step": round(tok_all / world, 1),
@@ -336,11 +368,13 @@ def dp_step_probe(config: str = "c3", micro_batches: int = 4, steps: int = 2, wa
             "ms_per_step_local": round(t_local_max * 1e3, 2), "ms_per_step_dp": round(t_dp * 1e3, 2),
             "allreduce_bytes": nbytes, "allreduce_alone_ms": round(t_ar * 1e3, 2),
             "allreduce_exposed_ms": round(exposed * 1e3, 2),
+            "optimizer_tail_ms": round(t_tail * 1e3, 2),
             "overlap": round(1.0 - min(1.0, exposed / t_ar), 4) if t_ar > 0 else None,
             "tokens_per_s_per_gpu": round(tok_all / world / t_dp, 1),
             "tokens_per_s": round(tok_all / t_dp, 1),
             "local_tokens_per_s_per_gpu": round(tok_all / world / t_local_max, 1),
             "extrapolated": {"samples_per_step": samples_per_step, "micro_batches_per_rank": round(mb_real / world, 1),
+                             "ms_per_micro_batch": round(per_mb * 1e3, 2),
                              "tokens_per_s_per_gpu": round(tok_per_mb * (mb_real / world) / t_real, 1),
                              "allreduce_share": round(exposed / t_real, 5)},
             "peak_mem_gb": round(peak, 2), "steps": steps, "warmup": warmup, "world": world}
