@@ -12,6 +12,7 @@ import os
 
 import numpy as np
 import torch
+from torch.autograd.graph import increment_version
 
 NO_DECAY = ("bias", "LayerNorm.weight")
 
@@ -108,6 +109,12 @@ class PrlAdamW(torch.optim.AdamW):
                                              sc.data_ptr() if sc is not None else None,
                                              torch.cuda.current_stream(params[0].device).cuda_stream),
                           "prl_adamw_step")
+            # the kernel wrote p, m, v through raw pointers: move their version counters as torch's
+            # in-place step would, so caches keyed on them (model_ops._fused_weight: the fused
+            # gate/up and q/k/v weights) see the update
+            increment_version(params)
+            increment_version(ms)
+            increment_version(vs)
         return loss
 
 

@@ -80,6 +80,34 @@ def test_fused_gate_up_matches_separate(monkeypatch):
     assert torch.equal(model_ops._fused_weight(holder, (wg, wu)), torch.cat([wg.detach(), wu.detach()]))
 
 
+def test_fused_weight_cache_follows_native_adamw():
+    """The native AdamW step (csrc/adamw.hip through raw pointers) moves the parameters' version
+    counters, so the cached cat(Wg, Wu) of the fused gate/up projection is rebuilt after every
+    optimizer step: the next forward uses the updated weights (== the separate form)."""
+    from pipelinerl_amd.finetune import model_ops
+    from pipelinerl_amd.finetune.optim import PrlAdamW, clip_grad_norm
+
+    g = torch.Generator(device=DEV).manual_seed(9)
+    T, H, I = 257, 256, 704
+    holder = torch.nn.Module()
+    wg = torch.nn.Parameter((torch.randn((I, H), generator=g, device=DEV) * 0.05).to(torch.bfloat16))
+    wu = torch.nn.Parameter((torch.randn((I, H), generator=g, device=DEV) * 0.05).to(torch.bfloat16))
+    opt = PrlAdamW([wg, wu], lr=1e-2, weight_decay=0.01)
+    for step in range(3):
+        x = torch.randn((1, T, H), generator=g, device=DEV).to(torch.bfloat16)
+        h = model_ops.GateUpSwiGLUFn.apply(x, wg, wu, holder)
+        with torch.no_grad():  # a fresh cache holds the current weights: the same bits
+            fresh = model_ops.GateUpSwiGLUFn.apply(x, wg, wu, torch.nn.Module())
+        assert torch.equal(h, fresh), step
+        h.float().pow(2).mean().backward()
+        before = (wg._version, wu._version)
+        clip_grad_norm([wg, wu], 0.3, opt)
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        assert wg._version > before[0] and wu._version > before[1]
+    assert torch.equal(model_ops._fused_weight(holder, (wg, wu)), torch.cat([wg.detach(), wu.detach()]))
+
+
 def test_fused_qkv_matches_separate():
     """QKVFn (one GEMM over cat(Wq, Wk, Wv), concatenated bias in the epilogue) == the separate
     SharedInputLinearFn over three micro-batches: q / k / v, dx, the weight and bias gradients to
