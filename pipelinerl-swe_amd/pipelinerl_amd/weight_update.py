@@ -137,6 +137,10 @@ class HipFlatPacker:
         P, D, N, O = self._tables(tensors, offsets)
         st = torch.cuda.current_stream(flat.device).cuda_stream
         _native.check(lib.prl_unflatten_bf16(flat.data_ptr(), P, D, N, O, len(tensors), st), "prl_unflatten_bf16")
+        # written through raw pointers: move the version counters as an in-place copy_ would
+        from torch.autograd.graph import increment_version
+
+        increment_version(tensors)
 
 
 def parameters_info(named: list[tuple[str, torch.Tensor]]) -> list[ParameterInfo]:
