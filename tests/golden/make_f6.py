@@ -13,7 +13,8 @@ in a namespace holding the loop's state, initialised as preprocess.py:430-449 do
 published samples) and carried from chunk to chunk.  Its collaborators are the reference's own
 ``collate_packed`` / ``create_sentinel_batch``; ``write_micro_batch_slices`` records the
 (lead trainer, micro-batch) it is given; ``max_model_version`` is recomputed after each chunk
-is appended over the entries still queued (:542-546).  After each chunk the loop is re-entered
+is appended over the entries still queued (:542-546).  For seq_parallel > 1 each write's
+slices (the reference's ``make_slices``, as ``write_micro_batch_slices`` sends them) are kept too.  After each chunk the loop is re-entered
 while entries remain (the outer loop does, the trainer keeping up).
 """
 
@@ -133,9 +134,13 @@ def main():
             for i, e in enumerate(data):  # carry the max over what is still queued, not the max seen
                 e["model_version"] = 7 if i < 6 else 3
         writes = run_reference(json.loads(json.dumps(data)), chunks, nt, sp, per_lead, seq_len)
+        # what write_micro_batch_slices sends each trainer of a lead's group (preprocess.py:327-338):
+        # the reference's own PipelineBatchEncoding.make_slices (types.py:144-180)
+        slices = [[encode(t + i, sl) for i, sl in enumerate(b.make_slices(sp))] if sp > 1 else []
+                  for t, b in writes]
         cases.append({"name": name, "num_trainers": nt, "seq_parallel": sp, "samples_per_lead_per_step": per_lead,
                       "seq_length": seq_len, "chunks": chunks, "input": data,
-                      "writes": [encode(t, b) for t, b in writes]})
+                      "writes": [encode(t, b) for t, b in writes], "slices": slices})
         print(name, len(writes), "writes,", sum(w[1].sentinel for w in writes), "sentinels")
     (HERE / "f6_packing.json").write_text(json.dumps({"source": "pipelinerl/preprocess.py:557-613", "eos": EOS,
                                                       "cases": cases}))

@@ -44,3 +44,9 @@ def test_packer_matches_reference_write_loop(case):
         assert set(g) == set(w), (i, set(g) ^ set(w))
         for k in w:
             assert g[k] == w[k], (i, k)
+    sp = case["seq_parallel"]
+    for i, ((t, b), want_slices) in enumerate(zip(writes, case["slices"])):  # types.py:144-180
+        got_slices = [_encode(t + j, s) for j, s in enumerate(b.make_slices(sp))] if sp > 1 else []
+        assert len(got_slices) == len(want_slices), i
+        for j, (g, w) in enumerate(zip(got_slices, want_slices)):
+            assert set(g) == set(w) and all(g[k] == w[k] for k in w), (i, j, [k for k in w if g.get(k) != w[k]])
