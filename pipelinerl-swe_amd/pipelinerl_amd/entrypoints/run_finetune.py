@@ -1,12 +1,20 @@
 """Trainer entrypoint (drop-in for pipelinerl/entrypoints/run_finetune.py).
 
-    torchrun --nproc-per-node N -m pipelinerl_amd.entrypoints.run_finetune \
-        --config-dir exp/conf --config-name exp_config \
+The reference launcher's own command line works with only the script path changed
+(launch.py:235-315 builds it; any accelerate config, ``--num_processes N``):
+
+    python -m accelerate.commands.launch --config_file conf/accelerate/base_mp.yaml \
+        --rdzv_backend c10d --num_processes N \
+        pipelinerl-swe_amd/pipelinerl_amd/entrypoints/run_finetune.py \
+        --config-dir exp/conf --config-name exp_config output_dir=exp hydra.run.dir=exp/finetune \
         +me.weight_update_group_init_method=tcp://HOST:9000 +me.weight_update_group_world_size=K \
         +me.llm_urls=http://a:8080+http://b:8080
 
-(accelerate's / DeepSpeed's ``--local_rank=N`` argument is accepted and ignored, as in the
-reference.)  Any exception kills the process (non-zero exit), so the launcher's watchdog sees it.
+It also runs as a module (``torchrun --nproc-per-node N -m pipelinerl_amd.entrypoints.run_finetune
+…``).  accelerate's / DeepSpeed's ``--local_rank=N`` argument is accepted and dropped, as the
+reference does (run_finetune.py:15-20); ranks come from the RANK / WORLD_SIZE / LOCAL_RANK /
+MASTER_* environment the launcher sets.  Any exception kills the process (non-zero exit), so the
+launcher's watchdog sees it.
 """
 
 from __future__ import annotations
@@ -14,9 +22,13 @@ from __future__ import annotations
 import argparse
 import logging
 import sys
+from pathlib import Path
 
-from ..config import load_config
-from ..finetune_loop import run_finetuning_loop
+if __package__ in (None, ""):  # run by path (the reference launcher's form): make the package importable
+    sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
+
+from pipelinerl_amd.config import load_config  # noqa: E402
+from pipelinerl_amd.finetune_loop import run_finetuning_loop  # noqa: E402
 
 
 def main(argv: list[str] | None = None) -> int:

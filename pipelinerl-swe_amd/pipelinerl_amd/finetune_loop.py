@@ -234,7 +234,8 @@ def run_finetuning_loop(cfg, step_fn: Callable = rl_step, model=None, tokenizer=
     ctx.barrier()
 
     metrics = TrainingMetrics()
-    if (state_dir / "training_state.pt").exists():
+    if state_dir.exists():  # finetune_loop.py:416-418: resume whenever the directory exists
+        check_training_state_layout(state_dir)
         metrics = load_training_state(state_dir, model, optimizer, lr_scheduler, metrics)
         metrics.lr = optimizer.param_groups[0]["lr"]
     if ctx.is_main:
@@ -274,6 +275,28 @@ def run_finetuning_loop(cfg, step_fn: Callable = rl_step, model=None, tokenizer=
                 actor_group.close()
             else:
                 dist.destroy_process_group(actor_group)
+
+
+class TrainingStateError(RuntimeError):
+    """A training_state/ directory this trainer cannot resume from."""
+
+
+def check_training_state_layout(state_dir: Path) -> None:
+    """The reference resumes whenever ``training_state/`` exists (finetune_loop.py:416-418), in one
+    of two layouts (finetune/checkpoints.py:169-180): Accelerate's ``training_state.pt`` (this
+    trainer's own, loaded) or DeepSpeed's ``model.save_checkpoint(dir, tag="deepspeed")`` (a
+    ``deepspeed/`` tag directory + ``latest``, the reference's default backend).  The DeepSpeed
+    layout holds ZeRO-partitioned model and optimizer shards this trainer does not read: starting
+    over at samples=0 would silently restart the weight versions the actors see, so raise."""
+    if (state_dir / "training_state.pt").exists():
+        return
+    if (state_dir / "deepspeed").is_dir() or (state_dir / "latest").exists():
+        raise TrainingStateError(
+            f"{state_dir} holds a DeepSpeed checkpoint (tag 'deepspeed', finetune/checkpoints.py:169-180); this "
+            "trainer resumes only from training_state.pt: convert it (DeepSpeed's zero_to_fp32 for the weights into "
+            "finetune/current) or start from a fresh output_dir")
+    raise TrainingStateError(f"{state_dir} exists but holds no training_state.pt (the reference would fail to "
+                             "load it too, finetune/checkpoints.py:229)")
 
 
 def grad_scale_convention(cfg) -> str:

@@ -264,3 +264,34 @@ def test_prl_adamw_cpu_falls_back_to_torch():
     for p, q in zip(pa, pb):
         assert torch.equal(p, q)
     assert isinstance(clip_grad_norm(pa, 1.0, ref), torch.Tensor)  # any other optimizer: torch's clip
+
+
+def test_resume_refuses_a_deepspeed_training_state(tmp_path, monkeypatch):
+    """The reference resumes whenever finetune/training_state/ exists (finetune_loop.py:416-418),
+    including DeepSpeed's tag layout (finetune/checkpoints.py:169-180: <dir>/deepspeed/ + latest).
+    This trainer cannot read ZeRO shards, so it raises instead of restarting at samples=0."""
+    sys.path[:0] = [str(ROOT / "tests")]
+    from cpu_rl_step import cpu_rl_step
+    from loop_helpers import loop_cfg
+    from pipelinerl_amd.finetune_loop import TrainingStateError, check_training_state_layout, run_finetuning_loop
+    from pipelinerl_amd.streams import reset_streams_backend
+
+    exp = tmp_path / "ds"
+    exp.mkdir()
+    per_step, _ = _setup(exp, 1)
+    state = exp / "finetune" / "training_state"
+    (state / "deepspeed").mkdir(parents=True)
+    (state / "latest").write_text("deepspeed")
+    for k in ("RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    reset_streams_backend()
+    cfg = loop_cfg(exp, exp / "tiny_qwen2", 1, per_step, 1, dist_backend=None)
+    with pytest.raises(TrainingStateError, match="DeepSpeed"):
+        run_finetuning_loop(cfg, step_fn=cpu_rl_step)
+    # an empty training_state/ fails too (the reference's torch.load of training_state.pt would)
+    empty = tmp_path / "empty_state"
+    empty.mkdir()
+    with pytest.raises(TrainingStateError, match="no training_state.pt"):
+        check_training_state_layout(empty)
+    (empty / "training_state.pt").write_bytes(b"")
+    check_training_state_layout(empty)  # the layout this trainer writes: accepted
