@@ -136,7 +136,7 @@ def _rows_parallel(fn, n_rows: int, chunk: int, threads: int):
 def rl_step_oracle(logits: np.ndarray, batch: dict, config: dict, current_step: int,
                    max_step: int, values: np.ndarray | None = None, grad_out: float = 1.0,
                    compute_grad: bool = True, dtype=np.float64, threads: int = 1,
-                   row_chunk: int = 64) -> dict[str, Any]:
+                   row_chunk: int = 64, grad_rows: np.ndarray | None = None) -> dict[str, Any]:
     """Restatement of rl_step (rl/__init__.py:130-377) on fixed logits.
 
     ``logits``: [B, L, V] (any float dtype, e.g. float32 or bf16 values held in float32).
@@ -145,7 +145,9 @@ def rl_step_oracle(logits: np.ndarray, batch: dict, config: dict, current_step: 
     ref_logprobs, old_logprobs, group_tokens, num_labels, overflow, is_packed.
     ``values``: optional [B, L] value-head output (value_model.py:50-52).
     Returns loss, stats, new_logprobs/entropy [B, L-1], and (optionally) dlogits [B, L, V]
-    and dvalues [B, L] for upstream gradient ``grad_out``.
+    and dvalues [B, L] for upstream gradient ``grad_out``.  ``grad_rows``: flat loss rows
+    q = b*(L-1)+t; when given, only those rows' gradients are formed (``dlogits_rows`` [len, V],
+    for full-size checks where [B, L, V] in float64 would not fit).
     Raises AssertionError / ValueError exactly where the reference does.
     """
     cfg = dict(RL_DEFAULTS)
@@ -320,6 +322,11 @@ def rl_step_oracle(logits: np.ndarray, batch: dict, config: dict, current_step: 
             return row_grad(flat_logits[a:b], flat_tgt[a:b], flat_lse[a:b], flat_ent[a:b],
                             flat_glp[a:b], flat_gh[a:b], temperature, dtype)
 
+        if grad_rows is not None:
+            q = np.asarray(grad_rows, dtype=np.int64)
+            out["dlogits_rows"] = row_grad(flat_logits[q], flat_tgt[q], flat_lse[q], flat_ent[q], flat_glp[q],
+                                           flat_gh[q], temperature, dtype)
+            return out
         gparts = _rows_parallel(_grad, R, row_chunk, threads)
         dlogits = np.zeros((B, L, V), dtype=dtype)
         dlogits[:, :-1, :] = np.concatenate(gparts).reshape(B, L - 1, V)

@@ -29,6 +29,15 @@ _ITEMS: dict[tuple, tuple] = {}
 BLOCK = 128  # keys / queries per workgroup of the HIP backward (csrc/attn_bwd.hip)
 
 
+def _to_device(rows: list, width: int, device) -> torch.Tensor:
+    """int32 [n, width] device copy of host rows without a host sync: staged in pinned memory, the
+    copy queued non-blocking (torch's pinned allocator keeps the staging buffer until it is done)."""
+    t = torch.tensor(rows if rows else [(0,) * width], dtype=torch.int32)
+    if torch.device(device).type != "cuda":
+        return t
+    return t.pin_memory().to(device, non_blocking=True)
+
+
 def _items(bounds: list[int], device) -> tuple:
     """(kv_items, q_items, n) int32 [n, 3] device tensors: (seq_start, seq_end, block_start) per
     128-row block of every sequence, heaviest first: key blocks by the causal query rows after
@@ -40,8 +49,7 @@ def _items(bounds: list[int], device) -> tuple:
         rows = [(a, b, x) for a, b in zip(bounds[:-1], bounds[1:]) for x in range(a, b, BLOCK)]
         kv = sorted(rows, key=lambda r: -(r[1] - r[2]))
         qb = sorted(rows, key=lambda r: -(min(r[2] + BLOCK, r[1]) - r[0]))
-        mk = lambda rr: torch.tensor(rr if rr else [(0, 0, 0)], dtype=torch.int32).to(device)  # noqa: E731
-        hit = (mk(kv), mk(qb), len(rows))
+        hit = (_to_device(kv, 3, device), _to_device(qb, 3, device), len(rows))
         if len(_ITEMS) > 64:
             _ITEMS.clear()
         _ITEMS[key] = hit
@@ -97,8 +105,8 @@ def _split_items(bounds: list[int], heads: int, kv_heads: int, device) -> tuple:
         cus = torch.cuda.get_device_properties(device).multi_processor_count
         kv_rows, units, groups, slots = split_plan(bounds, heads, kv_heads, cus)
         kv_rows = sorted(kv_rows, key=lambda r: -(r[1] - r[2]))
-        mk = lambda rr, w: torch.tensor(rr if rr else [(0,) * w], dtype=torch.int32).to(device)  # noqa: E731
-        hit = (mk(kv_rows, 3), len(kv_rows), mk(units, 7), len(units), mk(groups, 5), len(groups), slots)
+        hit = (_to_device(kv_rows, 3, device), len(kv_rows), _to_device(units, 7, device), len(units),
+               _to_device(groups, 5, device), len(groups), slots)
         if len(_SPLITS) > 64:
             _SPLITS.clear()
         _SPLITS[key] = hit
@@ -118,6 +126,9 @@ class PackedCausalAttention(torch.autograd.Function):
         T, H, D = q.shape
         ctx.bounds = bounds
         ctx.hip_fwd = os.environ.get("PRL_ATTN_FWD", "hip") == "hip"
+        ctx.split = os.environ.get("PRL_ATTN_SPLIT", "1") != "0"
+        if ctx.split:  # the backward's split plan, built here (cached per packing) so the backward queues only kernels
+            _split_items(bounds, H, k.shape[1], q.device)
         if ctx.hip_fwd:  # HIP forward: writes the backward's base-2 log-sum-exp [H, T] directly
             _, q_items, n = _items(bounds, q.device)
             out = torch.empty_like(q)
@@ -157,7 +168,7 @@ class PackedCausalAttention(torch.autograd.Function):
                                                       T, H, D, st), "prl_attn_bwd_preprocess")
         kv_items, q_items, n = _items(ctx.bounds, q.device)
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
-        if os.environ.get("PRL_ATTN_SPLIT", "1") != "0":  # heavy key blocks split over query heads
+        if ctx.split:  # heavy key blocks split over query heads
             kv_s, n_kv, units, n_units, groups, n_groups, slots = _split_items(ctx.bounds, H, k.shape[1], q.device)
             parts = torch.empty((max(slots, 1), 2, BLOCK, D), dtype=torch.float32, device=q.device)
             _native.check(lib.prl_attn_bwd_split(
@@ -263,7 +274,7 @@ def packed_kwargs(batch, device) -> dict:
     else:
         bounds = [int(x) for x in sb.cpu().tolist()]
     lens = [b - a for a, b in zip(bounds[:-1], bounds[1:])]
-    cu = torch.tensor(bounds, dtype=torch.int32).to(device, non_blocking=True)
+    cu = _to_device(bounds, 1, device).reshape(-1)
     mx = max(lens) if lens else 0
     return {"cu_seq_lens_q": cu, "cu_seq_lens_k": cu, "max_length_q": mx, "max_length_k": mx,
             "cu_seq_lens_host": bounds}

@@ -236,10 +236,21 @@ def disable_fused_projections() -> None:
     _FUSED_GATE_UP = _FUSED_QKV = False
 
 
+# Bumped by every writer the build knows of that changes weights in place (PrlAdamW.step,
+# HipFlatPacker.unflatten, load_weights_): a second key of the fused-weight caches beside the
+# version counters, which a write through ``p.data`` or a raw pointer does not move.
+_WEIGHT_EPOCH = [0]
+
+
+def weights_written() -> None:
+    """Invalidate every fused-weight cache (call after writing parameters outside autograd)."""
+    _WEIGHT_EPOCH[0] += 1
+
+
 def _fused_weight(holder, ws, slot: str = "_prl_fused_w") -> torch.Tensor:
     """cat(ws) cached on the module ``holder`` (so it lives and dies with the model), rebuilt when
-    a member's version counter or storage changes."""
-    ver = tuple(w._version for w in ws) + tuple(w.data_ptr() for w in ws)
+    a member's version counter or storage changes, or when weights_written() was called."""
+    ver = (_WEIGHT_EPOCH[0],) + tuple(w._version for w in ws) + tuple(w.data_ptr() for w in ws)
     hit = holder.__dict__.get(slot)
     if hit is not None and hit[0] == ver:
         return hit[1]
@@ -272,7 +283,7 @@ def _wgrad_group(dy, x, params):
             gemm.linear_wgrad(dy, x, out=G, accumulate=True)
             return [None] * len(params)
     dW = gemm.linear_wgrad(dy, x)
-    if (_FUSE_GRAD_ACCUM and all(isinstance(p, torch.nn.Parameter) and p.grad is None
+    if (_FUSE_GRAD_ACCUM and all(isinstance(p, torch.nn.Parameter) and p.requires_grad and p.grad is None
                                  and not p._post_accumulate_grad_hooks for p in params)):
         # the step's first micro-batch: the gradients become row blocks of dW, so the next
         # micro-batches find them back to back (what AccumulateGrad would store: dW itself)
@@ -282,8 +293,8 @@ def _wgrad_group(dy, x, params):
             a += p.shape[0]
         return [None] * len(params)
     out, a = [], 0
-    for p in params:
-        out.append(dW[a:a + p.shape[0]])
+    for p in params:  # a frozen member gets no gradient (its block is dropped)
+        out.append(dW[a:a + p.shape[0]] if p.requires_grad else None)
         a += p.shape[0]
     return out
 

@@ -62,6 +62,9 @@ class PrlAdamW(torch.optim.AdamW):
 
     @torch.no_grad()
     def step(self, closure=None):
+        from .model_ops import weights_written
+
+        weights_written()  # parameters change below (either path): drop the fused-weight caches
         loss = None
         if closure is not None:
             with torch.enable_grad():

@@ -18,7 +18,11 @@ divided by the FSDP world when sharded; activations = the tensors a patched Qwen
 layer keeps for its backward per token (the normed inputs of the q/k/v and gate/up GEMMs, q, k,
 v, the attention output, the residual stream, gate, up and the SwiGLU output), times
 ``seq_length`` tokens, times the layers, times a 1.25 allowance for backward temporaries; one
-label-row logits chunk; 5 % of the device plus 4 GiB of headroom.
+label-row logits chunk; the build's own long-lived buffers (the fused gate/up weight cache,
+2 I x H per layer when finetune/model_ops.py fuses the projection at this micro-batch size and the
+model is not FSDP-sharded; the lm_head weight gradient's staging, [V, H] bf16 from the single-chunk
+GEMM or an fp32 accumulator over several chunks, finetune/rl/fused_linear.py); 5 % of the device
+plus 4 GiB of headroom.
 """
 
 from __future__ import annotations
@@ -42,12 +46,13 @@ class RecomputePlan:
     state_bytes: int = 0
     activation_bytes: int = 0
     logits_bytes: int = 0
+    buffer_bytes: int = 0
     device_bytes: int = 0
 
     def as_dict(self) -> dict:
         return {"checkpoint": self.checkpoint, "reason": self.reason, "state_gb": round(self.state_bytes / 1e9, 2),
                 "activation_gb": round(self.activation_bytes / 1e9, 2), "logits_gb": round(self.logits_bytes / 1e9, 2),
-                "device_gb": round(self.device_bytes / 1e9, 2)}
+                "buffer_gb": round(self.buffer_bytes / 1e9, 2), "device_gb": round(self.device_bytes / 1e9, 2)}
 
 
 def activation_bytes_per_token(config, dtype_bytes: int = 2) -> int:
@@ -63,6 +68,26 @@ def activation_bytes_per_token(config, dtype_bytes: int = 2) -> int:
     # k, v: 2 kv; gate, up, SwiGLU out: 3 I; per-row statistics (rstd, lse) are negligible
     per_layer = 6 * H + 2 * kv + 3 * inter
     return per_layer * layers * dtype_bytes
+
+
+def build_buffer_bytes(config, seq: int, chunk: int, shard_world: int, dtype_bytes: int = 2) -> int:
+    """Long-lived buffers of the build's fused paths at this micro-batch size (upper bound)."""
+    from . import model_ops
+
+    H = int(config.hidden_size)
+    inter = int(getattr(config, "intermediate_size", 4 * H))
+    layers = int(config.num_hidden_layers)
+    vocab = int(getattr(config, "vocab_size", 0))
+    out = 0
+    if shard_world <= 1 and model_ops._FUSED_GATE_UP and seq <= model_ops._FUSED_GATE_UP_MAX_ROWS:
+        out += 2 * inter * H * layers * dtype_bytes  # cat(Wg, Wu) per layer (_fused_weight)
+    if shard_world <= 1 and getattr(model_ops, "_FUSED_QKV", False):
+        heads = int(getattr(config, "num_attention_heads", 1))
+        kv = int(getattr(config, "num_key_value_heads", None) or heads) * (H // heads)
+        out += (H + 2 * kv) * H * layers * dtype_bytes
+    # lm_head dW: bf16 from one GEMM (one chunk) or an fp32 accumulator (several chunks)
+    out += vocab * H * (dtype_bytes if seq <= chunk else 4)
+    return out
 
 
 def plan_gradient_checkpointing(args, model, device: torch.device, shard_world: int = 1,
@@ -93,8 +118,9 @@ def plan_gradient_checkpointing(args, model, device: torch.device, shard_world: 
     rl = args.get("rl", None) or {}
     chunk = min(int(seq), int(rl.get("lm_head_chunk_rows", 65536) or 65536))  # RLConfig default
     logits = chunk * vocab * pbytes
-    need = state + act + logits + int(HEADROOM_FRAC * total) + HEADROOM_BYTES
+    buffers = build_buffer_bytes(config, int(seq), chunk, int(shard_world), pbytes)
+    need = state + act + logits + buffers + int(HEADROOM_FRAC * total) + HEADROOM_BYTES
     keep = need <= total
     plan = RecomputePlan(not keep, ("activations fit: no recompute" if keep else "activations do not fit: recompute"),
-                         state, act, logits, total)
+                         state, act, logits, buffers, total)
     return plan

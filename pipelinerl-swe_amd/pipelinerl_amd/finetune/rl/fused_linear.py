@@ -34,6 +34,11 @@ from ..._native import NSTAT, PRL_BF16, PRL_F32
 from .fused import GrpoParams, _relative, _workspace
 
 _ADDMM_F32: dict[str, bool] = {}
+# Parity-test tap (tests/test_configs_gpu.py): when set, called as tap(stage, q_rows, chunk, rows)
+# with stage "logits" just before the loss kernel runs on a chunk and "dlogits" just after (the
+# chunk then holds the gradient, written in place), so a test can read the label-row path's own
+# logits, per-row outputs and dlogits.  Enqueues nothing when None (the product default).
+ROW_TAP = None
 
 
 def _accumulate_dw(dw: torch.Tensor, dlg: torch.Tensor, hc: torch.Tensor) -> None:
@@ -132,9 +137,13 @@ class LinearGrpoLossFn(torch.autograd.Function):
                 cb = _c_batch(lg.data_ptr(), lg.dtype, B, L, V, V, fields)
                 co = _native.PrlGrpoOutputs(*[rows[i].data_ptr() for i in range(8)], None,
                                             lg.data_ptr() if write_grad else None, None)
+                if ROW_TAP is not None:
+                    ROW_TAP("logits", qc, lg, rows)
                 _native.check(lib.prl_grpo_forward_rows(ctypes.byref(cb), ctypes.byref(cp), qc.data_ptr(),
                                                         qc.numel(), ctypes.byref(co), stream),
                               "prl_grpo_forward_rows")
+                if ROW_TAP is not None:
+                    ROW_TAP("dlogits", qc, lg, rows)
                 if write_grad and use_prl:  # ROCm hipBLASLt (include/prl_gemm.h)
                     dh.index_copy_(0, idx, gemm.linear_dgrad(lg, w))
                     if single:

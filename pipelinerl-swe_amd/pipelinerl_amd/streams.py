@@ -90,15 +90,32 @@ def _jsonable(x: Any) -> Any:
     return x
 
 
+_NATIVE_ENCODE: list = [None]  # None: not tried yet; False: libprl_data unavailable in this process
+
+
+def _native_encoder():
+    if _NATIVE_ENCODE[0] is None:
+        from . import native_data
+        try:
+            native_data.load()
+            _NATIVE_ENCODE[0] = native_data
+        except Exception as e:  # noqa: BLE001 - no library / toolchain on this host: json (same bytes)
+            logger.warning(f"libprl_data unavailable ({e}); stream lines are written with json.dumps")
+            _NATIVE_ENCODE[0] = False
+    return _NATIVE_ENCODE[0] or None
+
+
 def dumps(data: Any) -> str:
     """One stream line.  A pydantic model or dict (a PipelineBatchEncoding, a message) goes
     through libprl_data's encoder, byte-identical to json.dumps of the lists (numeric tensors /
-    arrays formatted natively); anything else through json."""
+    arrays formatted natively); anything else — or any line on a host where libprl_data neither
+    loads nor builds (an actor host without g++) — through json, which writes the same bytes."""
     if isinstance(data, BaseModel):
         data = data.model_dump()
     if isinstance(data, dict) and all(isinstance(k, str) for k in data):
-        from . import native_data
-        return native_data.encode_document(data)
+        enc = _native_encoder()
+        if enc is not None:
+            return enc.encode_document(data)
     return json.dumps(_jsonable(data), separators=(",", ":"))
 
 

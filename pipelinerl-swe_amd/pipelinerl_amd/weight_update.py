@@ -140,7 +140,10 @@ class HipFlatPacker:
         # written through raw pointers: move the version counters as an in-place copy_ would
         from torch.autograd.graph import increment_version
 
+        from .finetune.model_ops import weights_written
+
         increment_version(tensors)
+        weights_written()
 
 
 def parameters_info(named: list[tuple[str, torch.Tensor]]) -> list[ParameterInfo]:

@@ -10,7 +10,9 @@ against the pinned oracle (oracle/grpo_oracle.py) or a plain PyTorch fp32 restat
   C3  Qwen2.5-7B lm_head (V = 152 064, H = 3584) on the largest of C3's packed micro-batches
       (prompt U{64..512} + completion U{256..8192}, packing cap 12 000): the label-row lm_head +
       loss head vs the full-logits kernel on the same GEMM and vs the oracle (statistics of every
-      row 1e-4 on the same bf16 logits; sampled rows' log-prob / entropy / dlogits), softmax rows
+      row 1e-4 on the same bf16 logits); on 8 sampled label rows the LABEL-ROW path's own
+      log-probs / entropies (1e-4) and dlogits (1e-2) vs the oracle on the logits that path formed
+      (tapped through fused_linear.ROW_TAP), the full path's dlogits vs the oracle's; softmax rows
       of dlogits sum to ~0, bitwise determinism.
   C5  Qwen2.5-32B lm_head (H = 5120) with KL to the reference on (kl_coef 0.001, ref = old +
       N(0, 0.05²)), same checks.
@@ -171,9 +173,9 @@ class _HiddenModel(torch.nn.Module):
 
 def _head_case(config: str, H: int, max_tokens: int):
     from pipelinerl_amd import workloads
-    from pipelinerl_amd.finetune.rl import rl_step
+    from pipelinerl_amd.finetune.rl import fused_linear, rl_step
 
-    mbs = workloads.micro_batches(config, 6, seq_length=max_tokens)
+    mbs = workloads.micro_batches(config, 6, seed=1234, seq_length=max_tokens)
     b = max(mbs, key=lambda x: int(x.input_ids.shape[1]))
     T = int(b.input_ids.shape[1])
     V = 152064
@@ -181,11 +183,29 @@ def _head_case(config: str, H: int, max_tokens: int):
     h = torch.randn((1, T, H), generator=g, device=DEV).to(torch.bfloat16)
     w = (torch.randn((V, H), generator=g, device=DEV) * (2.0 / H ** 0.5)).to(torch.bfloat16)
     rlc = workloads.rl_config(config, 4096)
-    bd = to_batch(_host(b) | {"attention_mask": b.attention_mask.numpy(), "seq_boundaries": b.seq_boundaries.numpy()})
+    hb = _host(b)
+    bd = to_batch(hb | {"attention_mask": b.attention_mask.numpy(), "seq_boundaries": b.seq_boundaries.numpy()})
+    # sampled label rows (flat q = t for B = 1) whose label-row-path logits / outputs / dlogits are tapped
+    lab = np.nonzero(hb["labels"][0, 1:] != -100)[0]
+    pick = lab[np.linspace(0, lab.size - 1, 8).astype(int)]
+    pick_t = torch.tensor(pick, device=DEV)
+    tapped: dict = {}
+
+    def tap(stage, qc, lg, rows):
+        pos = torch.searchsorted(qc, pick_t)  # label rows are in increasing order
+        assert bool(torch.all(qc[pos.clamp(max=qc.numel() - 1)] == pick_t)), "one chunk holds every label row here"
+        tapped[stage] = lg.index_select(0, pos).float()  # stream-ordered: before / after the kernel
+        if stage == "dlogits":
+            tapped["rows"] = rows.index_select(1, pick_t).clone()
+
     runs = []
-    for _ in range(2):
+    for i in range(2):
         model = _HiddenModel(h.clone(), w)
-        loss, stats = rl_step(model, bd, 0, 10, rlc, defer_stats=True)
+        fused_linear.ROW_TAP = tap if i == 0 else None
+        try:
+            loss, stats = rl_step(model, bd, 0, 10, rlc, defer_stats=True)
+        finally:
+            fused_linear.ROW_TAP = None
         loss.backward()
         runs.append((float(loss.detach()), stats.resolve(), model.h.grad.clone(), model.lm_head.weight.grad.clone()))
         del model
@@ -206,20 +226,33 @@ def _head_case(config: str, H: int, max_tokens: int):
     df = dl.float()
     rowsum, absum = df.sum(-1).abs(), df.abs().sum(-1)
     assert bool(torch.all(rowsum <= 4e-3 * absum + 1e-12))
-    # every row's statistics vs the oracle on the same bf16 logits (fp32 oracle, 1e-4)
+    # every row's statistics vs the oracle on the same bf16 logits (fp32 oracle, 1e-4); the
+    # oracle's per-row upstream gradients (g_lp, g_h) and its dlogits for the sampled rows
     lg = full.logits.detach().float().cpu().numpy()
-    hb = _host(b)
-    o = grpo_oracle.rl_step_oracle(lg, hb, dict(rlc.model_dump()), 0, 10, compute_grad=False, dtype=np.float32,
-                                   threads=THREADS, row_chunk=64)
+    o = grpo_oracle.rl_step_oracle(lg, hb, dict(rlc.model_dump()), 0, 10, compute_grad=True, dtype=np.float32,
+                                   threads=THREADS, row_chunk=64, grad_rows=pick)
     _stats_close(stats_f, o["stats"], 1e-4, None, f"{config} full vs oracle")
     _stats_close(stats, o["stats"], 1e-2, None, f"{config} label-row vs oracle")
-    # sampled label rows: dlogits vs the oracle's analytic gradient
-    lab = np.nonzero(hb["labels"][0, 1:] != -100)[0]
-    pick = lab[np.linspace(0, lab.size - 1, 6).astype(int)]
+    # the full-logits kernel's dlogits on the sampled rows vs the oracle's (bf16 storage: 1e-2)
+    scale = float(np.abs(o["dlogits_rows"]).max())
+    ok, err = rel_close(dl[pick].float().cpu().numpy(), o["dlogits_rows"], 1e-2, 1e-3 * scale)
+    assert ok, (config, "full-path dlogits", err)
+    # the LABEL-ROW path's own outputs on the sampled rows vs the oracle on the logits that path
+    # formed (its own GEMM over the label rows; rl/__init__.py:200-210):
+    lg_rows = tapped["logits"].cpu().numpy()
     tgt = hb["input_ids"][0, pick + 1]
-    lse, H_, tlp = grpo_oracle.row_stats(lg[0, pick], tgt, None, 1.0)
-    assert np.allclose(tlp, o["new_logprobs"][0, pick], rtol=1e-5, atol=1e-4)
-    assert np.allclose(H_, o["entropy"][0, pick], rtol=1e-5, atol=1e-4)
+    lse, ent, tlp = grpo_oracle.row_stats(lg_rows, tgt, None, rlc.temperature)
+    rows = tapped["rows"].cpu().numpy()
+    assert np.allclose(rows[0], tlp, rtol=1e-5, atol=1e-4), (config, "label-row log-probs", rows[0] - tlp)
+    assert np.allclose(rows[1], ent, rtol=1e-5, atol=1e-4), (config, "label-row entropy", rows[1] - ent)
+    #   its dlogits vs the oracle's gradient of those logits (the oracle's per-row g_lp / g_h)
+    want = grpo_oracle.row_grad(lg_rows, tgt, lse, ent, o["g_lp"][0, pick], o["g_h"][0, pick], rlc.temperature)
+    got = tapped["dlogits"].cpu().numpy()
+    assert np.abs(want).max() > 0 and np.count_nonzero(o["g_lp"][0, pick]) >= 6
+    ok, err = rel_close(got, want, 1e-2, 1e-3 * float(np.abs(want).max()))
+    assert ok, (config, "label-row dlogits", err)
+    print(f"{config}: T={T}, label-row vs full GEMM logits max |diff| on the sampled rows "
+          f"{float(np.abs(lg_rows - lg[0, pick]).max()):.3g}, dlogits err {err:.3g} (scale {np.abs(want).max():.3g})")
     return T
 
 

@@ -108,6 +108,32 @@ def test_fused_weight_cache_follows_native_adamw():
     assert torch.equal(model_ops._fused_weight(holder, (wg, wu)), torch.cat([wg.detach(), wu.detach()]))
 
 
+def test_fused_gate_up_frozen_member_gets_no_gradient():
+    """A frozen gate with a trained up (or the reverse): the fused backward assigns no .grad to the
+    frozen member (the first micro-batch used to hand both members a row block of dW,
+    which then fed clipping and the optimizer), and the trained member's gradient == the separate
+    form's."""
+    from pipelinerl_amd.finetune import model_ops
+
+    g = torch.Generator(device=DEV).manual_seed(11)
+    T, H, I = 300, 256, 512
+    for frozen in ("gate", "up"):
+        wg = torch.nn.Parameter((torch.randn((I, H), generator=g, device=DEV) * 0.05).to(torch.bfloat16))
+        wu = torch.nn.Parameter((torch.randn((I, H), generator=g, device=DEV) * 0.05).to(torch.bfloat16))
+        (wg if frozen == "gate" else wu).requires_grad_(False)
+        wg2, wu2 = (torch.nn.Parameter(w.detach().clone(), requires_grad=w.requires_grad) for w in (wg, wu))
+        holder = torch.nn.Module()
+        for _ in range(2):  # the first micro-batch and an accumulating one
+            x = torch.randn((1, T, H), generator=g, device=DEV).to(torch.bfloat16)
+            dy = torch.randn((1, T, I), generator=g, device=DEV).to(torch.bfloat16)
+            model_ops.GateUpSwiGLUFn.apply(x, wg, wu, holder).backward(dy)
+            gs, us = model_ops.SharedInputLinearFn.apply(x, wg2, None, wu2, None)
+            model_ops.SwiGLUFn.apply(gs, us).backward(dy)
+        dead, live, live2 = (wg, wu, wu2) if frozen == "gate" else (wu, wg, wg2)
+        assert dead.grad is None, frozen
+        assert (live.grad.float() - live2.grad.float()).abs().max() <= 2e-2 * live2.grad.float().abs().max()
+
+
 def test_fused_qkv_matches_separate():
     """QKVFn (one GEMM over cat(Wq, Wk, Wv), concatenated bias in the epilogue) == the separate
     SharedInputLinearFn over three micro-batches: q / k / v, dx, the weight and bias gradients to

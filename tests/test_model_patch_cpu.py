@@ -105,3 +105,23 @@ def test_decoder_patch_keeps_the_installed_layer_contract(tmp_path):
         else:
             got = layer(x, position_embeddings=pe, past_key_values=None)
             assert isinstance(got, torch.Tensor) and torch.equal(got, want)
+
+
+def test_fused_weight_cache_invalidated_by_known_writers():
+    """model_ops._fused_weight keys its cat(Wg, Wu) cache on version counters, which a write
+    through ``p.data`` or a raw pointer does not move; the build's own writers also call
+    weights_written() (PrlAdamW.step, HipFlatPacker.unflatten), which drops every cache."""
+    import torch
+
+    from pipelinerl_amd.finetune import model_ops
+
+    holder = torch.nn.Module()
+    wg = torch.nn.Parameter(torch.ones(2, 3))
+    wu = torch.nn.Parameter(torch.zeros(2, 3))
+    a = model_ops._fused_weight(holder, (wg, wu))
+    assert model_ops._fused_weight(holder, (wg, wu)) is a  # cached
+    wg.data.fill_(5.0)  # p.data has its own version counter: the parameter's does not move
+    assert model_ops._fused_weight(holder, (wg, wu)) is a  # stale (the hazard)
+    model_ops.weights_written()
+    b = model_ops._fused_weight(holder, (wg, wu))
+    assert b is not a and float(b[0, 0]) == 5.0

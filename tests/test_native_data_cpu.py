@@ -267,3 +267,27 @@ def test_data_library_exports_header_symbols():
     assert lib.prl_json_members(None, 0, None, 0, ctypes.byref(n)) == 5001
     assert lib.prl_rl_group_stats(-1, None, 0, None, None, None, None, None) == 5001
     assert lib.prl_json_array_fill(None, 1, 1) == 5001
+
+
+def test_stream_writer_falls_back_to_json_without_the_library(monkeypatch):
+    """A process where libprl_data neither loads nor builds (an actor host without g++) still
+    writes stream lines: json.dumps, the same bytes the native encoder writes."""
+    from pipelinerl_amd import native_data, streams
+    from pipelinerl_amd.finetune.types import PipelineBatchEncoding
+
+    b = PipelineBatchEncoding(input_ids=torch.tensor([[1, 2, 3]]), labels=torch.tensor([[-100, 2, 3]]),
+                              attention_mask=torch.ones(1, 3, dtype=torch.long),
+                              rewards=torch.tensor([[0.0, 1.0, 1.0]]), advantages=torch.tensor([[0.0, 0.5, 0.5]]),
+                              ref_logprobs=torch.tensor([[0.0, -0.25, -1e-5]]),
+                              old_logprobs=torch.tensor([[0.0, -0.25, -1e-5]]),
+                              group_tokens=torch.ones(1, 3), num_labels=torch.full((1, 3), 2.0),
+                              overflow=torch.zeros(1, 3), model_version=3)
+    native = streams.dumps(b)
+
+    def broken():
+        raise native_data.PrlDataError("no g++ here")
+
+    monkeypatch.setattr(streams, "_NATIVE_ENCODE", [None])
+    monkeypatch.setattr(native_data, "load", broken)
+    assert streams.dumps(b) == native
+    assert streams._NATIVE_ENCODE[0] is False  # tried once per process

@@ -84,3 +84,34 @@ def test_label_row_chunk_sizes_the_logits(m7b):
     a = plan_gradient_checkpointing(_args(), m7b, cuda, device_bytes=288 * GB)
     b = plan_gradient_checkpointing(_args(rl={"lm_head_chunk_rows": 4096}), m7b, cuda, device_bytes=288 * GB)
     assert a.logits_bytes == 12000 * 152064 * 2 and b.logits_bytes == 4096 * 152064 * 2
+
+
+def test_build_buffers_are_counted(m7b, monkeypatch):
+    """The fused gate/up weight cache (2 I H per layer, when fused at this micro-batch size and not
+    sharded) and the lm_head dW staging ([V, H]: bf16 for one chunk, fp32 over several) enter the
+    estimate: at the 7B shapes 7.6 GB + 1.1 GB; at 32B under FSDP only the dW term."""
+    from pipelinerl_amd.finetune import model_ops
+    from pipelinerl_amd.finetune.recompute import plan_gradient_checkpointing
+
+    cuda = torch.device("cuda")
+    monkeypatch.setattr(model_ops, "_FUSED_GATE_UP", True)
+    p = plan_gradient_checkpointing(_args(), m7b, cuda, device_bytes=288 * GB)
+    cache = 2 * 18944 * 3584 * 28 * 2
+    assert p.buffer_bytes == cache + 152064 * 3584 * 2, p.as_dict()
+    # several lm_head chunks: an fp32 accumulator
+    p2 = plan_gradient_checkpointing(_args(rl={"lm_head_chunk_rows": 4096}), m7b, cuda, device_bytes=288 * GB)
+    assert p2.buffer_bytes == cache + 152064 * 3584 * 4
+    # above the fused size (12 288 tokens) the cache is not built
+    p3 = plan_gradient_checkpointing(_args(seq_length=16384), m7b, cuda, device_bytes=288 * GB)
+    assert p3.buffer_bytes == 152064 * 3584 * 2
+    monkeypatch.setattr(model_ops, "_FUSED_GATE_UP", False)
+    assert plan_gradient_checkpointing(_args(), m7b, cuda, device_bytes=288 * GB).buffer_bytes == 152064 * 3584 * 2
+    # a device the estimate barely fits without the buffers: with them, recompute
+    monkeypatch.setattr(model_ops, "_FUSED_GATE_UP", True)
+    base = p.state_bytes + p.activation_bytes + p.logits_bytes
+    dev = int((base + (4 << 30) + cache // 2) / 0.95)
+    assert plan_gradient_checkpointing(_args(), m7b, cuda, device_bytes=dev).checkpoint
+    # 32B under FSDP 4: no fused cache (off under sharding), the dW term only
+    m32 = _meta_model("32b")
+    p32 = plan_gradient_checkpointing(_args(seq_length=4096), m32, cuda, shard_world=4, device_bytes=288 * GB)
+    assert p32.buffer_bytes == 152064 * 5120 * 2 and not p32.checkpoint, p32.as_dict()
