@@ -82,8 +82,31 @@ class WorkerExtension:
         elems = max(8, int(request.bucket_bytes) // 2)
         for a, b in layout.buckets(elems):
             comm.broadcast(flat[a:b], self.process_group, src=0)
+        targets = self._direct_targets(layout)
+        if targets is not None:  # parameters held directly: one HIP unflatten pass (32 tensors per launch)
+            from .weight_update import HipFlatPacker
+
+            HipFlatPacker().unflatten(flat, targets, layout.offsets)
+            return
         for name, shape, n, off in zip(layout.names, layout.shapes, layout.numels, layout.offsets):
             self._load_one(name, flat[off:off + n].view(shape))
+
+    def _direct_targets(self, layout) -> list[torch.Tensor] | None:
+        """The destination tensors when the model holds every broadcast name as a plain
+        contiguous bf16 parameter of the same shape on this HIP device (the standalone actor's
+        ParamDictModel); None for models that remap names in load_weights (vLLM's fused qkv /
+        gate_up, vllm1.py:89-93), which keep the per-name load."""
+        params = getattr(self.model_runner.model, "params", None)
+        if not isinstance(params, dict) or self.device.type != "cuda":
+            return None
+        out = []
+        for name, shape in zip(layout.names, layout.shapes):
+            p = params.get(name)
+            if (p is None or p.dtype != torch.bfloat16 or tuple(p.shape) != tuple(shape) or not p.is_contiguous()
+                    or p.device != self.device or p.data_ptr() % 16):
+                return None
+            out.append(p.detach())  # shares the version counter: the unflatten moves it
+        return out
 
     def _load_one(self, name: str, tensor: torch.Tensor):
         loaded = self.model_runner.model.load_weights(weights=[(name, tensor)])

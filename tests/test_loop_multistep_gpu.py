@@ -1,0 +1,211 @@
+"""Cross-step state of the trainer loop: THREE optimizer steps of C1 through run_finetuning_loop
+with every default on (fused gate/up at these <= 12 288-token micro-batches, native AdamW, in-GEMM
+gradient accumulation, deferred statistics, the gc freeze, label-row lm_head) against a plain
+restatement of the reference's step run beside it on the same initial weights and micro-batches:
+HF eager ops on the same bf16 weights (the reference's precision: conf/finetune/base.yaml
+``load_as_bf16: True``, Accelerate's AdamW on them), torch's library attention, the torch
+restatement of rl_step (tests/cpu_rl_step.py, pinned to the oracle by test_configs_gpu.py),
+autograd accumulation, ``clip_grad_norm_(0.3)`` + ``torch.optim.AdamW`` + the cosine schedule
+(finetune_loop.py:700-719).
+
+Compared per step: every micro-batch's statistics, the pre-clip gradient norm, and each
+parameter's update (bf16 after - before) as one relative norm over the decoder weights.  A negative
+control re-runs the product with the fused gate/up weight cache frozen after its first build (the
+stale-weight bug fixed at the end of round 2) and requires the same comparison to fail by a wide
+margin, so the bounds here are known to catch that class of cross-step bug.
+
+Shapes: Qwen2.5-0.5B with 4 of its 24 decoder layers (random init), C1's rollout generator
+(workloads.rollouts("c1", 96)) packed at 4096 tokens, 32 samples per optimizer step, lr 1e-3 (so a
+step moves bf16 weights by several ulps)."""
+
+from __future__ import annotations
+
+import copy
+import json
+import math
+import os
+import types
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+LAYERS, ROLLOUTS, PER_STEP, LR = 4, 96, 32, 1e-3
+
+
+def _data(tmp_path):
+    from pipelinerl_amd import workloads
+    from pipelinerl_amd.finetune_loop import batch_sequence_count
+    from pipelinerl_amd.streams import SingleStreamSpec, reset_streams_backend, set_streams_backend, write_to_streams
+
+    data = workloads.rollouts("c1", ROLLOUTS)
+    writes = workloads.pack(data, 4096, PER_STEP)
+    reset_streams_backend()
+    set_streams_backend("files")
+    with write_to_streams(SingleStreamSpec(exp_path=tmp_path, topic="training_data", partition=0)) as w:
+        for _, b in writes:
+            w.write(b)
+    reset_streams_backend()
+    steps, cur, n = [], [], 0
+    for _, b in writes:
+        if b.sentinel:
+            continue
+        cur.append(b)
+        n += batch_sequence_count(b)
+        if n == PER_STEP:
+            steps.append(cur)
+            cur, n = [], 0
+    assert not cur and len(steps) == ROLLOUTS // PER_STEP
+    return steps
+
+
+def _product_run(tmp_path, init, stale_cache=False):
+    """run_finetuning_loop on the product path; returns (per-step parameter snapshots [fp32 on
+    the device], per-micro-batch stats, per-step pre-clip grad norms)."""
+    from loop_helpers import loop_cfg
+
+    import pipelinerl_amd.finetune.rl as rlmod
+    from pipelinerl_amd import finetune_loop, workloads
+    from pipelinerl_amd.finetune import model_ops
+    from pipelinerl_amd.trainer_probe import qwen2_model
+
+    model = qwen2_model("0.5b", torch.device(DEV), layers=LAYERS)
+    model.load_state_dict(init)
+    snaps = [{n: p.detach().float().clone() for n, p in model.named_parameters()}]
+    stats = []
+    orig_get, orig_resolve, orig_fused = finetune_loop.get_optimizer, rlmod.RLStats.resolve, model_ops._fused_weight
+
+    def get_optimizer(*a, **k):
+        opt = orig_get(*a, **k)
+        opt.register_step_post_hook(
+            lambda o, args, kw: snaps.append({n: p.detach().float().clone() for n, p in model.named_parameters()}))
+        return opt
+
+    def resolve(self):
+        d = orig_resolve(self)
+        if "loss" in d:
+            stats.append(d)
+        return d
+
+    def frozen_cache(holder, ws, slot="_prl_fused_w"):  # the round-2 bug: built once, never rebuilt
+        hit = holder.__dict__.get(slot)
+        return hit[1] if hit is not None else orig_fused(holder, ws, slot)
+
+    exp = tmp_path / ("stale" if stale_cache else "product")
+    exp.mkdir()
+    for f in ("streams",):
+        os.symlink(tmp_path / f, exp / f)
+    for k in ("RANK", "WORLD_SIZE", "MASTER_ADDR"):
+        os.environ.pop(k, None)
+    cfg = loop_cfg(exp, exp / "unused", 1, PER_STEP, ROLLOUTS // PER_STEP, dist_backend=None, learning_rate=LR,
+                   save_final_training_state=False, log_each_n_steps=1,
+                   rl=dict(policy_loss="ppo", epsilon=4, kl_coef=0.0, final_kl_coef=0.0,
+                           clamp_log_ratio_ref_new_value=5, temperature=1.0, divide_advantage_by_std=False))
+    finetune_loop.get_optimizer = get_optimizer
+    rlmod.RLStats.resolve = resolve
+    if stale_cache:
+        model_ops._fused_weight = frozen_cache
+    try:
+        tok = types.SimpleNamespace(eos_token_id=workloads.EOS, save_pretrained=lambda *a, **k: None)
+        m = finetune_loop.run_finetuning_loop(cfg, model=model, tokenizer=tok)
+    finally:
+        finetune_loop.get_optimizer, rlmod.RLStats.resolve, model_ops._fused_weight = orig_get, orig_resolve, orig_fused
+    assert m.completed_steps == ROLLOUTS // PER_STEP
+    lines = [json.loads(x) for x in (exp / "finetune" / "logs" / "metrics.jsonl").read_text().splitlines()]
+    norms = [ln["stats/grad_norm"] for ln in lines]
+    del model
+    torch.cuda.empty_cache()
+    return snaps, stats, norms
+
+
+def _reference_run(init, steps):
+    """The reference's step on the same bf16 weights: eager HF ops, library attention, torch
+    restatement of rl_step, autograd accumulation, clip_grad_norm_ + torch AdamW + cosine."""
+    from cpu_rl_step import cpu_rl_step
+    from transformers import get_scheduler
+
+    from pipelinerl_amd import workloads
+    from pipelinerl_amd.finetune.optim import get_grouped_params
+    from pipelinerl_amd.trainer_probe import qwen2_model
+
+    saved = {k: os.environ.get(k) for k in ("PRL_ATTN_FWD", "PRL_ATTN_BWD")}
+    os.environ.update(PRL_ATTN_FWD="torch", PRL_ATTN_BWD="torch")
+    try:
+        ref = qwen2_model("0.5b", torch.device(DEV), fused_ops=False, layers=LAYERS)
+        ref.load_state_dict(init)
+        opt = torch.optim.AdamW(get_grouped_params(ref, 0.01), lr=LR)
+        sched = get_scheduler("cosine", opt, 0, len(steps))
+        rlc = workloads.rl_config("c1", PER_STEP)
+        snaps = [{n: p.detach().float().clone() for n, p in ref.named_parameters()}]
+        stats, norms = [], []
+        for k, mbs in enumerate(steps):
+            for b in mbs:
+                bd = copy.deepcopy(b).to_device(DEV)
+                bd.seq_boundaries = b.seq_boundaries
+                loss, st = cpu_rl_step(ref, bd, k, len(steps), rlc)
+                loss.backward()
+                stats.append(st)
+            norms.append(float(torch.nn.utils.clip_grad_norm_(ref.parameters(), 0.3)))
+            opt.step()
+            opt.zero_grad(set_to_none=True)
+            sched.step()
+            snaps.append({n: p.detach().float().clone() for n, p in ref.named_parameters()})
+    finally:
+        for k, v in saved.items():
+            os.environ.pop(k, None) if v is None else os.environ.__setitem__(k, v)
+    del ref, opt
+    torch.cuda.empty_cache()
+    return snaps, stats, norms
+
+
+def _update_error(a, b, k, names) -> float:
+    """|| (a_k - a_{k-1}) - (b_k - b_{k-1}) || / || b_k - b_{k-1} || over ``names``."""
+    num = den = 0.0
+    for n in names:
+        da, db = a[k][n] - a[k - 1][n], b[k][n] - b[k - 1][n]
+        num += float((da - db).double().pow(2).sum())
+        den += float(db.double().pow(2).sum())
+    return math.sqrt(num / den)
+
+
+def _stat_error(got, want) -> float:
+    return max(abs(float(g[k]) - float(w[k])) / max(1.0, abs(float(w[k])))
+               for g, w in zip(got, want) for k in ("loss", "entropy", "ratio_new_old_sum", "ratio_new_old_squared_sum"))
+
+
+def test_c1_three_optimizer_steps_match_the_reference_step(tmp_path):
+    from pipelinerl_amd.trainer_probe import qwen2_model
+
+    steps = _data(tmp_path)
+    init = {k: v.detach().clone() for k, v in qwen2_model("0.5b", torch.device(DEV), layers=LAYERS).state_dict().items()}
+    ref_snaps, ref_stats, ref_norms = _reference_run(init, steps)
+    snaps, stats, norms = _product_run(tmp_path, init)
+    n_mb = sum(len(s) for s in steps)
+    assert len(stats) == len(ref_stats) == n_mb and len(snaps) == len(ref_snaps) == len(steps) + 1
+    layer_names = [n for n in init if ".layers." in n and not n.endswith("norm.weight")]
+    mlp_names = [n for n in layer_names if ".mlp." in n]
+    upd = [_update_error(snaps, ref_snaps, k, layer_names) for k in range(1, len(steps) + 1)]
+    upd_mlp = [_update_error(snaps, ref_snaps, k, mlp_names) for k in range(1, len(steps) + 1)]
+    upd_all = [_update_error(snaps, ref_snaps, k, list(init)) for k in range(1, len(steps) + 1)]
+    # per micro-batch statistics of steps 2 and 3 depend on the updated weights
+    first = len(steps[0])
+    st_err = [_stat_error(stats[:first], ref_stats[:first]), _stat_error(stats[first:], ref_stats[first:])]
+    gn_err = [abs(a - b) / b for a, b in zip(norms, ref_norms)]
+    for g, r in zip(stats, ref_stats):
+        assert g["num_output_tokens_sum"] == r["num_output_tokens_sum"]
+    # negative control: the stale fused-weight cache (round-2 bug) on the same run
+    bad_snaps, bad_stats, bad_norms = _product_run(tmp_path, init, stale_cache=True)
+    bad_upd_mlp = [_update_error(bad_snaps, ref_snaps, k, mlp_names) for k in range(1, len(steps) + 1)]
+    bad_st = _stat_error(bad_stats[first:], ref_stats[first:])
+    print(json.dumps({"update_rel_err_layers": upd, "update_rel_err_mlp": upd_mlp, "update_rel_err_all": upd_all,
+                      "stat_err_step1_later": st_err, "grad_norm_rel_err": gn_err,
+                      "stale_cache_update_rel_err_mlp": bad_upd_mlp, "stale_cache_stat_err_later": bad_st,
+                      "grad_norms": norms, "ref_grad_norms": ref_norms}))
+    # the product's steps == the reference's, step by step
+    assert max(gn_err) <= 2e-2, gn_err
+    assert max(st_err) <= 1e-2, st_err
+    assert max(upd) <= 0.1 and max(upd_mlp) <= 0.1, (upd, upd_mlp)
+    assert max(upd_all) <= 0.1, upd_all
+    # ... and the same bounds reject the stale-cache bug (from step 2 on), by a wide margin
+    assert max(bad_upd_mlp[1:]) >= 2 * 0.1, bad_upd_mlp
