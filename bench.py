@@ -145,6 +145,72 @@ def load_traffic(T: int, V: int) -> tuple[float | None, str | None]:
     return None, None
 
 
+def dp_scaling(world: int, c3: dict | None, trainer: dict | None) -> dict | None:
+    """The north star's trainer-step scaling quantity beside `value` (which, at N > 1, is the loss
+    head's weak scaling and linear by construction): C3's data-parallel 7B step tokens/s over N x
+    what one replica does alone on its GPU in the same run (its `local` timing, no all-reduce), per
+    measured 4-micro-batch step and extrapolated to C3's 4096-sample step (one all-reduce and one
+    optimizer tail per ~hundreds of micro-batches); and the 1.5B trainer step's."""
+    if not c3 or "tokens_per_s" not in c3:
+        return None
+    out = {"metric": "C3 DP trainer tokens/s / (N x one replica's local tokens/s)", "n_gpus": world,
+           "c3_tokens_per_s": c3["tokens_per_s"], "c3_local_tokens_per_s_per_gpu": c3["local_tokens_per_s_per_gpu"],
+           "c3_efficiency": round(c3["tokens_per_s"] / (world * c3["local_tokens_per_s_per_gpu"]), 4),
+           "c3_speedup_vs_one_replica": round(c3["tokens_per_s"] / c3["local_tokens_per_s_per_gpu"], 3)}
+    ex = c3.get("extrapolated") or {}
+    if ex.get("allreduce_share") is not None:
+        out["c3_extrapolated_efficiency"] = round(1.0 - ex["allreduce_share"], 5)
+        out["c3_extrapolated_tokens_per_s"] = round(ex["tokens_per_s_per_gpu"] * world, 1)
+    if trainer and trainer.get("dp_efficiency") is not None:
+        out["trainer_step_1.5b_efficiency"] = trainer["dp_efficiency"]
+    return out
+
+
+T_START = time.perf_counter()
+
+
+class ProbeRunner:
+    """Runs the bench's side probes independently: a probe that raises is reported as an error
+    (its traceback on this rank's stderr) and the next one still runs; the ranks agree over the CPU
+    control group ``ctrl`` whether a probe failed anywhere (``error_on_another_rank``); every
+    result carries its wall time (``wall`` collects them).  A device that no longer synchronises
+    ends the probing (SystemExit) rather than queueing more work on it."""
+
+    def __init__(self, rank: int, device, ctrl=None):
+        self.rank, self.device, self.ctrl = rank, torch.device(device), ctrl
+        self.wall: dict[str, float] = {}
+
+    def run(self, name: str, fn):
+        t0 = time.perf_counter()
+        res, ok = None, 1
+        try:
+            res = fn()
+        except Exception as e:  # noqa: BLE001
+            import traceback
+
+            ok = 0
+            print(f"[rank {self.rank}] probe {name} failed:\n{traceback.format_exc()}", file=sys.stderr, flush=True)
+            res = {"error": f"{type(e).__name__}: {e}"[:400]}
+        if self.device.type == "cuda":
+            try:
+                torch.cuda.synchronize(self.device)
+                torch.cuda.empty_cache()
+            except Exception as e:  # noqa: BLE001 - the device itself failed
+                res, ok = {"error": f"device after {name}: {type(e).__name__}: {e}"[:400]}, -1
+        if self.ctrl is not None:  # every rank learns whether the probe failed anywhere
+            flag = torch.tensor([ok], dtype=torch.int64)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.ctrl)
+            if int(flag) < 1 and ok == 1:
+                res = dict(res or {}, error_on_another_rank=True)
+            ok = min(ok, int(flag))
+        self.wall[name] = round(time.perf_counter() - t0, 1)
+        if isinstance(res, dict):
+            res["wall_s"] = self.wall[name]
+        if ok < 0:
+            raise SystemExit(f"device failure in probe {name}")
+        return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -228,31 +294,70 @@ def main():
         dist.all_reduce(k_max, op=dist.ReduceOp.MAX)
     elapsed = float(t_max)
     kern_ms = float(k_max)
-    # The probes below are reported beside `value`, never in it.  A probe that raises (on every rank
-    # alike: they are collective) is reported as an error and the later probes are skipped, so the
-    # bench line is still printed.
-    failed: list[str] = []
+    # The probes below are reported beside `value`, never in it.  Each one is independent: a probe
+    # that raises is reported as an error (every rank's traceback on stderr), the ranks agree on its
+    # outcome over a CPU control group, and the next probe still runs; each reports its wall time.
+    # Order = what the north star needs first (C3 DP scaling, the 1.5B step, C5, C4, the exchange
+    # microbenchmarks), so a driver lease that runs out loses the least important ones.
+    import datetime
 
-    def optional(name: str, fn):
-        if failed:
-            return {"skipped": f"after the {failed[0]} probe failed"}
-        try:
-            return fn()
-        except Exception as e:  # noqa: BLE001
-            import traceback
-
-            failed.append(name)
-            # every rank's own failure on stderr (rank 0's line carries only its own)
-            print(f"[rank {rank}] probe {name} failed:\n{traceback.format_exc()}", file=sys.stderr, flush=True)
-            torch.cuda.empty_cache()
-            return {"error": f"{type(e).__name__}: {e}"[:400]}
+    ctrl = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=900)) if world > 1 else None
+    runner = ProbeRunner(rank, dev, ctrl)
+    optional, probe_wall = runner.run, runner.wall
 
     logits = fields = None
     torch.cuda.empty_cache()
+    c3 = None
+    if not args.no_c3:
+        # configs[2] (C3): Qwen2.5-7B DP trainer step on C3's packed math rollouts, with the full
+        # bucketed 15.23 GB gradient all-reduce at N > 1 (local / DP / all-reduce-alone timings)
+        from pipelinerl_amd.trainer_probe import dp_step_probe
+
+        c3 = optional("c3_dp", lambda: dp_step_probe("c3", micro_batches=4, steps=2, warmup=1, device=dev,
+                                                      layers=4 if rehearse else None))
+    trainer = None
+    if not args.no_trainer_step:
+        # the whole optimizer step the loss head sits in
+        from pipelinerl_amd.trainer_probe import trainer_step_probe
+
+        trainer = optional("trainer_step", lambda: trainer_step_probe("1.5b", tokens=T, micro_batches=2, steps=2,
+                                                                      warmup=1, device=dev, fused_head=True,
+                                                                      layers=4 if rehearse else None))
+    fsdp = None
+    if world >= 4 and not args.no_fsdp:
+        # configs[4] (C5): Qwen2.5-32B shapes, FSDP2 over every rank, KL-to-reference on
+        from pipelinerl_amd.trainer_probe import fsdp_step_probe
+
+        fsdp = optional("fsdp_32b", lambda: fsdp_step_probe("32b", tokens=4096, micro_batches=1, steps=2, warmup=1,
+                                                             device=dev, kl_coef=0.001,
+                                                             layers=2 if rehearse else None))
+    split = None
+    if world > 1 and not args.no_split_pipeline:
+        # configs[3] (C4): half the ranks train Qwen2.5-7B shapes data-parallel, the other half are
+        # actors receiving every step's weights from trainer rank 0 while the trainers run the next
+        # step; reports the step time with and without the broadcast in flight (hidden_frac)
+        from pipelinerl_amd import comm_probe
+        from pipelinerl_amd.trainer_probe import TrainerStep, split_pipeline_probe
+
+        # a rehearsal puts every rank on one GPU: 4 of the 7B's layers, 4 096-token micro-batches
+        split_layers, split_tokens = (4, 4096) if rehearse else (None, 16384)
+
+        def split_run():
+            shapes = comm_probe.qwen2_param_shapes("7b", layers=split_layers)
+            r = split_pipeline_probe(
+                world // 2, steps=2, warmup=1, device=dev,
+                make_trainer=lambda g: TrainerStep("7b", tokens=split_tokens, micro_batches=2, device=dev, group=g,
+                                                   layers=split_layers),
+                make_actor_module=lambda: comm_probe.ShapedModule(shapes, device=dev, fill=0.0))
+            r["model"] = (f"Qwen2.5-7b shapes{f' ({split_layers} layers)' if split_layers else ''} (random init, "
+                          f"bf16), 2 x {split_tokens}-token micro-batches per trainer rank")
+            return r
+
+        split = optional("split_pipeline", split_run)
     comm = None
     if world > 1 and not args.no_comm_probe:
-        # the trainer's two exchange steps on the C2 model's parameter set, measured after the
-        # timed region: DP gradient all-reduce, trainer -> actors broadcast
+        # the trainer's two exchange steps on the C2 model's parameter set: DP gradient all-reduce,
+        # trainer -> actors broadcast
         from pipelinerl_amd import comm_probe
 
         def exchange():
@@ -262,59 +367,6 @@ def main():
                     "weight_broadcast": comm_probe.broadcast_probe(shapes, dev, iters=3)}
 
         comm = optional("exchange", exchange)
-    trainer = None
-    if not args.no_trainer_step:
-        # the whole optimizer step the loss head sits in
-        from pipelinerl_amd.trainer_probe import trainer_step_probe
-
-        torch.cuda.empty_cache()
-        trainer = optional("trainer_step", lambda: trainer_step_probe("1.5b", tokens=T, micro_batches=2, steps=2,
-                                                                      warmup=1, device=dev, fused_head=True))
-
-    c3 = None
-    if not args.no_c3:
-        # configs[2] (C3): Qwen2.5-7B DP trainer step on C3's packed math rollouts, with the full
-        # bucketed 15.23 GB gradient all-reduce at N > 1 (local / DP / all-reduce-alone timings)
-        from pipelinerl_amd.trainer_probe import dp_step_probe
-
-        torch.cuda.empty_cache()
-        c3 = optional("c3_dp", lambda: dp_step_probe("c3", micro_batches=4, steps=2, warmup=1, device=dev,
-                                                      layers=4 if rehearse else None))
-        torch.cuda.empty_cache()
-
-    split = None
-    if world > 1 and not args.no_split_pipeline:
-        # configs[3] (C4): half the ranks train Qwen2.5-7B shapes data-parallel, the other half are
-        # actors receiving every step's weights from trainer rank 0 while the trainers run the next
-        # step; reports the step time with and without the broadcast in flight (hidden_frac)
-        from pipelinerl_amd import comm_probe
-        from pipelinerl_amd.trainer_probe import TrainerStep, split_pipeline_probe
-
-        torch.cuda.empty_cache()
-        split_model = "1.5b" if rehearse else "7b"  # every rehearsal rank shares one GPU's memory
-
-        def split_run():
-            r = split_pipeline_probe(
-                world // 2, steps=2, warmup=1, device=dev,
-                make_trainer=lambda g: TrainerStep(split_model, tokens=16384, micro_batches=2, device=dev, group=g),
-                make_actor_module=lambda: comm_probe.ShapedModule(comm_probe.qwen2_param_shapes(split_model),
-                                                                  device=dev, fill=0.0))
-            r["model"] = f"Qwen2.5-{split_model} shapes (random init, bf16), 2 x 16384-token micro-batches per trainer rank"
-            return r
-
-        split = optional("split_pipeline", split_run)
-        torch.cuda.empty_cache()
-
-    fsdp = None
-    if world >= 4 and not args.no_fsdp:
-        # configs[4] (C5): Qwen2.5-32B shapes, FSDP2 over every rank, KL-to-reference on
-        from pipelinerl_amd.trainer_probe import fsdp_step_probe
-
-        torch.cuda.empty_cache()
-        fsdp = optional("fsdp_32b", lambda: fsdp_step_probe("32b", tokens=4096, micro_batches=1, steps=2, warmup=1,
-                                                             device=dev, kl_coef=0.001,
-                                                             layers=2 if rehearse else None))
-        torch.cuda.empty_cache()
 
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
@@ -355,16 +407,15 @@ def main():
                          "traffic_source": tsrc},
             "cpu_baseline": cpu,
         }
-        if comm is not None:
-            out["exchange"] = comm
-        if trainer is not None:
-            out["trainer_step"] = trainer
-        if c3 is not None:
-            out["c3_dp"] = c3
-        if split is not None:
-            out["split_pipeline"] = split
-        if fsdp is not None:
-            out["fsdp_32b"] = fsdp
+        scaling = dp_scaling(world, c3, trainer)
+        if scaling is not None:
+            out["dp_scaling"] = scaling
+        for key, res in (("c3_dp", c3), ("trainer_step", trainer), ("fsdp_32b", fsdp), ("split_pipeline", split),
+                         ("exchange", comm)):
+            if res is not None:
+                out[key] = res
+        out["probe_wall_s"] = probe_wall
+        out["wall_total_s"] = round(time.perf_counter() - T_START, 1)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -29,9 +29,12 @@ QWEN2 = {  # config.json of the published checkpoints
 }
 
 
-def qwen2_param_shapes(name: str) -> list[tuple[str, tuple[int, ...]]]:
-    """named_parameters() order and shapes of Qwen2ForCausalLM."""
-    c = QWEN2[name]
+def qwen2_param_shapes(name: str, layers: int | None = None) -> list[tuple[str, tuple[int, ...]]]:
+    """named_parameters() order and shapes of Qwen2ForCausalLM (``layers``: only that many decoder
+    layers, as trainer_probe.qwen2_model(layers=) builds)."""
+    c = dict(QWEN2[name])
+    if layers:
+        c["layers"] = layers
     H, I, kvd = c["hidden"], c["inter"], c["hidden"] // c["heads"] * c["kv"]
     out = [("model.embed_tokens.weight", (c["vocab"], H))]
     for i in range(c["layers"]):

@@ -262,7 +262,8 @@ class TrainerStep:
 
 def trainer_step_probe(name: str = "1.5b", tokens: int = 16384, seq: int = 2048, prompt: int = 256,
                        micro_batches: int = 4, steps: int = 3, warmup: int = 1, device=None,
-                       fused_head: bool = True, grad_ckpt: bool = False, fused_ops: bool = True) -> dict:
+                       fused_head: bool = True, grad_ckpt: bool = False, fused_ops: bool = True,
+                       layers: int | None = None) -> dict:
     """The optimizer step at this world size.  With several ranks the same replica is also timed
     without the gradient all-reduce first (``local_tokens_per_s_per_gpu``: what one GPU does on its
     own, on this node at this moment), so ``dp_efficiency`` = DP / local tokens/s per GPU is the
@@ -270,7 +271,8 @@ def trainer_step_probe(name: str = "1.5b", tokens: int = 16384, seq: int = 2048,
     device = device or torch.device("cuda", torch.cuda.current_device())
     torch.cuda.reset_peak_memory_stats(device)
     multi = dist.is_initialized() and dist.get_world_size() > 1
-    ts = TrainerStep(name, tokens, seq, prompt, micro_batches, device, fused_head, grad_ckpt, fused_ops, local=multi)
+    ts = TrainerStep(name, tokens, seq, prompt, micro_batches, device, fused_head, grad_ckpt, fused_ops, local=multi,
+                     layers=layers)
     world = dist.get_world_size() if dist.is_initialized() else 1
     local = None
     if multi:
@@ -282,7 +284,8 @@ def trainer_step_probe(name: str = "1.5b", tokens: int = 16384, seq: int = 2048,
     peak = torch.cuda.max_memory_allocated(device) / 1e9
     ts.close()
     total = tokens * micro_batches * world
-    out = {"model": f"Qwen2.5-{name} shapes (random init, bf16)", "tokens_per_micro_batch": tokens,
+    out = {"model": f"Qwen2.5-{name} shapes{f' ({layers} layers)' if layers else ''} (random init, bf16)",
+           "tokens_per_micro_batch": tokens,
            "micro_batches_per_step": micro_batches, "seq_len": seq, "prompt_len": prompt,
            "loss_head": "fused_lm_head" if fused_head else "fused", "fused_model_ops": fused_ops,
            "ms_per_optimizer_step": round(sec * 1e3, 2),

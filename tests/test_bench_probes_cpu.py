@@ -1,0 +1,64 @@
+"""bench.py's side-probe orchestration on a world-2 gloo group (CPU): a probe that fails on one
+rank only is reported on every rank and does not stop the next probe; wall times are recorded;
+the top-level DP scaling quantity is formed from the C3 probe's own local / DP timings."""
+
+import json
+import os
+import sys
+from pathlib import Path
+
+import torch
+import torch.multiprocessing as mp
+
+from test_finetune_loop_cpu import free_port
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _main(rank, world, port, out):
+    sys.path[:0] = [str(ROOT), str(ROOT / "pipelinerl-swe_amd")]
+    os.environ.update(OMP_NUM_THREADS="1")
+    import torch.distributed as dist
+
+    import bench
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    ctrl = dist.new_group(backend="gloo")
+    r = bench.ProbeRunner(rank, "cpu", ctrl)
+
+    def flaky():
+        if rank == 1:
+            raise RuntimeError("out of memory on rank 1")
+        return {"value": 1}
+
+    def collective():
+        t = torch.ones(1)
+        dist.all_reduce(t)
+        return {"sum": float(t)}
+
+    res = {"flaky": r.run("flaky", flaky), "after": r.run("after", collective), "wall": r.wall}
+    Path(out, f"r{rank}.json").write_text(json.dumps(res))
+    dist.destroy_process_group()
+
+
+def test_probe_failure_is_shared_and_does_not_skip_later_probes(tmp_path):
+    mp.spawn(_main, args=(2, free_port(), str(tmp_path)), nprocs=2, join=True)
+    r0, r1 = (json.loads((tmp_path / f"r{r}.json").read_text()) for r in range(2))
+    assert "error" in r1["flaky"] and "out of memory" in r1["flaky"]["error"]
+    assert r0["flaky"]["error_on_another_rank"] is True and r0["flaky"]["value"] == 1
+    for r in (r0, r1):
+        assert r["after"]["sum"] == 2.0  # the next collective probe ran on both ranks
+        assert set(r["wall"]) == {"flaky", "after"} and r["after"]["wall_s"] >= 0
+
+
+def test_dp_scaling_from_the_c3_probe():
+    sys.path[:0] = [str(ROOT)]
+    import bench
+
+    c3 = {"tokens_per_s": 7000.0 * 8 * 0.9, "local_tokens_per_s_per_gpu": 7000.0,
+          "extrapolated": {"allreduce_share": 0.002, "tokens_per_s_per_gpu": 7100.0}}
+    s = bench.dp_scaling(8, c3, {"dp_efficiency": 0.97})
+    assert s["c3_efficiency"] == 0.9 and s["c3_speedup_vs_one_replica"] == 7.2
+    assert s["c3_extrapolated_efficiency"] == 0.998 and s["c3_extrapolated_tokens_per_s"] == 56800.0
+    assert s["trainer_step_1.5b_efficiency"] == 0.97
+    assert bench.dp_scaling(8, {"error": "x"}, None) is None
