@@ -100,7 +100,10 @@ constexpr uint32_t kPadBf16x2 = 0xF1CAF1CAu;  // two bf16 -1.0e30: contributes 2
 // on the GPU (tests/test_grpo_edge_gpu.py::test_vocab_size_limits; the interleaved schedule
 // passes it; cause not found), so rows that large keep the interleaved schedule.  Qwen2.5's
 // vocabularies are NV = 19, covered by tests/test_grpo_edge_gpu.py::test_multi_row_per_workgroup.
-constexpr int kPhasedMaxNV = 20;
+#ifndef PRL_PHASED_MAX_NV
+#define PRL_PHASED_MAX_NV 20
+#endif
+constexpr int kPhasedMaxNV = PRL_PHASED_MAX_NV;
 #ifndef PRL_ROW_PERMUTE
 #define PRL_ROW_PERMUTE 1  // A/B (tools/build_variants.py row_permute): 7.40 vs 7.46 ms per C2 launch, same box
 #endif

@@ -183,11 +183,11 @@ def test_c1_three_optimizer_steps_match_the_reference_step(tmp_path):
     snaps, stats, norms = _product_run(tmp_path, init)
     n_mb = sum(len(s) for s in steps)
     assert len(stats) == len(ref_stats) == n_mb and len(snaps) == len(ref_snaps) == len(steps) + 1
-    layer_names = [n for n in init if ".layers." in n and not n.endswith("norm.weight")]
+    layer_names = [n for n in snaps[0] if ".layers." in n and not n.endswith("norm.weight")]
     mlp_names = [n for n in layer_names if ".mlp." in n]
     upd = [_update_error(snaps, ref_snaps, k, layer_names) for k in range(1, len(steps) + 1)]
     upd_mlp = [_update_error(snaps, ref_snaps, k, mlp_names) for k in range(1, len(steps) + 1)]
-    upd_all = [_update_error(snaps, ref_snaps, k, list(init)) for k in range(1, len(steps) + 1)]
+    upd_all = [_update_error(snaps, ref_snaps, k, list(snaps[0])) for k in range(1, len(steps) + 1)]
     # per micro-batch statistics of steps 2 and 3 depend on the updated weights
     first = len(steps[0])
     st_err = [_stat_error(stats[:first], ref_stats[:first]), _stat_error(stats[first:], ref_stats[first:])]

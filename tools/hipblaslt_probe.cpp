@@ -8,7 +8,10 @@
 // Problems are given in torch's row-major terms: pass fwd  Y[T,N]  = X[T,K] W[N,K]^T
 //                                               pass dgrad dX[T,K] = dY[T,N] W[N,K]
 //                                               pass wgrad dW[N,K] = dY[T,N]^T X[T,K]
-//   hipblaslt_probe [--heuristic-only | --top K] <pass> <T> <N> <K> [<pass> <T> <N> <K> ...]
+//   hipblaslt_probe [--heuristic-only | --top K] [--no-streamk] <pass> <T> <N> <K> [<pass> <T> <N> <K> ...]
+// --no-streamk: time only candidates whose kernel is data-parallel (no "_SK<n>_" with n > 0 in
+// its name: no cross-workgroup fix-up waits), and report the stream-K mode census of the
+// candidates and of the heuristic's pick (stream-K beside RCCL).
 // Build: hipcc -O2 --offload-arch=gfx950 tools/hipblaslt_probe.cpp -lhipblaslt -o tools/hipblaslt_probe.bin
 //
 // CAUTION: a full sweep runs every solution the library reports as supporting the problem, and
@@ -68,6 +71,16 @@ static Problem make(const char* pass, int64_t T, int64_t N, int64_t K) {
   return p;
 }
 
+// stream-K mode from a Tensile kernel name ("..._SK3_..."): 0 = data-parallel
+static int sk_mode(const std::string& name) {
+  size_t p = name.find("_SK");
+  while (p != std::string::npos) {
+    if (p + 3 < name.size() && name[p + 3] >= '0' && name[p + 3] <= '9') return name[p + 3] - '0';
+    p = name.find("_SK", p + 3);
+  }
+  return 0;
+}
+
 int main(int argc, char** argv) {
   bool heur_only = argc > 1 && !strcmp(argv[1], "--heuristic-only");  // skip the full sweep
   if (heur_only) {
@@ -77,6 +90,12 @@ int main(int argc, char** argv) {
   // --top K: time only the heuristic's K ranked candidates (the library's own picks for the
   // problem, not every solution of the catalog: the lower-risk sweep)
   int top = 0;
+  bool no_sk = false;
+  if (argc > 1 && !strcmp(argv[1], "--no-streamk")) {
+    no_sk = true;
+    --argc;
+    ++argv;
+  }
   if (argc > 2 && !strcmp(argv[1], "--top")) {
     top = atoi(argv[2]);
     argc -= 2;
@@ -185,7 +204,12 @@ int main(int argc, char** argv) {
                                   dt, dt, HIPBLAS_COMPUTE_32F, all));
     std::vector<std::pair<float, int>> res;
     int supported = 0;
+    int sk_census[10] = {0};
+    const int heur_sk = nh ? sk_mode(hipblaslt_ext::getKernelNameFromAlgo(h, heur[0].algo)) : -1;
     for (size_t i = 0; i < all.size(); ++i) {
+      const int skm = sk_mode(hipblaslt_ext::getKernelNameFromAlgo(h, all[i].algo));
+      sk_census[skm] += 1;
+      if (no_sk && skm != 0) continue;
       size_t need = 0;
       if (hipblaslt_ext::matmulIsAlgoSupported(h, desc, &alpha, la, lb, &beta, lc, lc, all[i].algo, need) !=
               HIPBLAS_STATUS_SUCCESS ||
@@ -207,14 +231,17 @@ int main(int argc, char** argv) {
     std::sort(res.begin(), res.end());
     double flops = 2.0 * T * N * K;
     printf("{\"pass\": \"%s\", \"T\": %lld, \"N\": %lld, \"K\": %lld, \"solutions\": %zu, \"supported\": %d, "
-           "\"heuristic_ms\": %.4f, \"heuristic_TFLOPs\": %.1f, \"heuristic_index\": %d, \"best\": [",
+           "\"heuristic_ms\": %.4f, \"heuristic_TFLOPs\": %.1f, \"heuristic_index\": %d, \"heuristic_sk\": %d, "
+           "\"no_streamk\": %s, \"sk_census\": [%d, %d, %d, %d, %d], \"best\": [",
            pass, (long long)T, (long long)N, (long long)K, all.size(), supported, t_heur,
-           t_heur > 0 ? flops / t_heur / 1e9 : 0.0, heur_idx);
+           t_heur > 0 ? flops / t_heur / 1e9 : 0.0, heur_idx, heur_sk, no_sk ? "true" : "false", sk_census[0],
+           sk_census[1], sk_census[2], sk_census[3], sk_census[4]);
     for (size_t j = 0; j < std::min<size_t>(5, res.size()); ++j) {
       auto& alg = all[res[j].second].algo;
-      printf("%s{\"ms\": %.4f, \"TFLOPs\": %.1f, \"index\": %d, \"kernel\": \"%s\"}", j ? ", " : "", res[j].first,
-             flops / res[j].first / 1e9, hipblaslt_ext::getIndexFromAlgo(alg),
-             hipblaslt_ext::getKernelNameFromAlgo(h, alg).substr(0, 120).c_str());
+      const std::string kn = hipblaslt_ext::getKernelNameFromAlgo(h, alg);
+      printf("%s{\"ms\": %.4f, \"TFLOPs\": %.1f, \"index\": %d, \"sk\": %d, \"kernel\": \"%s\"}", j ? ", " : "",
+             res[j].first, flops / res[j].first / 1e9, hipblaslt_ext::getIndexFromAlgo(alg), sk_mode(kn),
+             kn.substr(0, 120).c_str());
     }
     printf("]}\n");
     fflush(stdout);
