@@ -88,6 +88,27 @@ constexpr int kLoadAux = PRL_LOAD_AUX;
 constexpr int kStoreAux = PRL_STORE_AUX;
 constexpr uint32_t kPadBf16x2 = 0xF1CAF1CAu;  // two bf16 -1.0e30: contributes 2^-huge = 0
 
+// A 16-byte buffer store reads its data VGPRs after it issues.  A VALU write of one of those
+// registers in the next issue slot replaced the stored data on MI355X (NV = 24 phased schedule:
+// dword 1 of vectors 2 / 4 / 6 in lanes 12-15 of each 16 held the unpacked float of the next
+// vector's logit; tools/nv24_probe.py).  LLVM inserts the wait state only for stores
+// with no register in soffset, and these stores take the vector's row offset in an SGPR soffset,
+// so it emitted none.  The store is therefore fenced: nothing is scheduled across the two
+// barriers, and s_nop 1 gives the store two wait states before its data registers are reused
+// (tools/isa_store_hazard_scan.py checks the built ISA: tests/test_isa_hazards_cpu.py).
+#ifndef PRL_STORE_FENCE
+#define PRL_STORE_FENCE 1
+#endif
+__device__ __forceinline__ void store_row_b128(u32x4 o, __amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, o), rs,
+                                         voff, soff, kStoreAux);
+#if PRL_STORE_FENCE
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 1");
+  __builtin_amdgcn_sched_barrier(0);
+#endif
+}
+
 #ifndef PRL_PHASED
 // 1: a row's stores retire (vmcnt(0)) before the next row's loads are issued, so this CU never
 // mixes reads and writes: 7.50 -> 7.24 ms per C2 launch on one box (profiles/r02_loss_phase_ab.jsonl;
@@ -235,8 +256,7 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(d[2 * j], d[2 * j + 1]);
         }
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, o),
-                                               ws, voff, k * VSTRIDE, kStoreAux);
+        store_row_b128(o, ws, voff, k * VSTRIDE);
         if constexpr (!kPhased)
           buf[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rn, voff, k * VSTRIDE, kLoadAux));
       }

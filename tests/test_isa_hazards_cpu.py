@@ -1,0 +1,48 @@
+"""The loss head's row stores carry no VMEM store-data hazard in the built gfx950 ISA.
+
+Root cause of the round-2 "wrong dlogits at NV = 24 with the phased schedule": a
+``buffer_store_dwordx4`` with an SGPR soffset directly followed by a VALU write of one of its data
+VGPRs (LLVM inserts the wait state only when soffset holds no register); on MI355X the store then
+wrote the new register contents in some lanes (tools/nv24_probe.py: dword 1 of vectors 2 / 4 / 6,
+lanes 12-15 of each 16, the unpacked float of the next vector's logit).  csrc/grpo_loss.hip fences
+its stores (store_row_b128); this compiles the kernels for gfx950 (hipcc cross-compiles on the CPU)
+in both the product build and with the phased schedule at every register-resident vocabulary
+(PRL_PHASED_MAX_NV=24) and scans every function (tools/isa_store_hazard_scan.py), including the
+other HIP sources of the library."""
+
+import shutil
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+CSRC = ROOT / "pipelinerl-swe_amd" / "pipelinerl_amd" / "csrc"
+sys.path.insert(0, str(ROOT / "tools"))
+
+pytestmark = pytest.mark.skipif(not Path("/opt/rocm/bin/hipcc").exists() and not shutil.which("hipcc"),
+                                reason="hipcc not installed")
+
+
+@pytest.mark.parametrize("src,defines", [("grpo_loss.hip", {}), ("grpo_loss.hip", {"PRL_PHASED_MAX_NV": "24"}),
+                                         ("model_ops.hip", {}), ("flat_pack.hip", {}), ("adamw.hip", {})])
+def test_no_store_data_hazard(src, defines):
+    from isa_store_hazard_scan import compile_isa, scan
+
+    isa = compile_isa(CSRC / src, defines, include=[ROOT / "include", CSRC])
+    assert "grpo_fwd_resident" in isa or src != "grpo_loss.hip"
+    hits = scan(isa)
+    assert not hits, hits[:3]
+
+
+def test_scanner_finds_the_unfenced_store():
+    """Without the fence (PRL_STORE_FENCE=0) the phased NV = 21..24 kernels show the hazard: the
+    scanner is what detects the round-2 failure."""
+    from isa_store_hazard_scan import compile_isa, scan
+
+    isa = compile_isa(CSRC / "grpo_loss.hip", {"PRL_PHASED_MAX_NV": "24", "PRL_STORE_FENCE": "0"},
+                      include=[ROOT / "include", CSRC])
+    hits = scan(isa)
+    fns = {h["function"] for h in hits}
+    assert any("grpo_fwd_residentILi24E" in f for f in fns), fns
+    assert all(h["soffset_sgpr"] for h in hits)

@@ -32,6 +32,7 @@ import torch
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 LAYERS, ROLLOUTS, PER_STEP, LR = 4, 96, 32, 1e-3
+UPDATE_BOUND = 0.15  # relative update error per step (below half the stale-cache signal, 0.38 / 0.58)
 
 
 def _data(tmp_path):
@@ -202,10 +203,12 @@ def test_c1_three_optimizer_steps_match_the_reference_step(tmp_path):
                       "stat_err_step1_later": st_err, "grad_norm_rel_err": gn_err,
                       "stale_cache_update_rel_err_mlp": bad_upd_mlp, "stale_cache_stat_err_later": bad_st,
                       "grad_norms": norms, "ref_grad_norms": ref_norms}))
-    # the product's steps == the reference's, step by step
+    # the product's steps == the reference's, step by step.  Measured on MI355X (round 3): update
+    # error 0.05 / 0.06 / 0.12 (it grows as the cosine schedule shrinks the step towards the bf16
+    # quantum), statistics 2e-5, grad norm 4e-3; the stale cache: 0.05 / 0.38 / 0.58 from step 2
     assert max(gn_err) <= 2e-2, gn_err
-    assert max(st_err) <= 1e-2, st_err
-    assert max(upd) <= 0.1 and max(upd_mlp) <= 0.1, (upd, upd_mlp)
-    assert max(upd_all) <= 0.1, upd_all
-    # ... and the same bounds reject the stale-cache bug (from step 2 on), by a wide margin
-    assert max(bad_upd_mlp[1:]) >= 2 * 0.1, bad_upd_mlp
+    assert max(st_err) <= 1e-3, st_err
+    assert max(upd) <= UPDATE_BOUND and max(upd_mlp) <= UPDATE_BOUND, (upd, upd_mlp)
+    assert max(upd_all) <= UPDATE_BOUND, upd_all
+    # ... and the same bound rejects the stale-cache bug at every step from the second on, by 2x
+    assert min(bad_upd_mlp[1:]) >= 2 * UPDATE_BOUND, bad_upd_mlp
