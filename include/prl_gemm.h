@@ -56,6 +56,11 @@ int prl_gemm_heuristic_index(int op_a, int op_b, int64_t m, int64_t n, int64_t k
  * The binding registers the indices of its shipped solution table (gemm_solutions.json). */
 int prl_gemm_allow_solutions(const int32_t* indices, int n);
 
+/* Number of hipBLASLt handles created so far: one per (device, stream) that issued a GEMM (and
+ * one per device for prl_gemm_heuristic_index / prl_gemm_library).  Launches on different streams
+ * share no handle, workspace or plan. */
+int prl_gemm_handle_count(void);
+
 /* Path and version of the hipBLASLt in use, NUL-terminated into buf (the load error if it could
  * not be opened).  Returns 0 or the load error code. */
 int prl_gemm_library(char* buf, int len);

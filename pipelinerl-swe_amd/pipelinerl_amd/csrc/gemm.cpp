@@ -10,8 +10,11 @@
 //
 // Per (op_a, op_b, m, n, k, lda, ldb, ldd, d_dtype, beta != 0) the matmul descriptor, the three
 // matrix layouts and the chosen algorithm are built once and cached; a call is then one
-// hipblasLtMatmul on the caller's stream.  Each (device, stream) pair gets its own workspace, so
-// GEMMs on different streams never share scratch memory.
+// hipblasLtMatmul on the caller's stream.  Each (device, stream) pair gets its own hipBLASLt handle
+// and its own workspace, so GEMMs issued on different streams share no library state: the gfx950
+// solutions are stream-K kernels (Tensile "SK3": workgroups that finish a tile wait on flags other
+// workgroups of the same launch set), and a stream-K launch must never see another launch's
+// fix-up state ("stream-K beside RCCL").
 #include "prl_gemm.h"
 
 #include <hip/hip_runtime.h>
@@ -82,9 +85,9 @@ struct Plan {
 };
 
 std::mutex g_mu;
-std::map<int, hipblasLtHandle_t> g_handles;
+std::map<std::pair<int, hipStream_t>, hipblasLtHandle_t> g_handles;
 std::map<std::pair<int, hipStream_t>, void*> g_workspaces;
-std::map<std::pair<int, Key>, Plan> g_plans;
+std::map<std::pair<hipblasLtHandle_t, Key>, Plan> g_plans;
 // solution indices a caller may request (prl_gemm_allow_solutions): the set that ran clean in the
 // MI355X sweeps shipped with the library; anything else is refused before it reaches the GPU
 std::vector<int> g_allowed;
@@ -162,14 +165,15 @@ bool valid(int op_a, int op_b, int64_t m, int64_t n, int64_t k, int64_t lda, int
   return true;
 }
 
-int handle_for(int dev, hipblasLtHandle_t* h) {
-  auto it = g_handles.find(dev);
+int handle_for(int dev, hipStream_t st, hipblasLtHandle_t* h) {
+  auto key = std::make_pair(dev, st);
+  auto it = g_handles.find(key);
   if (it != g_handles.end()) {
     *h = it->second;
     return 0;
   }
   RET(hb(g_api.create(h)));
-  g_handles[dev] = *h;
+  g_handles[key] = *h;
   return 0;
 }
 
@@ -248,8 +252,8 @@ void destroy(Plan& p) {
 // past kMaxPlans entries it is emptied (a plan costs one heuristic query, ~0.1 ms of host time).
 constexpr size_t kMaxPlans = 4096;
 
-int plan_for(int dev, hipblasLtHandle_t h, const Key& k, Plan** out) {
-  auto key = std::make_pair(dev, k);
+int plan_for(hipblasLtHandle_t h, const Key& k, Plan** out) {
+  auto key = std::make_pair(h, k);
   auto it = g_plans.find(key);
   if (it != g_plans.end()) {
     *out = &it->second;
@@ -280,7 +284,7 @@ Key make_key(int op_a, int op_b, int64_t m, int64_t n, int64_t k, int64_t lda, i
 
 extern "C" {
 
-int prl_gemm_abi_version(void) { return 3; }
+int prl_gemm_abi_version(void) { return 4; }
 
 const char* prl_gemm_error_string(int code) {
   if (code == 0) return "ok";
@@ -314,11 +318,11 @@ int prl_gemm_bf16(int op_a, int op_b, int64_t m, int64_t n, int64_t k, const voi
   std::lock_guard<std::mutex> lock(g_mu);
   RET(load_api());
   hipblasLtHandle_t h;
-  RET(handle_for(dev, &h));
+  RET(handle_for(dev, st, &h));
   void* ws;
   RET(workspace_for(dev, st, &ws));
   Plan* p;
-  RET(plan_for(dev, h, make_key(op_a, op_b, m, n, k, lda, ldb, ldd, d_dtype, beta, solution, bias != nullptr), &p));
+  RET(plan_for(h, make_key(op_a, op_b, m, n, k, lda, ldb, ldd, d_dtype, beta, solution, bias != nullptr), &p));
   if (bias) RET(hb(g_api.desc_set(p->desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias))));
   float alpha = 1.f;
   return hb(g_api.matmul(h, p->desc, &alpha, A, p->la, B, p->lb, &beta, D, p->ld, D, p->ld, &p->algo, ws,
@@ -333,9 +337,15 @@ int prl_gemm_heuristic_index(int op_a, int op_b, int64_t m, int64_t n, int64_t k
   std::lock_guard<std::mutex> lock(g_mu);
   hipblasLtHandle_t h;
   Plan* p;
-  if (load_api() || handle_for(dev, &h) || plan_for(dev, h, make_key(op_a, op_b, m, n, k, lda, ldb, ldd, d_dtype, beta, -1), &p))
+  if (load_api() || handle_for(dev, nullptr, &h) ||
+      plan_for(h, make_key(op_a, op_b, m, n, k, lda, ldb, ldd, d_dtype, beta, -1), &p))
     return -1;
   return p->index;
+}
+
+int prl_gemm_handle_count(void) {
+  std::lock_guard<std::mutex> lock(g_mu);
+  return (int)g_handles.size();
 }
 
 int prl_gemm_allow_solutions(const int32_t* indices, int n) {
@@ -361,7 +371,7 @@ int prl_gemm_library(char* buf, int len) {
       int dev;
       hipblasLtHandle_t h;
       rc = hp(hipGetDevice(&dev));
-      if (!rc) rc = handle_for(dev, &h);
+      if (!rc) rc = handle_for(dev, nullptr, &h);
       if (!rc) rc = hb(g_api.version(h, &ver));
     }
   }

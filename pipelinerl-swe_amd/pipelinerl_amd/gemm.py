@@ -25,7 +25,7 @@ _PKG = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ["PRL_GEMM_LIB"]) if os.environ.get("PRL_GEMM_LIB") else _PKG / "libprl_gemm.so"
 HEADER_PATH = _PKG.parents[1] / "include" / "prl_gemm.h"
 SOLUTIONS_PATH = _PKG / "gemm_solutions.json"
-ABI_VERSION = 3
+ABI_VERSION = 4
 N_, T_ = 0, 1
 F32, BF16 = 0, 1
 PRL_GEMM_E_REFUSED = 4003
@@ -61,6 +61,7 @@ def load():
                                                c.c_int64, c.c_int64, c.c_int, c.c_float]),
         "prl_gemm_library": (c.c_int, [c.c_char_p, c.c_int]),
         "prl_gemm_allow_solutions": (c.c_int, [c.POINTER(c.c_int32), c.c_int]),
+        "prl_gemm_handle_count": (c.c_int, []),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

@@ -81,7 +81,7 @@ def test_gemm_library_exports_header_symbols():
     assert len(declared) >= 5
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.prl_gemm_abi_version() == gemm.ABI_VERSION == 3
+    assert lib.prl_gemm_abi_version() == gemm.ABI_VERSION == 4
     assert lib.prl_gemm_error_string(4001).decode() == "invalid argument"
     # m = 0, a bad op, null pointers, lda < m: all PRL_GEMM_E_INVALID
     assert lib.prl_gemm_bf16(0, 0, 0, 4, 4, 1, 4, 1, 4, None, 0.0, 1, 4, 1, -1, None) == 4001

@@ -116,3 +116,28 @@ def test_solution_index_and_errors():
         gemm.linear_wgrad(dy, x, out=torch.empty((N, K + 1), dtype=torch.bfloat16, device=DEV))
     with pytest.raises(gemm.GemmError):
         gemm.gemm(0, 0, K, N, T, x.float(), K, dy, N, out, K)
+
+
+def test_streams_get_their_own_handles():
+    """Each (device, stream) that issues a GEMM gets its own hipBLASLt handle and workspace (the
+    gfx950 solutions are stream-K kernels: no launch may share fix-up state with another stream's,
+    DESIGN.md §5).  The GEMMs here never overlap: each stream is drained before the next starts."""
+    from pipelinerl_amd import gemm
+
+    lib = gemm.load()
+    g = torch.Generator(device=DEV).manual_seed(4)
+    x = torch.randn((512, 384), generator=g, device=DEV).to(torch.bfloat16)
+    w = torch.randn((640, 384), generator=g, device=DEV).to(torch.bfloat16)
+    y0 = gemm.linear_fwd(x, w, solution=-1)
+    torch.cuda.synchronize()
+    n0 = lib.prl_gemm_handle_count()
+    side = torch.cuda.Stream(device=DEV)
+    with torch.cuda.stream(side):
+        y1 = gemm.linear_fwd(x, w, solution=-1)
+    side.synchronize()
+    n1 = lib.prl_gemm_handle_count()
+    with torch.cuda.stream(side):
+        gemm.linear_fwd(x, w, solution=-1)
+    side.synchronize()
+    assert n1 == n0 + 1 and lib.prl_gemm_handle_count() == n1  # one more handle, reused after
+    assert torch.equal(y0, y1)  # same plan choice on either handle
