@@ -48,6 +48,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 from pathlib import Path
 
@@ -183,6 +184,15 @@ class ProbeRunner:
     def run(self, name: str, fn):
         t0 = time.perf_counter()
         res, ok = None, 1
+        done = threading.Event()
+        if self.rank == 0:  # progress on stderr (a silent multi-minute probe looks hung to a watchdog)
+            print(f"[bench] probe {name} started", file=sys.stderr, flush=True)
+
+            def beat():
+                while not done.wait(45.0):
+                    print(f"[bench] probe {name} running {time.perf_counter() - t0:.0f} s", file=sys.stderr, flush=True)
+
+            threading.Thread(target=beat, daemon=True).start()
         try:
             res = fn()
         except Exception as e:  # noqa: BLE001
@@ -203,7 +213,11 @@ class ProbeRunner:
             if int(flag) < 1 and ok == 1:
                 res = dict(res or {}, error_on_another_rank=True)
             ok = min(ok, int(flag))
+        done.set()
         self.wall[name] = round(time.perf_counter() - t0, 1)
+        if self.rank == 0:
+            print(f"[bench] probe {name} done in {self.wall[name]} s ({'ok' if ok == 1 else 'failed'})", file=sys.stderr,
+                  flush=True)
         if isinstance(res, dict):
             res["wall_s"] = self.wall[name]
         if ok < 0:
