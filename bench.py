@@ -207,6 +207,19 @@ class ProbeRunner:
                 torch.cuda.empty_cache()
             except Exception as e:  # noqa: BLE001 - the device itself failed
                 res, ok = {"error": f"device after {name}: {type(e).__name__}: {e}"[:400]}, -1
+        # the probe's host memory back before the next one: Python garbage and torch's cached pinned
+        # buffers (gloo stages CUDA tensors through pinned host memory in the one-GPU rehearsal)
+        import gc
+
+        gc.collect()
+        if hasattr(torch._C, "_host_emptyCache"):
+            torch._C._host_emptyCache()
+        try:
+            import psutil
+
+            rss = round(psutil.Process().memory_info().rss / 2 ** 30, 2)
+        except Exception:  # noqa: BLE001
+            rss = None
         if self.ctrl is not None:  # every rank learns whether the probe failed anywhere
             flag = torch.tensor([ok], dtype=torch.int64)
             dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.ctrl)
@@ -220,6 +233,7 @@ class ProbeRunner:
                   flush=True)
         if isinstance(res, dict):
             res["wall_s"] = self.wall[name]
+            res["host_rss_gib_after"] = rss
         if ok < 0:
             raise SystemExit(f"device failure in probe {name}")
         return res
