@@ -34,6 +34,7 @@ VARIANTS = {
     "unphased": {"PRL_PHASED": "0"},
     "phased24": {"PRL_PHASED_MAX_NV": "24"},
     "nofence": {"PRL_STORE_FENCE": "0"},
+    "noslp": {"__flags__": "-fno-slp-vectorize"},
     "swiglu_gridstride": {"PRL_SWIGLU_PHASED": "0"},
     "swiglu_phased_wg2": {"PRL_SWIGLU_PHASED": "1", "PRL_SWIGLU_PHASED_WG": "2"},
     "swiglu_rows_phased": {"PRL_SWIGLU_ROWS_PHASED": "1"},
