@@ -201,17 +201,19 @@ class ProbeRunner:
             ok = 0
             print(f"[rank {self.rank}] probe {name} failed:\n{traceback.format_exc()}", file=sys.stderr, flush=True)
             res = {"error": f"{type(e).__name__}: {e}"[:400]}
+        # the probe's memory back before the next one: Python garbage first (reference cycles can
+        # hold a probe's model and optimizer state), then torch's cached device blocks and pinned host
+        # buffers (gloo stages CUDA tensors through pinned host memory in the one-GPU rehearsal,
+        # where every rank shares one card)
+        import gc
+
+        gc.collect()
         if self.device.type == "cuda":
             try:
                 torch.cuda.synchronize(self.device)
                 torch.cuda.empty_cache()
             except Exception as e:  # noqa: BLE001 - the device itself failed
                 res, ok = {"error": f"device after {name}: {type(e).__name__}: {e}"[:400]}, -1
-        # the probe's host memory back before the next one: Python garbage and torch's cached pinned
-        # buffers (gloo stages CUDA tensors through pinned host memory in the one-GPU rehearsal)
-        import gc
-
-        gc.collect()
         if hasattr(torch._C, "_host_emptyCache"):
             torch._C._host_emptyCache()
         try:
@@ -234,6 +236,8 @@ class ProbeRunner:
         if isinstance(res, dict):
             res["wall_s"] = self.wall[name]
             res["host_rss_gib_after"] = rss
+            if self.device.type == "cuda" and ok >= 0:
+                res["device_free_gib_after"] = round(torch.cuda.mem_get_info(self.device)[0] / 2 ** 30, 2)
         if ok < 0:
             raise SystemExit(f"device failure in probe {name}")
         return res
@@ -356,7 +360,8 @@ def main():
         # configs[4] (C5): Qwen2.5-32B shapes, FSDP2 over every rank, KL-to-reference on
         from pipelinerl_amd.trainer_probe import fsdp_step_probe
 
-        fsdp = optional("fsdp_32b", lambda: fsdp_step_probe("32b", tokens=4096, micro_batches=1, steps=2, warmup=1,
+        fsdp = optional("fsdp_32b", lambda: fsdp_step_probe("32b", tokens=2048 if rehearse else 4096, micro_batches=1,
+                                                             steps=2, warmup=1,
                                                              device=dev, kl_coef=0.001,
                                                              layers=2 if rehearse else None))
     split = None

@@ -26,6 +26,8 @@ GEMM_LIB = PKG / "libprl_gemm.so"
 DATA_LIB = PKG / "libprl_data.so"
 ARCH = "gfx950"
 SOURCES = ["grpo_loss.hip", "flat_pack.hip", "model_ops.hip", "attn_bwd.hip", "adamw.hip"]
+# per-source compiler flags (beside the common ones below)
+FILE_FLAGS: dict[str, list[str]] = {}
 
 
 def hipcc() -> str:
@@ -126,7 +128,7 @@ def build(force: bool = False, resource_usage: bool = False, verbose: bool = Fal
 
     def compile_one(src: str):
         obj = objdir / (Path(src).stem + ".o")
-        cmd = [cc, *flags, "-c", str(CSRC / src), "-o", str(obj)]
+        cmd = [cc, *flags, *FILE_FLAGS.get(src, []), "-c", str(CSRC / src), "-o", str(obj)]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-8000:]}")
