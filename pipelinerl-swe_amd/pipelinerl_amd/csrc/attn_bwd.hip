@@ -115,10 +115,6 @@ __device__ __forceinline__ void stage_store(const StageT<ROWS>& st, char* base, 
 #define PRL_ATTN_EXP_NOEXP 0  // timing experiment only (wrong results): backward exp2 replaced by a multiply
 #endif
 __device__ __forceinline__ float bexp2(float x) { return PRL_ATTN_EXP_NOEXP ? x * 0.5f : __builtin_amdgcn_exp2f(x); }
-#ifndef PRL_ATTN_DBUF
-#define PRL_ATTN_DBUF 0  // 1: two LDS stage buffers, one barrier per stage (the next stage is written to the
-                         // other buffer before this stage's tiles run; its global loads run two stages ahead)
-#endif
 #ifndef PRL_ATTN_INTERLEAVE
 #define PRL_ATTN_INTERLEAVE 1  // 0: one tile at a time everywhere (A/B builds, tools/build_variants.py)
 #endif
@@ -256,7 +252,7 @@ __device__ __forceinline__ void attn_bwd_dkdv(const __bf16* __restrict__ q, cons
                                               int s1, int kb, int h0, int h1, __bf16* __restrict__ dk,
                                               __bf16* __restrict__ dv, float* __restrict__ part, int64_t T, int H,
                                               int Hkv, float c2, float scale, int g, char* sQ, char* sdO, float* sL,
-                                              float* sDl, char* sKV, char* sQ2, char* sdO2, float* sL2, float* sDl2) {
+                                              float* sDl, char* sKV) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, w = tid >> 6, hi = lane >> 5, l32 = lane & 31;
   const int64_t rsq = (int64_t)H * D, rsk = (int64_t)Hkv * D;
@@ -306,40 +302,6 @@ __device__ __forceinline__ void attn_bwd_dkdv(const __bf16* __restrict__ q, cons
     nl = lse2[(int64_t)h * T + kb + tid];
     ndl = delta[(int64_t)h * T + kb + tid];
   }
-#if PRL_ATTN_DBUF
-  char* const bQ[2] = {sQ, sQ2};
-  char* const bO[2] = {sdO, sdO2};
-  float* const bL[2] = {sL, sL2};
-  float* const bD[2] = {sDl, sDl2};
-  auto put = [&](int p) {
-    stage_store(nq, bQ[p], tid);
-    stage_store(nd, bO[p], tid);
-    if (tid < BSTAGE) {
-      bL[p][tid] = nl;
-      bD[p][tid] = ndl;
-    }
-  };
-  auto fetch = [&](int qn) {
-    nq = stage_load<BSTAGE>(q, rsq, h, qn, s1, tid);
-    nd = stage_load<BSTAGE>(dout, rsq, h, qn, s1, tid);
-    if (tid < BSTAGE && qn + tid < s1) {
-      nl = lse2[(int64_t)h * T + qn + tid];
-      ndl = delta[(int64_t)h * T + qn + tid];
-    }
-  };
-  __syncthreads();  // every wave is done with the previous head's stages: both buffers are free
-  put(0);
-  if (kb + BSTAGE < s1) fetch(kb + BSTAGE);
-  int par = 0;
-  for (int q00 = kb; q00 < s1; q00 += BSTAGE, par ^= 1) {
-    __syncthreads();  // this stage (buffer par) is visible; every wave is done with buffer par ^ 1
-    if (q00 + BSTAGE < s1) {  // the next stage into the other buffer, its successor's loads behind it
-      put(par ^ 1);
-      if (q00 + 2 * BSTAGE < s1) fetch(q00 + 2 * BSTAGE);
-    }
-    const char *cQ = bQ[par], *cO = bO[par];
-    const float *cL = bL[par], *cD = bD[par];
-#else
   for (int q00 = kb; q00 < s1; q00 += BSTAGE) {
     __syncthreads();  // every wave is done with the previous stage
     stage_store(nq, sQ, tid);
@@ -358,18 +320,15 @@ __device__ __forceinline__ void attn_bwd_dkdv(const __bf16* __restrict__ q, cons
         ndl = delta[(int64_t)h * T + qn + tid];
       }
     }
-    const char *cQ = sQ, *cO = sdO;
-    const float *cL = sL, *cD = sDl;
-#endif
     if (PRL_ATTN_INTERLEAVE && BSTAGE == 2 * TILE && kw < s1 && q00 >= kw + TILE - 1 && q00 + TILE < s1) {  // wave-uniform
-      dkdv_pair(cQ, cO, cL, cD, kf, vf, key, kval, s1, lane, c2, dKt, dVt);
+      dkdv_pair(sQ, sdO, sL, sDl, kf, vf, key, kval, s1, lane, c2, dKt, dVt);
       continue;
     }
 #pragma unroll 1
     for (int half = 0; half < BSTAGE / TILE; ++half) {
       const int q0 = q00 + TILE * half;
       if (!dkdv_live(kw, q0, s1)) continue;  // wave-uniform
-      dkdv_tile(cQ + half * TILE * 256, cO + half * TILE * 256, cL + half * TILE, cD + half * TILE, q0, kf, vf, key,
+      dkdv_tile(sQ + half * TILE * 256, sdO + half * TILE * 256, sL + half * TILE, sDl + half * TILE, q0, kf, vf, key,
                 kval, s1, lane, c2, dKt, dVt);
     }
   }
@@ -475,7 +434,7 @@ __device__ __forceinline__ void attn_bwd_dq(const __bf16* __restrict__ q, const 
                                                    const float* __restrict__ lse2, const float* __restrict__ delta,
                                                    const int32_t* __restrict__ items, __bf16* __restrict__ dq,
                                                    int64_t T, int H, int Hkv, float c2, float scale, int it, int h,
-                                                   char* sK, char* sV, char* sQO, char* sK2, char* sV2) {
+                                                   char* sK, char* sV, char* sQO) {
   const int tid = threadIdx.x;
   const int s0 = items[3 * it], s1 = items[3 * it + 1], qb = items[3 * it + 2];
   const int lane = tid & 63, w = tid >> 6, hi = lane >> 5, l32 = lane & 31;
@@ -519,28 +478,6 @@ __device__ __forceinline__ void attn_bwd_dq(const __bf16* __restrict__ q, const 
   for (int i = 0; i < 4; ++i) dQt[i] = f32x16{};
   const int kend = (qb + 128 < s1 ? qb + 128 : s1);  // causal: keys <= the block's last query
   StageT<BSTAGE> nk = stage_load<BSTAGE>(k, rsk, g, s0, s1, tid), nv = stage_load<BSTAGE>(v, rsk, g, s0, s1, tid);
-#if PRL_ATTN_DBUF
-  char* const bK[2] = {sK, sK2};
-  char* const bV[2] = {sV, sV2};
-  stage_store(nk, bK[0], tid);  // the workgroup's first use of LDS: no barrier before it
-  stage_store(nv, bV[0], tid);
-  if (s0 + BSTAGE < kend) {
-    nk = stage_load<BSTAGE>(k, rsk, g, s0 + BSTAGE, s1, tid);
-    nv = stage_load<BSTAGE>(v, rsk, g, s0 + BSTAGE, s1, tid);
-  }
-  int par = 0;
-  for (int k00 = s0; k00 < kend; k00 += BSTAGE, par ^= 1) {
-    __syncthreads();  // this stage (buffer par) is visible; every wave is done with buffer par ^ 1
-    if (k00 + BSTAGE < kend) {
-      stage_store(nk, bK[par ^ 1], tid);
-      stage_store(nv, bV[par ^ 1], tid);
-      if (k00 + 2 * BSTAGE < kend) {
-        nk = stage_load<BSTAGE>(k, rsk, g, k00 + 2 * BSTAGE, s1, tid);
-        nv = stage_load<BSTAGE>(v, rsk, g, k00 + 2 * BSTAGE, s1, tid);
-      }
-    }
-    const char *cK = bK[par], *cV = bV[par];
-#else
   for (int k00 = s0; k00 < kend; k00 += BSTAGE) {
     __syncthreads();
     stage_store(nk, sK, tid);
@@ -550,17 +487,15 @@ __device__ __forceinline__ void attn_bwd_dq(const __bf16* __restrict__ q, const 
       nk = stage_load<BSTAGE>(k, rsk, g, k00 + BSTAGE, s1, tid);
       nv = stage_load<BSTAGE>(v, rsk, g, k00 + BSTAGE, s1, tid);
     }
-    const char *cK = sK, *cV = sV;
-#endif
     if (PRL_ATTN_INTERLEAVE && BSTAGE == 2 * TILE && qw < s1 && k00 + BSTAGE - 1 <= qw && k00 + BSTAGE <= s1) {  // wave-uniform
-      dq_pair(cK, cV, qf, of, qq, qval, s1, lane, c2, lq, dq_delta, dQt);
+      dq_pair(sK, sV, qf, of, qq, qval, s1, lane, c2, lq, dq_delta, dQt);
       continue;
     }
 #pragma unroll 1
     for (int half = 0; half < BSTAGE / TILE; ++half) {
       const int k0 = k00 + TILE * half;
       if (!dq_live(qw, k0, s1, kend)) continue;  // wave-uniform
-      dq_tile(cK + half * TILE * 256, cV + half * TILE * 256, k0, qf, of, qq, qval, s1, lane, c2, lq, dq_delta, dQt);
+      dq_tile(sK + half * TILE * 256, sV + half * TILE * 256, k0, qf, of, qq, qval, s1, lane, c2, lq, dq_delta, dQt);
     }
   }
   if (!qval) return;
@@ -612,13 +547,6 @@ __global__ __launch_bounds__(256, PRL_ATTN_BWD_MINB) void attn_bwd_fused(const _
                                                       float* __restrict__ parts) {
   __shared__ __attribute__((aligned(16))) char s0[STAGE * D * 2], s1[STAGE * D * 2];
   __shared__ __attribute__((aligned(16))) float sL[STAGE], sDl[STAGE];
-#if PRL_ATTN_DBUF
-  __shared__ __attribute__((aligned(16))) char s2[STAGE * D * 2], s3[STAGE * D * 2];
-  __shared__ __attribute__((aligned(16))) float sL2[STAGE], sDl2[STAGE];
-#else
-  char *s2 = nullptr, *s3 = nullptr;
-  float *sL2 = nullptr, *sDl2 = nullptr;
-#endif
 #if PRL_ATTN_KV_LDS
   // K and V (mode 2: V) images of the key block; the dQ role's Q and dO (dO)
   __shared__ __attribute__((aligned(16))) char sKV[(PRL_ATTN_KV_LDS == 1 ? 2 : 1) * 128 * D * 2];
@@ -630,15 +558,15 @@ __global__ __launch_bounds__(256, PRL_ATTN_BWD_MINB) void attn_bwd_fused(const _
   if (b < n_split) {
     const int32_t* u = split_units + 7 * b;
     attn_bwd_dkdv(q, k, v, dout, lse2, delta, u[1], u[2], u[4], u[5], dk, dv, parts + (int64_t)u[6] * 2 * 128 * D, T,
-                  H, Hkv, c2, scale, u[3], s0, s1, sL, sDl, sKV, s2, s3, sL2, sDl2);
+                  H, Hkv, c2, scale, u[3], s0, s1, sL, sDl, sKV);
   } else if (b < n_split + n_kv * Hkv) {
     const int it = (b - n_split) / Hkv, g = (b - n_split) % Hkv;
     attn_bwd_dkdv(q, k, v, dout, lse2, delta, kv_items[3 * it + 1], kv_items[3 * it + 2], g * rep, (g + 1) * rep, dk,
-                  dv, nullptr, T, H, Hkv, c2, scale, g, s0, s1, sL, sDl, sKV, s2, s3, sL2, sDl2);
+                  dv, nullptr, T, H, Hkv, c2, scale, g, s0, s1, sL, sDl, sKV);
   } else {
     const int nd = n_split + n_kv * Hkv;
     const int lq = xcd_group_remap(b - nd, (int)gridDim.x - nd, rep);
-    attn_bwd_dq(q, k, v, dout, lse2, delta, q_items, dq, T, H, Hkv, c2, scale, lq / H, lq % H, s0, s1, sKV, s2, s3);
+    attn_bwd_dq(q, k, v, dout, lse2, delta, q_items, dq, T, H, Hkv, c2, scale, lq / H, lq % H, s0, s1, sKV);
   }
 }
 
@@ -734,9 +662,6 @@ __global__ __launch_bounds__(256, PRL_ATTN_FWD_MINB) void attn_fwd(const __bf16*
                                                 __bf16* __restrict__ out, float* __restrict__ lse2, int64_t T, int H,
                                                 int Hkv, float c2) {
   __shared__ __attribute__((aligned(16))) char sK[STAGE * D * 2], sV[STAGE * D * 2];
-#if PRL_ATTN_DBUF
-  __shared__ __attribute__((aligned(16))) char sK2[STAGE * D * 2], sV2[STAGE * D * 2];
-#endif
   const int tid = threadIdx.x;
   const int lb = xcd_group_remap(blockIdx.x, gridDim.x, H / Hkv);
   const int it = lb / H, h = lb % H;
@@ -756,26 +681,6 @@ __global__ __launch_bounds__(256, PRL_ATTN_FWD_MINB) void attn_fwd(const __bf16*
   float m = -1e30f, l = 0.f;  // running max (base-2 units) and sum for query qq
   const int kend = (qb + 128 < s1 ? qb + 128 : s1);
   Stage nk = stage_load(k, rsk, g, s0, s1, tid), nv = stage_load(v, rsk, g, s0, s1, tid);
-#if PRL_ATTN_DBUF
-  stage_store(nk, sK, tid);
-  stage_store(nv, sV, tid);
-  if (s0 + STAGE < kend) {
-    nk = stage_load(k, rsk, g, s0 + STAGE, s1, tid);
-    nv = stage_load(v, rsk, g, s0 + STAGE, s1, tid);
-  }
-  int par = 0;
-  for (int k00 = s0; k00 < kend; k00 += STAGE, par ^= 1) {
-    __syncthreads();  // this stage (buffer par) is visible; every wave is done with buffer par ^ 1
-    if (k00 + STAGE < kend) {
-      stage_store(nk, par ? sK : sK2, tid);
-      stage_store(nv, par ? sV : sV2, tid);
-      if (k00 + 2 * STAGE < kend) {
-        nk = stage_load(k, rsk, g, k00 + 2 * STAGE, s1, tid);
-        nv = stage_load(v, rsk, g, k00 + 2 * STAGE, s1, tid);
-      }
-    }
-    const char *cK = par ? sK2 : sK, *cV = par ? sV2 : sV;
-#else
   for (int k00 = s0; k00 < kend; k00 += STAGE) {
     __syncthreads();
     stage_store(nk, sK, tid);
@@ -785,8 +690,6 @@ __global__ __launch_bounds__(256, PRL_ATTN_FWD_MINB) void attn_fwd(const __bf16*
       nk = stage_load(k, rsk, g, k00 + STAGE, s1, tid);
       nv = stage_load(v, rsk, g, k00 + STAGE, s1, tid);
     }
-    const char *cK = sK, *cV = sV;
-#endif
 #pragma unroll 1
     for (int half = 0; half < STAGE / TILE; ++half) {
       const int k0 = k00 + TILE * half;
@@ -794,9 +697,9 @@ __global__ __launch_bounds__(256, PRL_ATTN_FWD_MINB) void attn_fwd(const __bf16*
       // every key of the tile visible to every query of the wave: the unmasked body (all but the
       // diagonal tile of each wave); wave-uniform, two separate code paths
       if (k0 + TILE - 1 <= qw && k0 + TILE <= s1)
-        fwd_tile<false>(cK + half * TILE * 256, cV + half * TILE * 256, k0, qf, qq, qval, s1, lane, c2, m, l, Ot);
+        fwd_tile<false>(sK + half * TILE * 256, sV + half * TILE * 256, k0, qf, qq, qval, s1, lane, c2, m, l, Ot);
       else
-        fwd_tile<true>(cK + half * TILE * 256, cV + half * TILE * 256, k0, qf, qq, qval, s1, lane, c2, m, l, Ot);
+        fwd_tile<true>(sK + half * TILE * 256, sV + half * TILE * 256, k0, qf, qq, qval, s1, lane, c2, m, l, Ot);
     }
   }
   if (!qval) return;

@@ -35,8 +35,6 @@ VARIANTS = {
     "phased24": {"PRL_PHASED_MAX_NV": "24"},
     "nofence": {"PRL_STORE_FENCE": "0"},
     "noslp": {"__flags__": "-fno-slp-vectorize"},
-    "attn_dbuf": {"PRL_ATTN_DBUF": "1"},
-    "attn_dbuf_noslp": {"PRL_ATTN_DBUF": "1", "__flags__": "-fno-slp-vectorize"},
     "swiglu_gridstride": {"PRL_SWIGLU_PHASED": "0"},
     "swiglu_phased_wg2": {"PRL_SWIGLU_PHASED": "1", "PRL_SWIGLU_PHASED_WG": "2"},
     "swiglu_rows_phased": {"PRL_SWIGLU_ROWS_PHASED": "1"},
