@@ -332,6 +332,111 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_wide(const uint16_t* __restri
   for (int i = threadIdx.x; i < H; i += 256) partial[(int64_t)blockIdx.x * H + i] = red[i];
 }
 
+// Wide rows with the dw accumulators in LDS instead of registers (PRL_NORM_BWD_LDS, 5 <= NV <= 8):
+// rmsnorm_bwd_wide keeps 8 fp32 accumulators per 16-B vector (56 per lane at H = 3 584) beside the
+// packed x / dy / dres of the row and of the next one the compiler prefetches: 339 registers, one
+// wave per SIMD (3.8 TB/s).  Here each wave owns one H-float row of LDS (its rows' sums in the same
+// order, so the partials are bit-identical), the four rows fold in wave order at the end, and the
+// kernel fits 256 registers: two workgroups (two waves per SIMD) per CU, 2 x 4 x H x 4 B of LDS.
+// LDS layout per wave: [vector k][half h][lane][4 floats] (16-B, lane-contiguous: conflict-free).
+#ifndef PRL_NORM_BWD_LDS
+#define PRL_NORM_BWD_LDS 1
+#endif
+template <int NV, bool ADD>
+__global__ __launch_bounds__(256, 2) void rmsnorm_bwd_lds(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
+                                                          const uint16_t* __restrict__ w, const float* __restrict__ rstd,
+                                                          uint16_t* __restrict__ dx, float* __restrict__ partial,
+                                                          int64_t rows, int H, const uint16_t* __restrict__ dres) {
+  typedef float f32x4_t __attribute__((ext_vector_type(4)));
+  __shared__ f32x4_t acc[4][NV * 2 * 64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t wave = (int64_t)blockIdx.x * 4 + wid;
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
+  const int nv8 = H >> 3;
+  const float invH = 1.0f / (float)H;
+  f32x4_t* my = acc[wid];
+#pragma unroll
+  for (int i = 0; i < NV * 2; ++i) my[i * 64 + lane] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  u32x4 wv[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int c = k * 64 + lane;
+    wv[k] = c < nv8 ? reinterpret_cast<const u32x4*>(w)[c] : u32x4{0, 0, 0, 0};
+  }
+  for (int64_t r = wave; r < rows; r += nwaves) {
+    const u32x4* xr = reinterpret_cast<const u32x4*>(x + r * H);
+    const u32x4* gr = reinterpret_cast<const u32x4*>(dy + r * H);
+    const float rs = rstd[r];
+    u32x4 xv[NV], gv[NV], dv[ADD ? NV : 1];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = k * 64 + lane;
+      xv[k] = c < nv8 ? __builtin_nontemporal_load(xr + c) : u32x4{0, 0, 0, 0};
+      gv[k] = c < nv8 ? __builtin_nontemporal_load(gr + c) : u32x4{0, 0, 0, 0};
+      if constexpr (ADD)
+        dv[k] = c < nv8 ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(dres + r * H) + c)
+                        : u32x4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int k = 0; k < NV; ++k) asm volatile("" : "+v"(wv[k]));
+    float dot = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      f32x4_t a0 = my[(2 * k) * 64 + lane], a1 = my[(2 * k + 1) * 64 + lane];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float g0 = r16(lo(gv[k][j]) * lo(wv[k][j])), g1 = r16(hi(gv[k][j]) * hi(wv[k][j]));
+        dot = __builtin_fmaf(g0, lo(xv[k][j]), __builtin_fmaf(g1, hi(xv[k][j]), dot));
+        const float t0 = r16(lo(xv[k][j]) * rs), t1 = r16(hi(xv[k][j]) * rs);
+        const float c0 = r16(lo(gv[k][j]) * t0), c1 = r16(hi(gv[k][j]) * t1);
+        if (j < 2) {
+          a0[2 * j] += c0;
+          a0[2 * j + 1] += c1;
+        } else {
+          a1[2 * j - 4] += c0;
+          a1[2 * j - 3] += c1;
+        }
+      }
+      my[(2 * k) * 64 + lane] = a0;
+      my[(2 * k + 1) * 64 + lane] = a1;
+    }
+    dot = wave_sum(dot);
+    const float cfac = rs * rs * rs * invH * dot;
+    u32x4* dr = reinterpret_cast<u32x4*>(dx + r * H);
+#pragma unroll
+    for (int k = 0; k < NV; ++k) asm volatile("" : "+v"(xv[k]), "+v"(gv[k]), "+v"(wv[k]));  // re-unpack below
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = k * 64 + lane;
+      if (c < nv8) {
+        u32x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float g0 = r16(lo(gv[k][j]) * lo(wv[k][j])), g1 = r16(hi(gv[k][j]) * hi(wv[k][j]));
+          o[j] = pack(rs * g0 - cfac * lo(xv[k][j]), rs * g1 - cfac * hi(xv[k][j]));
+        }
+        if constexpr (ADD) {  // + the residual branch's gradient, summed as autograd would (bf16 + bf16)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = pack(lo(o[j]) + lo(dv[k][j]), hi(o[j]) + hi(dv[k][j]));
+        }
+        __builtin_nontemporal_store(o, dr + c);
+      }
+    }
+  }
+  __syncthreads();
+  // block partial of dw: the 4 waves' rows folded in wave order (as rmsnorm_bwd_wide does)
+  const float* a = reinterpret_cast<const float*>(&acc[0][0]);
+  constexpr int kRow = NV * 2 * 64 * 4;  // floats per wave row
+  for (int i = threadIdx.x; i < H; i += 256) {
+    const int v8 = i >> 3, j = i & 7, k = v8 >> 6, ln = v8 & 63;
+    const int off = ((2 * k + (j >> 2)) * 64 + ln) * 4 + (j & 3);
+    float sum = a[off];
+#pragma unroll
+    for (int wi = 1; wi < 4; ++wi) sum = sum + a[wi * kRow + off];
+    partial[(int64_t)blockIdx.x * H + i] = sum;
+  }
+}
+
 // dw = sum over the bwd kernel's block partials, deterministic, two levels:
 // stage 1: block (column tile of 64, slice s) -> 4 waves x (rows of the slice) -> LDS fold;
 // stage 2: one thread per column folds the slices in order.
@@ -717,9 +822,10 @@ hipError_t launch_norm_fwd(const void* x, const void* w, void* y, float* rstd, i
 template <int NV, bool ADD>
 hipError_t launch_norm_bwd_t(const void* dy, const void* x, const void* w, const float* rstd, void* dx, float* partial,
                              int64_t rows, int H, int grid, hipStream_t s, const void* dres) {
-  hipLaunchKernelGGL((NV <= 4 ? rmsnorm_bwd_narrow<NV, ADD> : rmsnorm_bwd_wide<NV, ADD>), dim3(grid), dim3(256), 0, s,
-                     (const uint16_t*)dy, (const uint16_t*)x, (const uint16_t*)w, rstd, (uint16_t*)dx, partial, rows, H,
-                     (const uint16_t*)dres);
+  auto kern = NV <= 4 ? rmsnorm_bwd_narrow<NV, ADD>
+                      : (PRL_NORM_BWD_LDS && NV <= 8 ? rmsnorm_bwd_lds<NV, ADD> : rmsnorm_bwd_wide<NV, ADD>);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, (const uint16_t*)dy, (const uint16_t*)x, (const uint16_t*)w,
+                     rstd, (uint16_t*)dx, partial, rows, H, (const uint16_t*)dres);
   return hipGetLastError();
 }
 template <int NV>
@@ -776,6 +882,9 @@ constexpr int kNormBlocks = 2048;  // rmsnorm backward blocks (4 waves each): en
 #ifndef PRL_NORM_FWD_GRID
 #define PRL_NORM_FWD_GRID 1536
 #endif
+#ifndef PRL_NORM_LDS_GRID
+#define PRL_NORM_LDS_GRID 512
+#endif
 #ifndef PRL_NORM_GRID
 #define PRL_NORM_GRID 768
 #endif
@@ -815,7 +924,9 @@ static int norm_backward(const void* dy, const void* x, const void* w, const flo
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int nv = (int)((H / 8 + 63) / 64);
   const int64_t g = (rows + 3) / 4;
-  const int grid = (int)(g < PRL_NORM_GRID ? (g > 0 ? g : 1) : PRL_NORM_GRID);
+  // the LDS-accumulator kernel holds two workgroups per CU: one resident round is 2 x 256
+  const int cap = (PRL_NORM_BWD_LDS && nv > 4 && nv <= 8) ? PRL_NORM_LDS_GRID : PRL_NORM_GRID;
+  const int grid = (int)(g < cap ? (g > 0 ? g : 1) : cap);
   float* partial = static_cast<float*>(workspace);
   hipError_t e = norm_bwd_table(nv, dy, x, w, rstd, dx, partial, rows, (int)H, grid, s, dres,
                                 std::make_integer_sequence<int, kMaxNVBwd>{});

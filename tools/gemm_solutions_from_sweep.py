@@ -1,7 +1,7 @@
 """Merge tools/hipblaslt_probe.bin sweep lines (JSONL) into pipelinerl_amd/gemm_solutions.json:
 for each problem whose fastest solution beats the library heuristic by > 3 %, record
 {T, index, ms, heuristic_ms} under "pass:N:K:dtype:accumulate" ("wgrad32" = the fp32 accumulating
-lm_head weight gradient).  prl_gemm uses an entry for token counts within 2x of its T.
+lm_head weight gradient, "wgradacc" = a bf16 weight gradient added into .grad, beta = 1).  prl_gemm uses an entry for token counts within 2x of its T.
 
     python tools/gemm_solutions_from_sweep.py profiles/r01_hipblaslt_rocm72_sweep_*.jsonl
 """
@@ -22,8 +22,9 @@ def main(paths):
             d = json.loads(line)
             if not d.get("best") or d["heuristic_ms"] <= 0 or d["best"][0]["ms"] >= 0.97 * d["heuristic_ms"]:
                 continue
-            pas, f32 = ("wgrad", True) if d["pass"] == "wgrad32" else (d["pass"], False)
-            key = f"{pas}:{d['N']}:{d['K']}:{'f32' if f32 else 'bf16'}:{int(f32)}"
+            pas, f32, acc = {"wgrad32": ("wgrad", True, True), "wgradacc": ("wgrad", False, True)}.get(
+                d["pass"], (d["pass"], False, False))
+            key = f"{pas}:{d['N']}:{d['K']}:{'f32' if f32 else 'bf16'}:{int(acc)}"
             ent = [e for e in table.get(key, []) if e["T"] != d["T"]]
             ent.append({"T": d["T"], "index": d["best"][0]["index"], "ms": d["best"][0]["ms"],
                         "heuristic_ms": d["heuristic_ms"]})

@@ -62,7 +62,7 @@ static Problem make(const char* pass, int64_t T, int64_t N, int64_t K) {
     p = {HIPBLAS_OP_T, HIPBLAS_OP_N, N, T, K, K, K, N};
   } else if (!strcmp(pass, "dgrad")) {  // dX^T[K,T] = W^T (col-major KxN, op N) * dY^T (col-major NxT, op N)
     p = {HIPBLAS_OP_N, HIPBLAS_OP_N, K, T, N, K, N, K};
-  } else if (!strcmp(pass, "wgrad") || !strcmp(pass, "wgrad32")) {  // dW^T[K,N] = X^T (col-major KxT, op N) * dY (col-major NxT, op T)
+  } else if (!strcmp(pass, "wgrad") || !strcmp(pass, "wgrad32") || !strcmp(pass, "wgradacc")) {  // dW^T[K,N] = X^T (col-major KxT, op N) * dY (col-major NxT, op T)
     p = {HIPBLAS_OP_N, HIPBLAS_OP_T, K, N, T, K, N, K};
   } else {
     fprintf(stderr, "unknown pass %s\n", pass);
@@ -131,6 +131,7 @@ int main(int argc, char** argv) {
     int64_t T = atoll(argv[a + 1]), N = atoll(argv[a + 2]), K = atoll(argv[a + 3]);
     Problem p = make(pass, T, N, K);
     const bool f32 = !strcmp(pass, "wgrad32");  // fp32 dW accumulated over chunks (beta = 1)
+    const bool acc = f32 || !strcmp(pass, "wgradacc");  // bf16 dW added into .grad (beta = 1)
     const hipDataType dt = f32 ? HIP_R_32F : HIP_R_16BF;
     int64_t a_rows = p.opA == HIPBLAS_OP_N ? p.m : p.k, a_cols = p.opA == HIPBLAS_OP_N ? p.k : p.m;
     int64_t b_rows = p.opB == HIPBLAS_OP_N ? p.k : p.n, b_cols = p.opB == HIPBLAS_OP_N ? p.n : p.k;
@@ -152,7 +153,7 @@ int main(int argc, char** argv) {
     CK(hipblasLtMatrixLayoutCreate(&la, HIP_R_16BF, a_rows, a_cols, p.lda));
     CK(hipblasLtMatrixLayoutCreate(&lb, HIP_R_16BF, b_rows, b_cols, p.ldb));
     CK(hipblasLtMatrixLayoutCreate(&lc, dt, p.m, p.n, p.ldc));
-    float alpha = 1.f, beta = f32 ? 1.f : 0.f;
+    float alpha = 1.f, beta = acc ? 1.f : 0.f;
     for (int r = 0; r < 2; ++r) CK(hipMemset(C[r], 0, c_bytes));
 
     // one timed probe launch first; only solutions within 1.3x of the best so far get the full
