@@ -17,7 +17,7 @@ import torch  # noqa: E402
 from pipelinerl_amd import _native  # noqa: E402
 
 
-def run(lib, rows, H, add, seed=0):
+def run(lib, rows, H, add, seed=0, time_iters=0):
     g = torch.Generator(device="cuda").manual_seed(seed)
     x = (torch.randn((rows, H), generator=g, device="cuda") * 2).to(torch.bfloat16)
     w = (1 + 0.1 * torch.randn(H, generator=g, device="cuda")).to(torch.bfloat16)
@@ -48,6 +48,18 @@ def run(lib, rows, H, add, seed=0):
                nb.value, rows, H, st)
     assert rc == 0, rc
     torch.cuda.synchronize()
+    if time_iters:  # the C-ABI call alone (backward kernel + the two dw folds), HIP events
+        args = ((dy.data_ptr(), dh.data_ptr(), x.data_ptr(), w.data_ptr(), rstd.data_ptr(), dx.data_ptr(), dw.data_ptr(),
+                 ws.data_ptr(), nb.value, rows, H, st) if add else
+                (dy.data_ptr(), x.data_ptr(), w.data_ptr(), rstd.data_ptr(), dx.data_ptr(), dw.data_ptr(), ws.data_ptr(),
+                 nb.value, rows, H, st))
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(time_iters):
+            f(*args)
+        e1.record()
+        e1.synchronize()
+        return dx, dw, e0.elapsed_time(e1) / time_iters
     return dx, dw
 
 
@@ -61,6 +73,14 @@ def main():
             dxb, dwb = run(b, rows, H, add)
             out.append({"rows": rows, "H": H, "add": add, "dx_equal": bool(torch.equal(dxa.view(torch.int16), dxb.view(torch.int16))),
                         "dw_equal": bool(torch.equal(dwa.view(torch.int16), dwb.view(torch.int16)))})
+    # timing, alternated: the C ABI call at the 7B add-norm shape (C3 micro-batch rows)
+    tim = {"product": [], "other": []}
+    for _ in range(4):
+        for name, lib in (("product", a), ("other", b)):
+            tim[name].append(round(run(lib, 8704, 3584, True, time_iters=200)[2] * 1e3, 2))
+    nbytes = 4 * 8704 * 3584 * 2
+    out.append({"add_rmsnorm_backward_8704x3584_us": tim, "algorithmic_bytes": nbytes,
+                "TBps": {k: round(nbytes / (min(v) * 1e-6) / 1e12, 3) for k, v in tim.items()}})
     print(json.dumps(out))
 
 
