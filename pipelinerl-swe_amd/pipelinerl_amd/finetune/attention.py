@@ -14,6 +14,7 @@ the build's HIP flash-attention backward (csrc/attn_bwd.hip; 1.41x / 1.15x the l
 
 from __future__ import annotations
 
+import heapq
 import logging
 import os
 
@@ -58,31 +59,22 @@ def _items(bounds: list[int], device) -> tuple:
 
 _SPLITS: dict[tuple, tuple] = {}
 SPLIT_MIN_RATIO = 1.2
+# part cap as a fraction of the target; None: chosen per packing by _makespan.  PRL_ATTN_SPLIT_CAP=1.0
+# is the round-2 rule (A/B), tools/attn_role_split.py sweeps it
+SPLIT_CAP_FRAC: float | None = float(os.environ["PRL_ATTN_SPLIT_CAP"]) if os.environ.get("PRL_ATTN_SPLIT_CAP") else None
+SPLIT_CAPS = (1.0, 0.5, 0.33)
+SPLIT_MARGIN = 0.04
+# Costs of the list-schedule model (MI355X, 28 / 4 and 12 / 2 heads, profiles/r03_attn_cap_sweep.jsonl):
+# one 32-query tile of one query head in a dK/dV workgroup, one 32-key tile in a dQ workgroup, the
+# fp32 partial a split part writes, and attn_bwd_dkdv_reduce (launch + reading the partials).
+KV_TILE_US, Q_TILE_US, PART_US = 1.2, 0.93, 4.0
+REDUCE_US, REDUCE_US_PER_SLOT = 5.0, 0.033
 
 
-def split_plan(bounds: list[int], heads: int, kv_heads: int, cus: int) -> tuple[list, list, list, int]:
-    """Which dK/dV key blocks to split over the query heads of their group (host arithmetic only).
-
-    A dK/dV workgroup sweeps all ``rep = heads / kv_heads`` query heads over every query after its
-    key block: for the first blocks of a long sequence that is far more than a CU's share of the
-    launch (a lone 4 096-token sequence at 28 / 4 heads: its first workgroup alone runs as long as
-    two whole sequences, profiles/r02_attn_ragged.jsonl).  Work is counted in MFMAs per wave (one
-    wave per SIMD: a workgroup's duration follows it): dK/dV 32 per 32-query tile per query head,
-    dQ 24 per 32-key tile.  Key blocks whose workgroup exceeds 1.2 x target, target = max(the
-    per-SIMD average, the largest dQ workgroup), are cut into min(rep, ceil(work / target))
-    contiguous head ranges (below 1.2 the split measured no faster: profiles/r02_attn_split_ab.jsonl).
-
-    Returns (kv_rows, split_units, split_groups, slots): the unsplit (seq_start, seq_end,
-    block_start) rows, the 7-tuples and 5-tuples of prl_attn_bwd_split, and the partial slots."""
-    rep = heads // kv_heads
-    rows = [(a, b, x) for a, b in zip(bounds[:-1], bounds[1:]) for x in range(a, b, BLOCK)]
-    w_kv = {r: rep * 32 * -(-(r[1] - r[2]) // 32) for r in rows}
-    w_q = [24 * -(-(min(r[2] + BLOCK, r[1]) - r[0]) // 32) for r in rows]
-    total = 4 * (kv_heads * sum(w_kv.values()) + heads * sum(w_q))
-    target = max(total / (4 * max(1, cus)), max(w_q, default=0), 1)
+def _plan(rows: list, w_kv: dict, rep: int, kv_heads: int, cap: float | None) -> tuple[list, list, list, int]:
     kv_rows, units, groups, slot = [], [], [], 0
     for r in rows:
-        parts = min(rep, -(-w_kv[r] // int(target))) if w_kv[r] > SPLIT_MIN_RATIO * target else 1
+        parts = min(rep, -(-w_kv[r] // cap)) if cap is not None and w_kv[r] > SPLIT_MIN_RATIO * cap else 1
         if parts <= 1:
             kv_rows.append(r)
             continue
@@ -94,6 +86,65 @@ def split_plan(bounds: list[int], heads: int, kv_heads: int, cus: int) -> tuple[
                 slot += 1
     units.sort(key=lambda u: -(u[5] - u[4]) * (u[1] - u[2]))  # heaviest first
     return kv_rows, units, groups, slot
+
+
+def _makespan(rows: list, kv_rows: list, units: list, slots: int, heads: int, kv_heads: int, cus: int) -> float:
+    """Modelled duration (us) of the fused launch + the partial reduce: the workgroups in launch
+    order (split parts, key blocks, query blocks, each heaviest first), one per CU, each starting on
+    the CU that frees first (one wave per SIMD: a CU runs one workgroup at a time)."""
+    rep = heads // kv_heads
+    jobs = [(u[5] - u[4]) * -(-(u[1] - u[2]) // 32) * KV_TILE_US + PART_US for u in units]
+    for r in sorted(kv_rows, key=lambda r: -(r[1] - r[2])):
+        jobs += [rep * -(-(r[1] - r[2]) // 32) * KV_TILE_US] * kv_heads
+    for r in sorted(rows, key=lambda r: -(min(r[2] + BLOCK, r[1]) - r[0])):
+        jobs += [-(-(min(r[2] + BLOCK, r[1]) - r[0]) // 32) * Q_TILE_US] * heads
+    free = [0.0] * max(1, cus)
+    end = 0.0
+    for j in jobs:
+        t = heapq.heappop(free) + j
+        heapq.heappush(free, t)
+        end = max(end, t)
+    return end + (REDUCE_US + REDUCE_US_PER_SLOT * slots if units else 0.0)
+
+
+def split_plan(bounds: list[int], heads: int, kv_heads: int, cus: int) -> tuple[list, list, list, int]:
+    """Which dK/dV key blocks to split over the query heads of their group (host arithmetic only).
+
+    A dK/dV workgroup sweeps all ``rep = heads / kv_heads`` query heads over every query after its
+    key block: for the first blocks of a long sequence that is far more than a CU's share of the
+    launch (a lone 4 096-token sequence at 28 / 4 heads: its first workgroup alone runs as long as
+    two whole sequences, profiles/r02_attn_ragged.jsonl).  Work is counted in MFMAs per wave (one
+    wave per SIMD: a workgroup's duration follows it): dK/dV 32 per 32-query tile per query head,
+    dQ 24 per 32-key tile; target = max(the per-SIMD average, the largest dQ workgroup).  A plan
+    with part cap c cuts the key blocks whose workgroup exceeds 1.2 x (c x target) into
+    min(rep, ceil(work / (c x target))) contiguous head ranges.  The caps of SPLIT_CAPS are priced
+    by _makespan (a list schedule of the launch with measured per-tile costs); the cheapest is
+    taken if it beats the unsplit launch by SPLIT_MARGIN (the parts' fp32 partials and the reduce
+    are not free: on 4 x 2048-token packings splitting measured slower, profiles/r03_attn_cap_sweep.jsonl).
+
+    Returns (kv_rows, split_units, split_groups, slots): the unsplit (seq_start, seq_end,
+    block_start) rows, the 7-tuples and 5-tuples of prl_attn_bwd_split, and the partial slots."""
+    rep = heads // kv_heads
+    rows = [(a, b, x) for a, b in zip(bounds[:-1], bounds[1:]) for x in range(a, b, BLOCK)]
+    w_kv = {r: rep * 32 * -(-(r[1] - r[2]) // 32) for r in rows}
+    w_q = [24 * -(-(min(r[2] + BLOCK, r[1]) - r[0]) // 32) for r in rows]
+    total = 4 * (kv_heads * sum(w_kv.values()) + heads * sum(w_q))
+    target = max(total / (4 * max(1, cus)), max(w_q, default=0), 1)
+    if SPLIT_CAP_FRAC is not None:
+        return _plan(rows, w_kv, rep, kv_heads, max(1, int(SPLIT_CAP_FRAC * target)))
+    best = _plan(rows, w_kv, rep, kv_heads, None)
+    if rep < 2:
+        return best
+    t_one = _makespan(rows, best[0], best[1], best[3], heads, kv_heads, cus)
+    t_best = t_one
+    for c in SPLIT_CAPS:
+        plan = _plan(rows, w_kv, rep, kv_heads, max(1, int(c * target)))
+        if not plan[1]:
+            continue
+        t = _makespan(rows, plan[0], plan[1], plan[3], heads, kv_heads, cus)
+        if t < t_best and t < (1 - SPLIT_MARGIN) * t_one:
+            best, t_best = plan, t
+    return best
 
 
 def _split_items(bounds: list[int], heads: int, kv_heads: int, device) -> tuple:

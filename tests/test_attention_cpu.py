@@ -66,7 +66,7 @@ def test_split_plan_covers_every_block_once():
     """split_plan (host side of prl_attn_bwd_split): every (key block, kv head) is computed exactly
     once — unsplit, or as parts whose query-head ranges tile the group in order — the slots are
     0..n-1, groups point at their parts, heavy blocks of a lone sequence are split and a packing
-    of many equal sequences is not (below the 1.2 x target threshold)."""
+    of many equal sequences is not (the modelled launch is no faster split)."""
     from pipelinerl_amd.finetune.attention import BLOCK, split_plan
 
     for bounds, heads, kv in (([0, 4096], 28, 4), ([0, 6122], 12, 2), ([0, 3000, 3400, 3500], 28, 4),
@@ -91,3 +91,26 @@ def test_split_plan_covers_every_block_once():
             assert units
         if bounds == [0, 8192, 16384]:
             assert not units
+
+
+def test_split_plan_is_priced_by_the_launch_model():
+    """The chosen plan's modelled makespan (list schedule of the fused launch + the partial reduce)
+    is never above the unsplit launch's, and the fixed part cap of round 2 (PRL_ATTN_SPLIT_CAP=1.0)
+    is still available."""
+    from pipelinerl_amd.finetune import attention as A
+
+    for lens, heads, kv in (([8511], 28, 4), ([3755, 1617, 6053], 28, 4), ([2048] * 4, 28, 4),
+                            ([2048] * 32, 12, 2), ([6122], 12, 2), ([1, 700, 2200, 200], 14, 2)):
+        bounds = [sum(lens[:i]) for i in range(len(lens) + 1)]
+        rows = [(a, b, x) for a, b in zip(bounds[:-1], bounds[1:]) for x in range(a, b, A.BLOCK)]
+        kv_rows, units, groups, slots = A.split_plan(bounds, heads, kv, 256)
+        t = A._makespan(rows, kv_rows, units, slots, heads, kv, 256)
+        t_one = A._makespan(rows, rows, [], 0, heads, kv, 256)
+        assert t <= t_one and (not units or t < (1 - A.SPLIT_MARGIN) * t_one)
+    saved = A.SPLIT_CAP_FRAC
+    try:
+        A.SPLIT_CAP_FRAC = 1.0
+        assert not A.split_plan([0, 8511], 28, 4, 256)[1]  # below 1.2 x target: unsplit under the old rule
+    finally:
+        A.SPLIT_CAP_FRAC = saved
+    assert A.split_plan([0, 8511], 28, 4, 256)[1]  # the model splits it (2.32 -> 2.09 ms measured)
