@@ -144,6 +144,47 @@ __device__ __forceinline__ void interleave() {
     if (NVALU) SGB(kSgValu, NVALU);
   }
 }
+#ifndef PRL_ATTN_CLOCK_PROBE
+#define PRL_ATTN_CLOCK_PROBE 0  // diagnostic builds only (tools/build_variants.py attn_clock): per-workgroup clock stamps
+#endif
+#if PRL_ATTN_CLOCK_PROBE
+// (shader clock, 100 MHz real time) at a workgroup's start and end, and wave 0's shader cycles per
+// phase of the stage loop, into buffers of their own that nothing else reads (MI355X_MICROARCH.md,
+// DVFS item 6); read by prl_attn_clock_read (tools/attn_clock.py)
+constexpr int kClockSlots = 1 << 16;
+__device__ unsigned long long g_clock[4 * kClockSlots];
+__device__ unsigned long long g_phase[8 * kClockSlots];
+__device__ __forceinline__ void clock_stamp(int b, unsigned long long t0, unsigned long long r0) {
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0 && b < kClockSlots) {
+    g_clock[4 * b] = t0;
+    g_clock[4 * b + 1] = r0;
+    g_clock[4 * b + 2] = t1;
+    g_clock[4 * b + 3] = r1;
+  }
+}
+// phases: 0 first barrier (waiting for the other waves), 1 LDS stage store + second barrier
+// (incl. the wait for the stage's global loads), 2 issuing the next stage's loads, 3 paired
+// tiles, 4 single (masked) tiles, 5 stages
+struct PhaseClock {
+  unsigned long long acc[6] = {0, 0, 0, 0, 0, 0};
+  unsigned long long t = 0;
+  __device__ __forceinline__ void start() { t = __builtin_amdgcn_s_memtime(); }
+  __device__ __forceinline__ void lap(int i) {
+    const unsigned long long n = __builtin_amdgcn_s_memtime();
+    acc[i] += n - t;
+    t = n;
+  }
+  __device__ __forceinline__ void store() const {
+    const int b = blockIdx.x;
+    if (threadIdx.x == 0 && b < kClockSlots)
+      for (int i = 0; i < 6; ++i) g_phase[8 * b + i] = acc[i];
+  }
+};
+#define PROBE(x) x
+#else
+#define PROBE(x)
+#endif
 // ---- dK / dV role: 32-query tiles against the wave's 32 keys (key on the lane) ----
 __device__ __forceinline__ bool dkdv_live(int kw, int q0, int s1) {  // wave-uniform
   return !(kw >= s1 || kw > q0 + TILE - 1 || q0 >= s1);
@@ -294,6 +335,7 @@ __device__ __forceinline__ void attn_bwd_dkdv(const __bf16* __restrict__ q, cons
     dKt[i] = f32x16{};
     dVt[i] = f32x16{};
   }
+  PROBE(PhaseClock pc);
 #pragma unroll 1
   for (int h = h0; h < h1; ++h) {
   StageT<BSTAGE> nq = stage_load<BSTAGE>(q, rsq, h, kb, s1, tid), nd = stage_load<BSTAGE>(dout, rsq, h, kb, s1, tid);
@@ -303,7 +345,9 @@ __device__ __forceinline__ void attn_bwd_dkdv(const __bf16* __restrict__ q, cons
     ndl = delta[(int64_t)h * T + kb + tid];
   }
   for (int q00 = kb; q00 < s1; q00 += BSTAGE) {
+    PROBE(pc.start(); pc.acc[5]++);
     __syncthreads();  // every wave is done with the previous stage
+    PROBE(pc.lap(0));
     stage_store(nq, sQ, tid);
     stage_store(nd, sdO, tid);
     if (tid < BSTAGE) {
@@ -311,6 +355,7 @@ __device__ __forceinline__ void attn_bwd_dkdv(const __bf16* __restrict__ q, cons
       sDl[tid] = ndl;
     }
     __syncthreads();
+    PROBE(pc.lap(1));
     const int qn = q00 + BSTAGE;  // prefetch the next stage behind this stage's MFMAs
     if (qn < s1 && !PRL_ATTN_EXP_NOLOAD) {
       nq = stage_load<BSTAGE>(q, rsq, h, qn, s1, tid);
@@ -320,8 +365,10 @@ __device__ __forceinline__ void attn_bwd_dkdv(const __bf16* __restrict__ q, cons
         ndl = delta[(int64_t)h * T + qn + tid];
       }
     }
+    PROBE(pc.lap(2));
     if (PRL_ATTN_INTERLEAVE && BSTAGE == 2 * TILE && kw < s1 && q00 >= kw + TILE - 1 && q00 + TILE < s1) {  // wave-uniform
       dkdv_pair(sQ, sdO, sL, sDl, kf, vf, key, kval, s1, lane, c2, dKt, dVt);
+      PROBE(pc.lap(3));
       continue;
     }
 #pragma unroll 1
@@ -331,8 +378,10 @@ __device__ __forceinline__ void attn_bwd_dkdv(const __bf16* __restrict__ q, cons
       dkdv_tile(sQ + half * TILE * 256, sdO + half * TILE * 256, sL + half * TILE, sDl + half * TILE, q0, kf, vf, key,
                 kval, s1, lane, c2, dKt, dVt);
     }
+    PROBE(pc.lap(4));
   }
   }
+  PROBE(pc.store());
   if (!kval) return;
   if (part) {
     float* pk = part + (int64_t)(key - kb) * D;
@@ -478,17 +527,23 @@ __device__ __forceinline__ void attn_bwd_dq(const __bf16* __restrict__ q, const 
   for (int i = 0; i < 4; ++i) dQt[i] = f32x16{};
   const int kend = (qb + 128 < s1 ? qb + 128 : s1);  // causal: keys <= the block's last query
   StageT<BSTAGE> nk = stage_load<BSTAGE>(k, rsk, g, s0, s1, tid), nv = stage_load<BSTAGE>(v, rsk, g, s0, s1, tid);
+  PROBE(PhaseClock pc);
   for (int k00 = s0; k00 < kend; k00 += BSTAGE) {
+    PROBE(pc.start(); pc.acc[5]++);
     __syncthreads();
+    PROBE(pc.lap(0));
     stage_store(nk, sK, tid);
     stage_store(nv, sV, tid);
     __syncthreads();
+    PROBE(pc.lap(1));
     if (k00 + BSTAGE < kend && !PRL_ATTN_EXP_NOLOAD) {
       nk = stage_load<BSTAGE>(k, rsk, g, k00 + BSTAGE, s1, tid);
       nv = stage_load<BSTAGE>(v, rsk, g, k00 + BSTAGE, s1, tid);
     }
+    PROBE(pc.lap(2));
     if (PRL_ATTN_INTERLEAVE && BSTAGE == 2 * TILE && qw < s1 && k00 + BSTAGE - 1 <= qw && k00 + BSTAGE <= s1) {  // wave-uniform
       dq_pair(sK, sV, qf, of, qq, qval, s1, lane, c2, lq, dq_delta, dQt);
+      PROBE(pc.lap(3));
       continue;
     }
 #pragma unroll 1
@@ -497,7 +552,9 @@ __device__ __forceinline__ void attn_bwd_dq(const __bf16* __restrict__ q, const 
       if (!dq_live(qw, k0, s1, kend)) continue;  // wave-uniform
       dq_tile(sK + half * TILE * 256, sV + half * TILE * 256, k0, qf, of, qq, qval, s1, lane, c2, lq, dq_delta, dQt);
     }
+    PROBE(pc.lap(4));
   }
+  PROBE(pc.store());
   if (!qval) return;
   __bf16* dqr = dq + (int64_t)qq * rs + h * D;
 #pragma unroll
@@ -555,6 +612,9 @@ __global__ __launch_bounds__(256, PRL_ATTN_BWD_MINB) void attn_bwd_fused(const _
 #endif
   const int b = blockIdx.x;
   const int rep = H / Hkv;
+#if PRL_ATTN_CLOCK_PROBE
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+#endif
   if (b < n_split) {
     const int32_t* u = split_units + 7 * b;
     attn_bwd_dkdv(q, k, v, dout, lse2, delta, u[1], u[2], u[4], u[5], dk, dv, parts + (int64_t)u[6] * 2 * 128 * D, T,
@@ -568,6 +628,9 @@ __global__ __launch_bounds__(256, PRL_ATTN_BWD_MINB) void attn_bwd_fused(const _
     const int lq = xcd_group_remap(b - nd, (int)gridDim.x - nd, rep);
     attn_bwd_dq(q, k, v, dout, lse2, delta, q_items, dq, T, H, Hkv, c2, scale, lq / H, lq % H, s0, s1, sKV);
   }
+#if PRL_ATTN_CLOCK_PROBE
+  clock_stamp(b, t0, r0);
+#endif
 }
 
 // dK / dV of split key blocks: the parts' fp32 partials summed in part order (deterministic),
@@ -864,5 +927,19 @@ int prl_attn_bwd_split(const void* q, const void* k, const void* v, const void* 
   return attn_bwd_launch(q, k, v, dout, lse2, delta, kv_items, n_kv_items, q_items, n_q_items, split_units, n_split,
                          split_groups, n_groups, parts, dq, dk, dv, tokens, heads, kv_heads, head_dim, scale, stream);
 }
+
+#if PRL_ATTN_CLOCK_PROBE
+// diagnostic builds only: the stamps of the last attn_bwd_fused launch, 4 x n u64
+int prl_attn_clock_read(unsigned long long* host, int32_t n) {
+  if (!host || n < 0 || n > kClockSlots) return PRL_E_INVALID;
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_clock), sizeof(unsigned long long) * 4 * (size_t)n, 0,
+                                  hipMemcpyDeviceToHost);
+}
+int prl_attn_phase_read(unsigned long long* host, int32_t n) {
+  if (!host || n < 0 || n > kClockSlots) return PRL_E_INVALID;
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * 8 * (size_t)n, 0,
+                                  hipMemcpyDeviceToHost);
+}
+#endif
 
 }  // extern "C"
