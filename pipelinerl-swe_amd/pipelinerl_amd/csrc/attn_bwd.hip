@@ -108,6 +108,43 @@ __device__ __forceinline__ void stage_store(const StageT<ROWS>& st, char* base, 
   }
 }
 
+#ifndef PRL_ATTN_BUF_STAGE
+#define PRL_ATTN_BUF_STAGE 1  // 0: the flat per-row-tested stage loads (A/B, tools/build_variants.py attn_flat_stage)
+#endif
+// The same stage through buffer loads: a wave-uniform descriptor over rows [r0, r1) of the tensor
+// (base at row r0, r1 - r0 rows of rs elements), so rows past the sequence end fall outside it and
+// read 0 with no per-row test, and the per-thread offsets are computed once per head (vbase = the
+// thread's first chunk: row tid / 16, head h, 16-B chunk tid % 16; chunk j is 16 j rows further).
+// The flat form's 64-bit address arithmetic and per-row branches took 15-19 % of the backward's
+// cycles (tools/attn_clock.py); this form issues 8 loads and ~15 scalar instructions per stage and
+// runs the backward 3-7 % and the forward 3-6 % faster (profiles/r03_attn_buf_stage_ab.jsonl).
+// Spreading the 8 loads over the paired tiles' MFMAs instead of one burst after the barrier was
+// measured no faster (same file): the issue cycles moved into the tiles.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const __bf16* X, int64_t rs, int r0, int r1) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(X + (int64_t)r0 * rs), 0,
+                                           (int)((int64_t)(r1 > r0 ? r1 - r0 : 0) * rs * 2), 0x00020000);
+}
+__device__ __forceinline__ int stage_vbase(int64_t rs, int h, int tid) {
+  return (tid >> 4) * (int)(rs * 2) + h * D * 2 + (tid & 15) * 16;
+}
+template <int ROWS = STAGE>
+__device__ __forceinline__ StageT<ROWS> stage_load_rows(const __bf16* __restrict__ X, int64_t rs, int h, int r0,
+                                                        int r1, int tid, int vbase) {
+#if PRL_ATTN_BUF_STAGE
+  (void)h;
+  (void)tid;
+  const __amdgpu_buffer_rsrc_t rsrc = rows_rsrc(X, rs, r0, r1);
+  StageT<ROWS> st;
+#pragma unroll
+  for (int j = 0; j < ROWS * 16 / 256; ++j)
+    st.x[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, vbase + j * 16 * (int)(rs * 2), 0, 0));
+  return st;
+#else
+  (void)vbase;
+  return stage_load<ROWS>(X, rs, h, r0, r1, tid);
+#endif
+}
+
 #ifndef PRL_ATTN_EXP_NOLOAD
 #define PRL_ATTN_EXP_NOLOAD 0  // timing experiment only (wrong results): backward stages after the first not loaded
 #endif
@@ -338,7 +375,9 @@ __device__ __forceinline__ void attn_bwd_dkdv(const __bf16* __restrict__ q, cons
   PROBE(PhaseClock pc);
 #pragma unroll 1
   for (int h = h0; h < h1; ++h) {
-  StageT<BSTAGE> nq = stage_load<BSTAGE>(q, rsq, h, kb, s1, tid), nd = stage_load<BSTAGE>(dout, rsq, h, kb, s1, tid);
+  const int vb = stage_vbase(rsq, h, tid);
+  StageT<BSTAGE> nq = stage_load_rows<BSTAGE>(q, rsq, h, kb, s1, tid, vb),
+                 nd = stage_load_rows<BSTAGE>(dout, rsq, h, kb, s1, tid, vb);
   float nl = 0.f, ndl = 0.f;
   if (tid < BSTAGE && kb + tid < s1) {
     nl = lse2[(int64_t)h * T + kb + tid];
@@ -358,8 +397,8 @@ __device__ __forceinline__ void attn_bwd_dkdv(const __bf16* __restrict__ q, cons
     PROBE(pc.lap(1));
     const int qn = q00 + BSTAGE;  // prefetch the next stage behind this stage's MFMAs
     if (qn < s1 && !PRL_ATTN_EXP_NOLOAD) {
-      nq = stage_load<BSTAGE>(q, rsq, h, qn, s1, tid);
-      nd = stage_load<BSTAGE>(dout, rsq, h, qn, s1, tid);
+      nq = stage_load_rows<BSTAGE>(q, rsq, h, qn, s1, tid, vb);
+      nd = stage_load_rows<BSTAGE>(dout, rsq, h, qn, s1, tid, vb);
       if (tid < BSTAGE && qn + tid < s1) {
         nl = lse2[(int64_t)h * T + qn + tid];
         ndl = delta[(int64_t)h * T + qn + tid];
@@ -526,7 +565,9 @@ __device__ __forceinline__ void attn_bwd_dq(const __bf16* __restrict__ q, const 
 #pragma unroll
   for (int i = 0; i < 4; ++i) dQt[i] = f32x16{};
   const int kend = (qb + 128 < s1 ? qb + 128 : s1);  // causal: keys <= the block's last query
-  StageT<BSTAGE> nk = stage_load<BSTAGE>(k, rsk, g, s0, s1, tid), nv = stage_load<BSTAGE>(v, rsk, g, s0, s1, tid);
+  const int vb = stage_vbase(rsk, g, tid);
+  StageT<BSTAGE> nk = stage_load_rows<BSTAGE>(k, rsk, g, s0, s1, tid, vb),
+                 nv = stage_load_rows<BSTAGE>(v, rsk, g, s0, s1, tid, vb);
   PROBE(PhaseClock pc);
   for (int k00 = s0; k00 < kend; k00 += BSTAGE) {
     PROBE(pc.start(); pc.acc[5]++);
@@ -537,8 +578,8 @@ __device__ __forceinline__ void attn_bwd_dq(const __bf16* __restrict__ q, const 
     __syncthreads();
     PROBE(pc.lap(1));
     if (k00 + BSTAGE < kend && !PRL_ATTN_EXP_NOLOAD) {
-      nk = stage_load<BSTAGE>(k, rsk, g, k00 + BSTAGE, s1, tid);
-      nv = stage_load<BSTAGE>(v, rsk, g, k00 + BSTAGE, s1, tid);
+      nk = stage_load_rows<BSTAGE>(k, rsk, g, k00 + BSTAGE, s1, tid, vb);
+      nv = stage_load_rows<BSTAGE>(v, rsk, g, k00 + BSTAGE, s1, tid, vb);
     }
     PROBE(pc.lap(2));
     if (PRL_ATTN_INTERLEAVE && BSTAGE == 2 * TILE && qw < s1 && k00 + BSTAGE - 1 <= qw && k00 + BSTAGE <= s1) {  // wave-uniform
@@ -743,15 +784,16 @@ __global__ __launch_bounds__(256, PRL_ATTN_FWD_MINB) void attn_fwd(const __bf16*
   for (int i = 0; i < 4; ++i) Ot[i] = f32x16{};
   float m = -1e30f, l = 0.f;  // running max (base-2 units) and sum for query qq
   const int kend = (qb + 128 < s1 ? qb + 128 : s1);
-  Stage nk = stage_load(k, rsk, g, s0, s1, tid), nv = stage_load(v, rsk, g, s0, s1, tid);
+  const int vb = stage_vbase(rsk, g, tid);
+  Stage nk = stage_load_rows(k, rsk, g, s0, s1, tid, vb), nv = stage_load_rows(v, rsk, g, s0, s1, tid, vb);
   for (int k00 = s0; k00 < kend; k00 += STAGE) {
     __syncthreads();
     stage_store(nk, sK, tid);
     stage_store(nv, sV, tid);
     __syncthreads();
     if (k00 + STAGE < kend) {
-      nk = stage_load(k, rsk, g, k00 + STAGE, s1, tid);
-      nv = stage_load(v, rsk, g, k00 + STAGE, s1, tid);
+      nk = stage_load_rows(k, rsk, g, k00 + STAGE, s1, tid, vb);
+      nv = stage_load_rows(v, rsk, g, k00 + STAGE, s1, tid, vb);
     }
 #pragma unroll 1
     for (int half = 0; half < STAGE / TILE; ++half) {

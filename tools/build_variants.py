@@ -38,6 +38,7 @@ VARIANTS = {
     "norm_regacc": {"PRL_NORM_BWD_LDS": "0"},
     "norm_lds768": {"PRL_NORM_LDS_GRID": "768"},
     "attn_clock": {"PRL_ATTN_CLOCK_PROBE": "1"},
+    "attn_flat_stage": {"PRL_ATTN_BUF_STAGE": "0"},
     "swiglu_gridstride": {"PRL_SWIGLU_PHASED": "0"},
     "swiglu_phased_wg2": {"PRL_SWIGLU_PHASED": "1", "PRL_SWIGLU_PHASED_WG": "2"},
     "swiglu_rows_phased": {"PRL_SWIGLU_ROWS_PHASED": "1"},
