@@ -24,6 +24,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <utility>
+
 #include "prl_hip.h"
 
 namespace prl_attn {
@@ -181,6 +183,19 @@ __device__ __forceinline__ void interleave() {
     if (NVALU) SGB(kSgValu, NVALU);
   }
 }
+// a pipeline segment (dkdv_pipeline): the half softmax's 4 L / delta reads and the first PRL_ATTN_LEAD
+// operand reads, then NMFMA groups of (1 MFMA, its NREAD operand reads, NVALU vector instructions)
+template <int NMFMA, int NREAD, int NVALU>
+__device__ __forceinline__ void interleave_seg() {
+  constexpr int kLead = PRL_ATTN_LEAD < NMFMA ? PRL_ATTN_LEAD : NMFMA;
+  SGB(kSgDsRead, 4 + NREAD * kLead);
+#pragma unroll
+  for (int i = 0; i < NMFMA; ++i) {
+    SGB(kSgMfma, 1);
+    if (i + kLead < NMFMA) SGB(kSgDsRead, NREAD);
+    SGB(kSgValu, NVALU);
+  }
+}
 #ifndef PRL_ATTN_CLOCK_PROBE
 #define PRL_ATTN_CLOCK_PROBE 0  // diagnostic builds only (tools/build_variants.py attn_clock): per-workgroup clock stamps
 #endif
@@ -203,24 +218,45 @@ __device__ __forceinline__ void clock_stamp(int b, unsigned long long t0, unsign
 // phases: 0 first barrier (waiting for the other waves), 1 LDS stage store + second barrier
 // (incl. the wait for the stage's global loads), 2 issuing the next stage's loads, 3 paired
 // tiles, 4 single (masked) tiles, 5 stages
+// and, inside the paired tiles, wave 0's cycles per region of the pair schedule (regions 0-3 in
+// the order of dkdv_pair / dq_pair; slot 4 counts the pairs)
+__device__ unsigned long long g_pair[8 * kClockSlots];
 struct PhaseClock {
   unsigned long long acc[6] = {0, 0, 0, 0, 0, 0};
-  unsigned long long t = 0;
+  unsigned long long pr[5] = {0, 0, 0, 0, 0};
+  unsigned long long t = 0, tp = 0;
   __device__ __forceinline__ void start() { t = __builtin_amdgcn_s_memtime(); }
   __device__ __forceinline__ void lap(int i) {
     const unsigned long long n = __builtin_amdgcn_s_memtime();
     acc[i] += n - t;
     t = n;
   }
+  __device__ __forceinline__ void pair_start() {
+    tp = __builtin_amdgcn_s_memtime();
+    pr[4]++;
+  }
+  __device__ __forceinline__ void pair_lap(int i) {
+    const unsigned long long n = __builtin_amdgcn_s_memtime();
+    pr[i] += n - tp;
+    tp = n;
+  }
   __device__ __forceinline__ void store() const {
     const int b = blockIdx.x;
-    if (threadIdx.x == 0 && b < kClockSlots)
+    if (threadIdx.x == 0 && b < kClockSlots) {
       for (int i = 0; i < 6; ++i) g_phase[8 * b + i] = acc[i];
+      for (int i = 0; i < 5; ++i) g_pair[8 * b + i] = pr[i];
+    }
   }
 };
 #define PROBE(x) x
+#define PAIR_CLOCK_ARG , PhaseClock& pcl
+#define PAIR_CLOCK_PASS , pc
+#define PAIR_LAP(x) pcl.x
 #else
 #define PROBE(x)
+#define PAIR_CLOCK_ARG
+#define PAIR_CLOCK_PASS
+#define PAIR_LAP(x)
 #endif
 // ---- dK / dV role: 32-query tiles against the wave's 32 keys (key on the lane) ----
 __device__ __forceinline__ bool dkdv_live(int kw, int q0, int s1) {  // wave-uniform
@@ -272,6 +308,25 @@ __device__ __forceinline__ void dkdv_probs(const f32x16& S, const f32x16& dP, co
     }
   }
 }
+// the unmasked softmax of one half of the tile's 16 accumulator rows (HALF 0: rows 0-7 -> pb[0] / sb[0],
+// HALF 1: rows 8-15 -> pb[1] / sb[1]); the same arithmetic as dkdv_probs<false>, so the two halves
+// together give its results bit for bit
+template <int HALF>
+__device__ __forceinline__ void dkdv_probs_half(const f32x16& S, const f32x16& dP, const float* tL, const float* tDl,
+                                                int hi, float c2, bf16x8* pb, bf16x8* sb) {
+#pragma unroll
+  for (int gg = 2 * HALF; gg < 2 * HALF + 2; ++gg) {
+    const f32x4 Lr = *reinterpret_cast<const f32x4*>(tL + 8 * gg + 4 * hi);
+    const f32x4 Dr = *reinterpret_cast<const f32x4*>(tDl + 8 * gg + 4 * hi);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = 4 * gg + j;
+      const float p = bexp2(__builtin_fmaf(S[r], c2, -Lr[j]));
+      pb[r >> 3][r & 7] = (__bf16)p;
+      sb[r >> 3][r & 7] = (__bf16)(p * (dP[r] - Dr[j]));
+    }
+  }
+}
 // dV^T += dO^T P, dK^T += Q^T dS (unscaled)
 __device__ __forceinline__ void dkdv_acc(const char* tQ, const char* tdO, int lane, const bf16x8* pb, const bf16x8* sb,
                                          f32x16* dKt, f32x16* dVt) {
@@ -299,22 +354,215 @@ __device__ __forceinline__ void dkdv_tile(const char* tQ, const char* tdO, const
 template <typename KR, typename VR>
 __device__ __forceinline__ void dkdv_pair(const char* tQ, const char* tdO, const float* tL, const float* tDl,
                                           KR kf, VR vf, int key, bool kval, int s1, int lane,
-                                          float c2, f32x16* dKt, f32x16* dVt) {
+                                          float c2, f32x16* dKt, f32x16* dVt PAIR_CLOCK_ARG) {
   const int hi = lane >> 5, l32 = lane & 31;
   const char *tQb = tQ + TILE * 256, *tdOb = tdO + TILE * 256;
   f32x16 Sa = f32x16{}, dPa = f32x16{}, Sb = f32x16{}, dPb = f32x16{};
   bf16x8 pa[2], sa[2], pb[2], sb[2];
+  PAIR_LAP(pair_start());
   dkdv_scores(tQ, tdO, kf, vf, l32, hi, Sa, dPa);
   sched_fence();
+  PAIR_LAP(pair_lap(0));
   dkdv_scores(tQb, tdOb, kf, vf, l32, hi, Sb, dPb);
   dkdv_probs<false>(Sa, dPa, tL, tDl, 0, key, kval, s1, hi, c2, pa, sa);
   interleave<16, 1, 8>();
   sched_fence();
+  PAIR_LAP(pair_lap(1));
   dkdv_acc(tQ, tdO, lane, pa, sa, dKt, dVt);
   dkdv_probs<false>(Sb, dPb, tL + TILE, tDl + TILE, 0, key, kval, s1, hi, c2, pb, sb);
   interleave<16, 2, 8>();
   sched_fence();
+  PAIR_LAP(pair_lap(2));
   dkdv_acc(tQb, tdOb, lane, pb, sb, dKt, dVt);
+  PROBE(sched_fence());
+  PAIR_LAP(pair_lap(3));
+}
+
+#ifndef PRL_ATTN_PIPE
+#define PRL_ATTN_PIPE 0  // 1: the dK/dV tile pipeline below (A/B, tools/build_variants.py attn_pipe); 0: the two-barrier pair loop
+#endif
+// The dK/dV role past the diagonal as one software pipeline over its 32-query tiles.  The pair loop
+// above puts a tile's whole softmax (~110 vector instructions) under the 16 MFMAs of the next
+// tile's S / dP, and both tiles' softmaxes under half of the pair's 64 MFMAs: those regions ran at
+// 76-79 cycles per MFMA against 38-42 for the MFMA-only ones (tools/attn_clock.py, pair regions).
+// Here the MFMA stream is S/dP(t), dV/dK += (t-1), S/dP(t+1), dV/dK += t, ... and the softmax of
+// tile t is split by accumulator rows into two halves, one under dV/dK += (t-1) and one under
+// S/dP(t+1): every 16-MFMA segment carries half a softmax.  Tile t's stage must stay in LDS until
+// dV/dK += t, which runs after the next stage's first tile, so stages rotate over three LDS slots
+// and each stage needs one barrier: stage i+1 is stored (from the registers its loads filled one
+// stage earlier) right after stage i's barrier, into the slot stage i-2 used, which every wave left
+// before that barrier.  The accumulation order of dK^T / dV^T is the tile order, as in the pair
+// loop, so results are bit-identical to it.
+constexpr int kSlot = 2 * STAGE * D * 2 + 2 * STAGE * 4;  // Q image, dO image, L2, delta of one 64-row stage
+__device__ __forceinline__ void pipe_store(const StageT<BSTAGE>& nq, const StageT<BSTAGE>& nd, float nl, float ndl,
+                                           char* slot, int tid) {
+  stage_store(nq, slot, tid);
+  stage_store(nd, slot + STAGE * 256, tid);
+  if (tid < BSTAGE) {
+    float* f = reinterpret_cast<float*>(slot + 2 * STAGE * 256);
+    f[tid] = nl;
+    f[STAGE + tid] = ndl;
+  }
+}
+__device__ __forceinline__ const float* slot_L(const char* slot) {
+  return reinterpret_cast<const float*>(slot + 2 * STAGE * 256);
+}
+__device__ __forceinline__ const float* slot_D(const char* slot) { return slot_L(slot) + STAGE; }
+// one 64-row stage of Q and dO (query head h, rows r0 .. r0 + 63) and its L2 / delta into an LDS slot by
+// LDS-DMA: wave w fills rows 16w .. 16w + 15 of each image, 4 rows (1 KiB) per instruction.  The DMA
+// writes lane-linearly (lane l -> byte 16 l of the instruction's 1 KiB), so the XOR swizzle of toff is
+// applied on the source side: lane l reads chunk (l & 15) ^ swz(row) of its row.  Rows past the
+// sequence end fall outside the buffer descriptors and land as zeros.  Waves 0 and 1 also fetch the
+// 64 L2 / delta values (4 B per lane).  Completion: the __syncthreads that starts the stage's item.
+typedef __attribute__((address_space(3))) void lds_void;
+__device__ __forceinline__ void stage_dma(const __bf16* __restrict__ q, const __bf16* __restrict__ dout,
+                                          const float* __restrict__ lse2, const float* __restrict__ delta, int64_t rs,
+                                          int64_t T, int h, int r0, int s1, char* slot, int w, int lane) {
+  const __amdgpu_buffer_rsrc_t rq = rows_rsrc(q, rs, r0, s1), ro = rows_rsrc(dout, rs, r0, s1);
+  const int p = lane & 15;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int r = 16 * w + 4 * j + (lane >> 4);
+    const int c = p ^ (((r & 3) << 2) | ((r >> 2) & 3));
+    const int voff = r * (int)(rs * 2) + h * D * 2 + c * 16;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rq, (lds_void*)(slot + 1024 * (4 * w + j)), 16, voff, 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(ro, (lds_void*)(slot + STAGE * 256 + 1024 * (4 * w + j)), 16, voff, 0, 0,
+                                             0);
+  }
+  if (w < 2) {  // wave-uniform
+    const float* src = (w == 0 ? lse2 : delta) + h * T + r0;
+    const int nb = (s1 - r0 < STAGE ? s1 - r0 : STAGE) * 4;
+    const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), 0, nb, 0x00020000);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rl, (lds_void*)(slot + 2 * STAGE * 256 + w * STAGE * 4), 4, lane * 4, 0, 0,
+                                             0);
+  }
+}
+
+#ifndef PRL_ATTN_PIPE_SCHED
+#define PRL_ATTN_PIPE_SCHED 1  // 0: the pipeline's segments scheduled by sched_group_barrier patterns (A/B)
+#endif
+#ifndef PRL_ATTN_PIPE_LEAD
+#define PRL_ATTN_PIPE_LEAD 4  // MFMA operands read this many MFMAs ahead in the explicit schedule
+#endif
+// One pipelined stage (64 MFMAs) with every instruction placed by hand: gap g = MFMA g, the LDS
+// reads of MFMA g + LEAD's operand and gap g's share of a softmax half, then a scheduling fence, so
+// the compiler keeps the order (the sched_group_barrier patterns above left the vector work in
+// clumps).  Segments of 16 gaps: S/dP(a) | dV/dK += previous b | S/dP(b) | dV/dK += a, carrying the
+// softmax halves: previous b rows 8-15 | a rows 0-7 | a rows 8-15 | b rows 0-7.  In a segment, local
+// gap t = 0 reads the half's L2 / delta rows, t = 2..9 forms p = 2^(c2 S - L2) of element t - 2 and
+// t = 8..15 dS = p (dP - delta) of element t - 8, packing element pairs to bf16 (the arithmetic of
+// dkdv_probs).  MFMA operands: S/dP segments: row reads (Q even, dO odd gaps, chunk 2 (t/2) + hi);
+// dV/dK segments: transposed reads of dO (even) / Q (odd), d-chunk t / 4, k-step (t / 2) & 1 -- the
+// order of dkdv_scores / dkdv_acc, so the accumulation order and the results are the pair loop's.
+// PREV = false: the head's first pipelined stage (no previous tile b: no segment-1 vector work, no
+// segment-2 MFMAs).  Every index below is a constant once the gap loop is unrolled.
+struct PipeTile {
+  const char *q, *o;   // the 32-row tile's Q and dO images in LDS
+  const float *L, *D;  // its 32 L2 / delta values
+};
+__device__ __forceinline__ bf16x8 pipe_operand(int g, const PipeTile& pbt, const PipeTile& a, const PipeTile& b,
+                                               int lane) {
+  const int seg = g >> 4, t = g & 15;
+  if (seg == 0 || seg == 2) {
+    const PipeTile& x = seg == 0 ? a : b;
+    return row_read((t & 1) ? x.o : x.q, lane & 31, 2 * (t >> 1) + (lane >> 5));
+  }
+  const PipeTile& y = seg == 1 ? pbt : a;
+  return tr_operand((t & 1) ? y.q : y.o, lane, t >> 2, (t >> 1) & 1);
+}
+template <bool PREV>
+struct PipeIter {
+  static constexpr int LEAD = PRL_ATTN_PIPE_LEAD;
+  static constexpr bool live(int g) { return PREV || (g >> 4) != 1; }  // MFMA g exists
+  const PipeTile &pbt, &a, &b;
+  const bf16x8 *kf, *vf;
+  int lane, hi;
+  float c2;
+  f32x16 &Sa, &dPa, &Sb, &dPb;
+  bf16x8 *pa, *sa, *pb, *sb;
+  f32x16 *dKt, *dVt;
+  bf16x8 ring[LEAD];
+  f32x4 Lr[2], Dr[2];
+  float pv[8];
+
+  template <int G>
+  __device__ __forceinline__ void gap() {
+    constexpr int seg = G >> 4, t = G & 15;
+    // 1. MFMA G
+    if constexpr (live(G)) {
+      const bf16x8 op = ring[G % LEAD];
+      if constexpr (seg == 0 || seg == 2) {
+        f32x16& S = seg == 0 ? Sa : Sb;
+        f32x16& dP = seg == 0 ? dPa : dPb;
+        if constexpr (t == 0) S = mfma(op, kf[0], f32x16{});
+        else if constexpr (t == 1) dP = mfma(op, vf[0], f32x16{});
+        else if constexpr (t & 1) dP = mfma(op, vf[t >> 1], dP);
+        else S = mfma(op, kf[t >> 1], S);
+      } else {
+        const bf16x8* pp = seg == 1 ? pb : pa;
+        const bf16x8* ss = seg == 1 ? sb : sa;
+        constexpr int dc = t >> 2, ks = (t >> 1) & 1;
+        if constexpr (t & 1) dKt[dc] = mfma(op, ss[ks], dKt[dc]);
+        else dVt[dc] = mfma(op, pp[ks], dVt[dc]);
+      }
+    }
+    // 2. the operand of MFMA G + LEAD
+    if constexpr (G + LEAD < 64 && live(G + LEAD)) ring[(G + LEAD) % LEAD] = operand<G + LEAD>();
+    // 3. this gap's share of the segment's softmax half
+    if constexpr (PREV || seg != 0) {
+      const f32x16& S = (seg == 0 || seg == 3) ? Sb : Sa;
+      const f32x16& dP = (seg == 0 || seg == 3) ? dPb : dPa;
+      const PipeTile& st = seg == 0 ? pbt : (seg == 3 ? b : a);
+      constexpr int half = (seg == 0 || seg == 2) ? 1 : 0;
+      bf16x8* pd = (seg == 0 || seg == 3) ? pb : pa;
+      bf16x8* sd = (seg == 0 || seg == 3) ? sb : sa;
+      if constexpr (t == 0) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          Lr[u] = *reinterpret_cast<const f32x4*>(st.L + 8 * (2 * half + u) + 4 * hi);
+          Dr[u] = *reinterpret_cast<const f32x4*>(st.D + 8 * (2 * half + u) + 4 * hi);
+        }
+      }
+      if constexpr (t >= 2 && t < 10) {  // p of element e: accumulator row 8 half + e
+        constexpr int e = t - 2;
+        pv[e] = bexp2(__builtin_fmaf(S[8 * half + e], c2, -Lr[e >> 2][e & 3]));
+      }
+      if constexpr (t >= 8) {  // dS of element e
+        constexpr int e = t - 8;
+        pd[half][e] = (__bf16)pv[e];
+        sd[half][e] = (__bf16)(pv[e] * (dP[8 * half + e] - Dr[e >> 2][e & 3]));
+      }
+    }
+    sched_fence();
+  }
+  template <int G>
+  __device__ __forceinline__ bf16x8 operand() const {
+    constexpr int seg = G >> 4, t = G & 15;
+    if constexpr (seg == 0 || seg == 2) {
+      const PipeTile& x = seg == 0 ? a : b;
+      return row_read((t & 1) ? x.o : x.q, lane & 31, 2 * (t >> 1) + hi);
+    } else {
+      const PipeTile& y = seg == 1 ? pbt : a;
+      return tr_operand((t & 1) ? y.q : y.o, lane, t >> 2, (t >> 1) & 1);
+    }
+  }
+  template <int... G>
+  __device__ __forceinline__ void prime(std::integer_sequence<int, G...>) {
+    ((live(G) ? (void)(ring[G] = operand<G>()) : (void)0), ...);
+  }
+  template <int... G>
+  __device__ __forceinline__ void run(std::integer_sequence<int, G...>) {
+    (gap<G>(), ...);
+  }
+};
+template <bool PREV>
+__device__ __forceinline__ void dkdv_iter(const PipeTile& pbt, const PipeTile& a, const PipeTile& b,
+                                          const bf16x8* kf, const bf16x8* vf, int lane, float c2, f32x16& Sa,
+                                          f32x16& dPa, f32x16& Sb, f32x16& dPb, bf16x8* pa, bf16x8* sa, bf16x8* pb,
+                                          bf16x8* sb, f32x16* dKt, f32x16* dVt) {
+  PipeIter<PREV> it{pbt, a, b, kf, vf, lane, lane >> 5, c2, Sa, dPa, Sb, dPb, pa, sa, pb, sb, dKt, dVt, {}, {}, {}, {}};
+  it.prime(std::make_integer_sequence<int, PipeIter<PREV>::LEAD>{});
+  it.run(std::make_integer_sequence<int, 64>{});
 }
 
 // items: int32 triplets (seq_start, seq_end, block_start), block = 128 keys (dkdv) / queries (dq).
@@ -330,7 +578,7 @@ __device__ __forceinline__ void attn_bwd_dkdv(const __bf16* __restrict__ q, cons
                                               int s1, int kb, int h0, int h1, __bf16* __restrict__ dk,
                                               __bf16* __restrict__ dv, float* __restrict__ part, int64_t T, int H,
                                               int Hkv, float c2, float scale, int g, char* sQ, char* sdO, float* sL,
-                                              float* sDl, char* sKV) {
+                                              float* sDl, char* sKV, char* sPipe) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, w = tid >> 6, hi = lane >> 5, l32 = lane & 31;
   const int64_t rsq = (int64_t)H * D, rsk = (int64_t)Hkv * D;
@@ -373,6 +621,146 @@ __device__ __forceinline__ void attn_bwd_dkdv(const __bf16* __restrict__ q, cons
     dVt[i] = f32x16{};
   }
   PROBE(PhaseClock pc);
+#if PRL_ATTN_PIPE
+  {
+    // the sequence of (query head, 64-row stage) items; item m lands in LDS slot m % 3 by LDS-DMA
+    // issued right after item m - 1's barrier (one stage ahead, no staging registers, no LDS store
+    // pass), and the barrier that starts item m (its __syncthreads waits for the DMA) is the only
+    // one per stage.  Stages 0 and 1 of a head hold the diagonal: the pair / masked-tile code;
+    // stages from 2 on: the pipeline, drained at the head's last stage.
+    const int nst = (s1 - kb + BSTAGE - 1) / BSTAGE;
+    PROBE(PhaseClock& pcl = pc);
+    stage_dma(q, dout, lse2, delta, rsq, T, h0, kb, s1, sPipe, w, lane);
+    int cs = 0;
+    // start item (h, i): wait for it, refill the slot two items back with the next item
+    auto begin_item = [&](int h, int i) -> char* {
+      const int ns = cs == 2 ? 0 : cs + 1;
+      PROBE(pc.start(); pc.acc[5]++);
+      __syncthreads();  // item (h, i) is in slot cs; every wave is done with the slot ns held
+      PROBE(pc.lap(0));
+      const int hn = i + 1 < nst ? h : h + 1, in = i + 1 < nst ? i + 1 : 0;
+      if (hn < h1 && !PRL_ATTN_EXP_NOLOAD)
+        stage_dma(q, dout, lse2, delta, rsq, T, hn, kb + in * BSTAGE, s1, sPipe + ns * kSlot, w, lane);
+      sched_fence();
+      PROBE(pc.lap(2));
+      char* const cur = sPipe + cs * kSlot;
+      cs = ns;
+      return cur;
+    };
+#pragma unroll 1
+    for (int h = h0; h < h1; ++h) {
+#pragma unroll 1
+      for (int i = 0; i < 2 && i < nst; ++i) {  // the diagonal stages
+        const char* const cur = begin_item(h, i);
+        const char *cq = cur, *co = cur + STAGE * 256;
+        const float *cL = slot_L(cur), *cD = slot_D(cur);
+        const int q00 = kb + i * BSTAGE;
+        if (PRL_ATTN_INTERLEAVE && kw < s1 && q00 >= kw + TILE - 1 && q00 + TILE < s1) {  // wave-uniform
+          dkdv_pair(cq, co, cL, cD, kf, vf, key, kval, s1, lane, c2, dKt, dVt PAIR_CLOCK_PASS);
+        } else {
+#pragma unroll 1
+          for (int half = 0; half < BSTAGE / TILE; ++half) {
+            const int q0 = q00 + TILE * half;
+            if (!dkdv_live(kw, q0, s1)) continue;  // wave-uniform
+            dkdv_tile(cq + half * TILE * 256, co + half * TILE * 256, cL + half * TILE, cD + half * TILE, q0, kf, vf,
+                      key, kval, s1, lane, c2, dKt, dVt);
+          }
+        }
+        PROBE(pc.lap(4));
+      }
+      if (nst <= 2) continue;
+      // stages 2 .. nst - 1: every row is past every key of the block (no masks)
+      f32x16 Sa, dPa, Sb, dPb;
+      bf16x8 pa[2], sa[2], pb[2], sb[2];
+#if PRL_ATTN_PIPE_SCHED
+      auto tiles = [](const char* cur, PipeTile& ta, PipeTile& tb) {
+        ta = PipeTile{cur, cur + STAGE * 256, slot_L(cur), slot_D(cur)};
+        tb = PipeTile{cur + TILE * 256, cur + STAGE * 256 + TILE * 256, slot_L(cur) + TILE, slot_D(cur) + TILE};
+      };
+      PipeTile ta, tb, prevb;
+      tiles(begin_item(h, 2), ta, tb);
+      PAIR_LAP(pair_start());
+      dkdv_iter<false>(ta, ta, tb, kf, vf, lane, c2, Sa, dPa, Sb, dPb, pa, sa, pb, sb, dKt, dVt);
+      PAIR_LAP(pair_lap(3));
+      PROBE(pc.lap(3));
+      prevb = tb;
+#pragma unroll 1
+      for (int i = 3; i < nst; ++i) {
+        tiles(begin_item(h, i), ta, tb);
+        PAIR_LAP(pair_start());
+        dkdv_iter<true>(prevb, ta, tb, kf, vf, lane, c2, Sa, dPa, Sb, dPb, pa, sa, pb, sb, dKt, dVt);
+        PAIR_LAP(pair_lap(3));
+        PROBE(pc.lap(3));
+        prevb = tb;
+      }
+      // drain: the head's last tile b
+      dkdv_probs_half<1>(Sb, dPb, prevb.L, prevb.D, hi, c2, pb, sb);
+      sched_fence();
+      dkdv_acc(prevb.q, prevb.o, lane, pb, sb, dKt, dVt);
+      sched_fence();
+#else
+      const char* cur = begin_item(h, 2);
+      const char *cq = cur, *co = cur + STAGE * 256;
+      const float *cL = slot_L(cur), *cD = slot_D(cur);
+      Sa = f32x16{};
+      dPa = f32x16{};
+      dkdv_scores(cq, co, kf, vf, l32, hi, Sa, dPa);
+      sched_fence();
+      dkdv_probs_half<0>(Sa, dPa, cL, cD, hi, c2, pa, sa);
+      sched_fence();
+#pragma unroll 1
+      for (int i = 2;; ++i) {
+        PAIR_LAP(pair_start());
+        if (i > 2) {
+          const char *pq = cq, *po = co;
+          const float *pL = cL, *pD = cD;
+          cur = begin_item(h, i);
+          cq = cur;
+          co = cur + STAGE * 256;
+          cL = slot_L(cur);
+          cD = slot_D(cur);
+          PAIR_LAP(pair_start());
+          // S / dP of tile a | the previous tile b's softmax, rows 8-15
+          dkdv_probs_half<1>(Sb, dPb, pL + TILE, pD + TILE, hi, c2, pb, sb);
+          Sa = f32x16{};
+          dPa = f32x16{};
+          dkdv_scores(cq, co, kf, vf, l32, hi, Sa, dPa);
+          interleave_seg<16, 1, 4>();
+          sched_fence();
+          PAIR_LAP(pair_lap(0));
+          // dV / dK += the previous tile b | tile a's softmax, rows 0-7
+          dkdv_probs_half<0>(Sa, dPa, cL, cD, hi, c2, pa, sa);
+          dkdv_acc(pq + TILE * 256, po + TILE * 256, lane, pb, sb, dKt, dVt);
+          interleave_seg<16, 2, 4>();
+          sched_fence();
+          PAIR_LAP(pair_lap(1));
+        }
+        // S / dP of tile b | tile a's softmax, rows 8-15
+        dkdv_probs_half<1>(Sa, dPa, cL, cD, hi, c2, pa, sa);
+        Sb = f32x16{};
+        dPb = f32x16{};
+        dkdv_scores(cq + TILE * 256, co + TILE * 256, kf, vf, l32, hi, Sb, dPb);
+        interleave_seg<16, 1, 4>();
+        sched_fence();
+        PAIR_LAP(pair_lap(2));
+        // dV / dK += tile a | tile b's softmax, rows 0-7
+        dkdv_probs_half<0>(Sb, dPb, cL + TILE, cD + TILE, hi, c2, pb, sb);
+        dkdv_acc(cq, co, lane, pa, sa, dKt, dVt);
+        interleave_seg<16, 2, 4>();
+        sched_fence();
+        PAIR_LAP(pair_lap(3));
+        PROBE(pc.lap(3));
+        if (i + 1 == nst) break;
+      }
+      // drain: the head's last tile b
+      dkdv_probs_half<1>(Sb, dPb, cL + TILE, cD + TILE, hi, c2, pb, sb);
+      sched_fence();
+      dkdv_acc(cq + TILE * 256, co + TILE * 256, lane, pb, sb, dKt, dVt);
+      sched_fence();
+#endif
+    }
+  }
+#else
 #pragma unroll 1
   for (int h = h0; h < h1; ++h) {
   const int vb = stage_vbase(rsq, h, tid);
@@ -406,7 +794,7 @@ __device__ __forceinline__ void attn_bwd_dkdv(const __bf16* __restrict__ q, cons
     }
     PROBE(pc.lap(2));
     if (PRL_ATTN_INTERLEAVE && BSTAGE == 2 * TILE && kw < s1 && q00 >= kw + TILE - 1 && q00 + TILE < s1) {  // wave-uniform
-      dkdv_pair(sQ, sdO, sL, sDl, kf, vf, key, kval, s1, lane, c2, dKt, dVt);
+      dkdv_pair(sQ, sdO, sL, sDl, kf, vf, key, kval, s1, lane, c2, dKt, dVt PAIR_CLOCK_PASS);
       PROBE(pc.lap(3));
       continue;
     }
@@ -420,6 +808,7 @@ __device__ __forceinline__ void attn_bwd_dkdv(const __bf16* __restrict__ q, cons
     PROBE(pc.lap(4));
   }
   }
+#endif
   PROBE(pc.store());
   if (!kval) return;
   if (part) {
@@ -499,22 +888,29 @@ __device__ __forceinline__ void dq_tile(const char* tK, const char* tV, int k0, 
 // two unmasked tiles, interleaved as in dkdv_pair
 template <typename KR, typename VR>
 __device__ __forceinline__ void dq_pair(const char* tK, const char* tV, KR qf, VR of, int qq,
-                                        bool qval, int s1, int lane, float c2, float lq, float dq_delta, f32x16* dQt) {
+                                        bool qval, int s1, int lane, float c2, float lq, float dq_delta, f32x16* dQt
+                                        PAIR_CLOCK_ARG) {
   const int hi = lane >> 5, l32 = lane & 31;
   const char *tKb = tK + TILE * 256, *tVb = tV + TILE * 256;
   f32x16 Sa = f32x16{}, dPa = f32x16{}, Sb = f32x16{}, dPb = f32x16{};
   bf16x8 sa[2], sb[2];
+  PAIR_LAP(pair_start());
   dq_scores(tK, tV, qf, of, l32, hi, Sa, dPa);
   sched_fence();
+  PAIR_LAP(pair_lap(0));
   dq_scores(tKb, tVb, qf, of, l32, hi, Sb, dPb);
   dq_probs<false>(Sa, dPa, 0, qq, qval, s1, hi, c2, lq, dq_delta, sa);
   interleave<16, 1, 5>();
   sched_fence();
+  PAIR_LAP(pair_lap(1));
   dq_acc(tK, lane, sa, dQt);
   dq_probs<false>(Sb, dPb, 0, qq, qval, s1, hi, c2, lq, dq_delta, sb);
   interleave<8, 2, 10>();
   sched_fence();
+  PAIR_LAP(pair_lap(2));
   dq_acc(tKb, lane, sb, dQt);
+  PROBE(sched_fence());
+  PAIR_LAP(pair_lap(3));
 }
 
 __device__ __forceinline__ void attn_bwd_dq(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
@@ -583,7 +979,7 @@ __device__ __forceinline__ void attn_bwd_dq(const __bf16* __restrict__ q, const 
     }
     PROBE(pc.lap(2));
     if (PRL_ATTN_INTERLEAVE && BSTAGE == 2 * TILE && qw < s1 && k00 + BSTAGE - 1 <= qw && k00 + BSTAGE <= s1) {  // wave-uniform
-      dq_pair(sK, sV, qf, of, qq, qval, s1, lane, c2, lq, dq_delta, dQt);
+      dq_pair(sK, sV, qf, of, qq, qval, s1, lane, c2, lq, dq_delta, dQt PAIR_CLOCK_PASS);
       PROBE(pc.lap(3));
       continue;
     }
@@ -643,8 +1039,19 @@ __global__ __launch_bounds__(256, PRL_ATTN_BWD_MINB) void attn_bwd_fused(const _
                                                       int H, int Hkv, float c2, float scale,
                                                       const int32_t* __restrict__ split_units, int n_split,
                                                       float* __restrict__ parts) {
+#if PRL_ATTN_PIPE
+  // three stage slots for the dK/dV pipeline; slot 2 doubles as the two-barrier loops' stage (the
+  // diagonal stages of dK/dV, every stage of dQ)
+  __shared__ __attribute__((aligned(16))) char sPipe[3 * kSlot];
+  char* const s0 = sPipe + 2 * kSlot;
+  char* const s1 = s0 + STAGE * D * 2;
+  float* const sL = reinterpret_cast<float*>(s0 + 2 * STAGE * D * 2);
+  float* const sDl = sL + STAGE;
+#else
   __shared__ __attribute__((aligned(16))) char s0[STAGE * D * 2], s1[STAGE * D * 2];
   __shared__ __attribute__((aligned(16))) float sL[STAGE], sDl[STAGE];
+  char* const sPipe = nullptr;
+#endif
 #if PRL_ATTN_KV_LDS
   // K and V (mode 2: V) images of the key block; the dQ role's Q and dO (dO)
   __shared__ __attribute__((aligned(16))) char sKV[(PRL_ATTN_KV_LDS == 1 ? 2 : 1) * 128 * D * 2];
@@ -659,11 +1066,11 @@ __global__ __launch_bounds__(256, PRL_ATTN_BWD_MINB) void attn_bwd_fused(const _
   if (b < n_split) {
     const int32_t* u = split_units + 7 * b;
     attn_bwd_dkdv(q, k, v, dout, lse2, delta, u[1], u[2], u[4], u[5], dk, dv, parts + (int64_t)u[6] * 2 * 128 * D, T,
-                  H, Hkv, c2, scale, u[3], s0, s1, sL, sDl, sKV);
+                  H, Hkv, c2, scale, u[3], s0, s1, sL, sDl, sKV, sPipe);
   } else if (b < n_split + n_kv * Hkv) {
     const int it = (b - n_split) / Hkv, g = (b - n_split) % Hkv;
     attn_bwd_dkdv(q, k, v, dout, lse2, delta, kv_items[3 * it + 1], kv_items[3 * it + 2], g * rep, (g + 1) * rep, dk,
-                  dv, nullptr, T, H, Hkv, c2, scale, g, s0, s1, sL, sDl, sKV);
+                  dv, nullptr, T, H, Hkv, c2, scale, g, s0, s1, sL, sDl, sKV, sPipe);
   } else {
     const int nd = n_split + n_kv * Hkv;
     const int lq = xcd_group_remap(b - nd, (int)gridDim.x - nd, rep);
@@ -980,6 +1387,11 @@ int prl_attn_clock_read(unsigned long long* host, int32_t n) {
 int prl_attn_phase_read(unsigned long long* host, int32_t n) {
   if (!host || n < 0 || n > kClockSlots) return PRL_E_INVALID;
   return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * 8 * (size_t)n, 0,
+                                  hipMemcpyDeviceToHost);
+}
+int prl_attn_pair_read(unsigned long long* host, int32_t n) {
+  if (!host || n < 0 || n > kClockSlots) return PRL_E_INVALID;
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pair), sizeof(unsigned long long) * 8 * (size_t)n, 0,
                                   hipMemcpyDeviceToHost);
 }
 #endif

@@ -84,6 +84,13 @@ def run(lens, H, HKV):
     _native.check(phase_read(ctypes.addressof(pbuf), grid), "prl_attn_phase_read")
     ph = np.frombuffer(pbuf, dtype=np.uint64).reshape(grid, 8).astype(np.float64)
     ghz = cyc / np.maximum(real, 1.0)
+    pair_read = getattr(lib, "prl_attn_pair_read", None)
+    pair = None
+    if pair_read is not None:
+        pair_read.restype, pair_read.argtypes = ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32]
+        qbuf = (ctypes.c_ulonglong * (8 * grid))()
+        _native.check(pair_read(ctypes.addressof(qbuf), grid), "prl_attn_pair_read")
+        pair = np.frombuffer(qbuf, dtype=np.uint64).reshape(grid, 8).astype(np.float64)
 
     # MFMAs of each workgroup's busiest wave, in launch order
     u = units.cpu().numpy().reshape(-1, 7)[:n_units] if n_units else np.zeros((0, 7), np.int64)
@@ -96,7 +103,17 @@ def run(lens, H, HKV):
     mf = np.asarray(mf, np.float64)
     kv, qq = slice(0, n_kv_wg), slice(n_kv_wg, grid)
     area = sum(L * L / 2 for L in lens)
-    return {"lens": lens, "H": H, "Hkv": HKV, "workgroups": grid, "warm_launches": reps, "wall_ms": round(wall_ms, 4),
+    extra = {}
+    if pair is not None:
+        # wave 0's cycles per region of the pair schedule, per pair: each region issues 16 MFMAs
+        # (dQ: 16, 16, 8, 8), so 512 / 512 / 256 / 256 cycles would be the MFMA-bound floor
+        names = {"dkdv": ("S_a_dP_a", "S_b_dP_b+softmax_a", "acc_a+softmax_b", "acc_b"),
+                 "dq": ("S_a_dP_a", "S_b_dP_b+softmax_a", "acc_a+softmax_b", "acc_b")}
+        extra["pair_region_cycles"] = {
+            role: {nm: round(float(pair[sl, i].sum() / max(pair[sl, 4].sum(), 1.0)), 1) for i, nm in enumerate(names[role])}
+            for role, sl in (("dkdv", kv), ("dq", qq))}
+        extra["pairs_per_wg"] = {role: round(float(pair[sl, 4].mean()), 1) for role, sl in (("dkdv", kv), ("dq", qq))}
+    return {**extra,"lens": lens, "H": H, "Hkv": HKV, "workgroups": grid, "warm_launches": reps, "wall_ms": round(wall_ms, 4),
             "clock_ghz": {"median": round(float(np.median(ghz)), 3), "p10": round(float(np.percentile(ghz, 10)), 3),
                           "p90": round(float(np.percentile(ghz, 90)), 3)},
             "mfma_pipe_busy": {"dkdv": round(float(32 * mf[kv].sum() / cyc[kv].sum()), 3),

@@ -46,6 +46,12 @@ VARIANTS = {
     "attn_v_lds": {"PRL_ATTN_KV_LDS": "2"},
     "attn_bstage32": {"PRL_ATTN_INTERLEAVE": "0", "PRL_ATTN_BSTAGE": "32"},
     "phased_nowait": {"PRL_PHASED": "2"},
+    "attn_nopipe": {"PRL_ATTN_PIPE": "0"},
+    "attn_clock_nopipe": {"PRL_ATTN_CLOCK_PROBE": "1", "PRL_ATTN_PIPE": "0"},
+    "attn_pipe": {"PRL_ATTN_PIPE": "1"},
+    "attn_pipe_sgb": {"PRL_ATTN_PIPE": "1", "PRL_ATTN_PIPE_SCHED": "0"},
+    "attn_pipe_lead6": {"PRL_ATTN_PIPE": "1", "PRL_ATTN_PIPE_LEAD": "6"},
+    "attn_clock_pipe": {"PRL_ATTN_CLOCK_PROBE": "1", "PRL_ATTN_PIPE": "1"},
 }
 
 if __name__ == "__main__":
