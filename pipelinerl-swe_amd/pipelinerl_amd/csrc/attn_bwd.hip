@@ -379,7 +379,7 @@ __device__ __forceinline__ void dkdv_pair(const char* tQ, const char* tdO, const
 }
 
 #ifndef PRL_ATTN_PIPE
-#define PRL_ATTN_PIPE 0  // 1: the dK/dV tile pipeline below (A/B, tools/build_variants.py attn_pipe); 0: the two-barrier pair loop
+#define PRL_ATTN_PIPE 1  // 0: every stage through the two-barrier pair loop above (A/B, tools/build_variants.py attn_nopipe)
 #endif
 // The dK/dV role past the diagonal as one software pipeline over its 32-query tiles.  The pair loop
 // above puts a tile's whole softmax (~110 vector instructions) under the 16 MFMAs of the next
@@ -415,27 +415,61 @@ __device__ __forceinline__ const float* slot_D(const char* slot) { return slot_L
 // sequence end fall outside the buffer descriptors and land as zeros.  Waves 0 and 1 also fetch the
 // 64 L2 / delta values (4 B per lane).  Completion: the __syncthreads that starts the stage's item.
 typedef __attribute__((address_space(3))) void lds_void;
-__device__ __forceinline__ void stage_dma(const __bf16* __restrict__ q, const __bf16* __restrict__ dout,
-                                          const float* __restrict__ lse2, const float* __restrict__ delta, int64_t rs,
-                                          int64_t T, int h, int r0, int s1, char* slot, int w, int lane) {
-  const __amdgpu_buffer_rsrc_t rq = rows_rsrc(q, rs, r0, s1), ro = rows_rsrc(dout, rs, r0, s1);
+struct DmaJob {
+  __amdgpu_buffer_rsrc_t rq, ro, rl;  // Q / dO rows r0 .. s1 - 1 of all heads; this wave's L2 (w 0) or delta (w 1)
+  char* slot;                          // destination slot
+  int soff;                            // the head's byte offset in a row
+};
+// the job for item (h, r0) into slot; valid = false: zero-size descriptors (the pieces move nothing)
+__device__ __forceinline__ DmaJob make_job(const __bf16* __restrict__ q, const __bf16* __restrict__ dout,
+                                           const float* __restrict__ lse2, const float* __restrict__ delta, int64_t rs,
+                                           int64_t T, int h, int r0, int s1, char* slot, int w, bool valid) {
+  const int r1 = valid ? s1 : r0;
+  const float* src = (w == 0 ? lse2 : delta) + h * T + r0;
+  const int nb = valid ? (s1 - r0 < STAGE ? s1 - r0 : STAGE) * 4 : 0;
+  return DmaJob{rows_rsrc(q, rs, r0, r1), rows_rsrc(dout, rs, r0, r1),
+                __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), 0, nb, 0x00020000), slot, h * D * 2};
+}
+// the lane's byte offsets of its 16-B chunk in rows 16 w + 4 j + lane / 16 (j = 0..3) of a stage,
+// the XOR swizzle applied on the source side (see stage_dma)
+__device__ __forceinline__ void dma_lane_offsets(int64_t rs, int w, int lane, int* dvo) {
   const int p = lane & 15;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int r = 16 * w + 4 * j + (lane >> 4);
-    const int c = p ^ (((r & 3) << 2) | ((r >> 2) & 3));
-    const int voff = r * (int)(rs * 2) + h * D * 2 + c * 16;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rq, (lds_void*)(slot + 1024 * (4 * w + j)), 16, voff, 0, 0, 0);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(ro, (lds_void*)(slot + STAGE * 256 + 1024 * (4 * w + j)), 16, voff, 0, 0,
-                                             0);
+    dvo[j] = r * (int)(rs * 2) + (p ^ (((r & 3) << 2) | ((r >> 2) & 3))) * 16;
   }
-  if (w < 2) {  // wave-uniform
-    const float* src = (w == 0 ? lse2 : delta) + h * T + r0;
-    const int nb = (s1 - r0 < STAGE ? s1 - r0 : STAGE) * 4;
-    const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), 0, nb, 0x00020000);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rl, (lds_void*)(slot + 2 * STAGE * 256 + w * STAGE * 4), 4, lane * 4, 0, 0,
-                                             0);
+}
+// piece k (0..8) of a job: 0-3 Q rows, 4-7 dO rows (1 KiB each), 8 the 64 L2 / delta values (waves 0, 1)
+template <int K>
+__device__ __forceinline__ void dma_piece(const DmaJob& j, const int* dvo, int w, int lane) {
+  if constexpr (K < 4) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(j.rq, (lds_void*)(j.slot + 1024 * (4 * w + K)), 16, dvo[K], j.soff, 0, 0);
+  } else if constexpr (K < 8) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(j.ro, (lds_void*)(j.slot + STAGE * 256 + 1024 * (4 * w + K - 4)), 16,
+                                             dvo[K - 4], j.soff, 0, 0);
+  } else {
+    if (w < 2)  // wave-uniform
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(j.rl, (lds_void*)(j.slot + 2 * STAGE * 256 + w * STAGE * 4), 4,
+                                               lane * 4, 0, 0, 0);
   }
+}
+// one 64-row stage of Q and dO (query head h, rows r0 .. r0 + 63) and its L2 / delta into an LDS slot
+// by LDS-DMA: wave w fills rows 16w .. 16w + 15 of each image, 4 rows (1 KiB) per instruction.  The
+// DMA writes lane-linearly (lane l -> byte 16 l of the instruction's 1 KiB), so the XOR swizzle of
+// toff is applied on the source side: lane l reads chunk (l & 15) ^ swz(row) of its row.  Rows past
+// the sequence end fall outside the buffer descriptors and land as zeros.  Completion: the
+// __syncthreads that starts the stage's item.
+__device__ __forceinline__ void stage_dma(const DmaJob& j, const int* dvo, int w, int lane) {
+  dma_piece<0>(j, dvo, w, lane);
+  dma_piece<1>(j, dvo, w, lane);
+  dma_piece<2>(j, dvo, w, lane);
+  dma_piece<3>(j, dvo, w, lane);
+  dma_piece<4>(j, dvo, w, lane);
+  dma_piece<5>(j, dvo, w, lane);
+  dma_piece<6>(j, dvo, w, lane);
+  dma_piece<7>(j, dvo, w, lane);
+  dma_piece<8>(j, dvo, w, lane);
 }
 
 #ifndef PRL_ATTN_PIPE_SCHED
@@ -630,17 +664,26 @@ __device__ __forceinline__ void attn_bwd_dkdv(const __bf16* __restrict__ q, cons
     // stages from 2 on: the pipeline, drained at the head's last stage.
     const int nst = (s1 - kb + BSTAGE - 1) / BSTAGE;
     PROBE(PhaseClock& pcl = pc);
-    stage_dma(q, dout, lse2, delta, rsq, T, h0, kb, s1, sPipe, w, lane);
+    const int wu = __builtin_amdgcn_readfirstlane(w);  // provably wave-uniform: descriptors and LDS bases in SGPRs
+    int dvo[4];
+    dma_lane_offsets(rsq, wu, lane, dvo);
+    stage_dma(make_job(q, dout, lse2, delta, rsq, T, h0, kb, s1, sPipe, wu, true), dvo, wu, lane);
     int cs = 0;
-    // start item (h, i): wait for it, refill the slot two items back with the next item
+    // start item (h, i): wait for it, then refill the slot two items back with the next item
+    // (issuing the 9 pieces one every 7 MFMAs of the schedule instead measured slower: 4543 vs 4337
+    // cycles per stage; each piece holds the wave ~100 cycles wherever it is issued)
     auto begin_item = [&](int h, int i) -> char* {
       const int ns = cs == 2 ? 0 : cs + 1;
       PROBE(pc.start(); pc.acc[5]++);
+      // the LDS-DMA of item (h, i) done (hipcc's wait before the barrier does not always count the
+      // DMA: one loop's barrier had none, and dK went wrong), then every wave's
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();  // item (h, i) is in slot cs; every wave is done with the slot ns held
       PROBE(pc.lap(0));
       const int hn = i + 1 < nst ? h : h + 1, in = i + 1 < nst ? i + 1 : 0;
-      if (hn < h1 && !PRL_ATTN_EXP_NOLOAD)
-        stage_dma(q, dout, lse2, delta, rsq, T, hn, kb + in * BSTAGE, s1, sPipe + ns * kSlot, w, lane);
+      stage_dma(make_job(q, dout, lse2, delta, rsq, T, hn, kb + in * BSTAGE, s1, sPipe + ns * kSlot, wu,
+                         hn < h1 && !PRL_ATTN_EXP_NOLOAD),
+                dvo, wu, lane);
       sched_fence();
       PROBE(pc.lap(2));
       char* const cur = sPipe + cs * kSlot;
@@ -1040,10 +1083,10 @@ __global__ __launch_bounds__(256, PRL_ATTN_BWD_MINB) void attn_bwd_fused(const _
                                                       const int32_t* __restrict__ split_units, int n_split,
                                                       float* __restrict__ parts) {
 #if PRL_ATTN_PIPE
-  // three stage slots for the dK/dV pipeline; slot 2 doubles as the two-barrier loops' stage (the
-  // diagonal stages of dK/dV, every stage of dQ)
+  // three stage slots for the dK/dV role; the dQ role's K / V stage uses the first 32 KiB (at the
+  // bottom of LDS: its reads keep 16-bit immediate offsets; at slot 2 the dQ role ran 4-10 % slower)
   __shared__ __attribute__((aligned(16))) char sPipe[3 * kSlot];
-  char* const s0 = sPipe + 2 * kSlot;
+  char* const s0 = sPipe;
   char* const s1 = s0 + STAGE * D * 2;
   float* const sL = reinterpret_cast<float*>(s0 + 2 * STAGE * D * 2);
   float* const sDl = sL + STAGE;

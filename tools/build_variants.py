@@ -48,10 +48,8 @@ VARIANTS = {
     "phased_nowait": {"PRL_PHASED": "2"},
     "attn_nopipe": {"PRL_ATTN_PIPE": "0"},
     "attn_clock_nopipe": {"PRL_ATTN_CLOCK_PROBE": "1", "PRL_ATTN_PIPE": "0"},
-    "attn_pipe": {"PRL_ATTN_PIPE": "1"},
-    "attn_pipe_sgb": {"PRL_ATTN_PIPE": "1", "PRL_ATTN_PIPE_SCHED": "0"},
-    "attn_pipe_lead6": {"PRL_ATTN_PIPE": "1", "PRL_ATTN_PIPE_LEAD": "6"},
-    "attn_clock_pipe": {"PRL_ATTN_CLOCK_PROBE": "1", "PRL_ATTN_PIPE": "1"},
+    "attn_pipe_sgb": {"PRL_ATTN_PIPE_SCHED": "0"},
+    "attn_pipe_lead6": {"PRL_ATTN_PIPE_LEAD": "6"},
 }
 
 if __name__ == "__main__":
