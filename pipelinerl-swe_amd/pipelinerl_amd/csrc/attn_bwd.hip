@@ -956,6 +956,134 @@ __device__ __forceinline__ void dq_pair(const char* tK, const char* tV, KR qf, V
   PAIR_LAP(pair_lap(3));
 }
 
+#if PRL_ATTN_PIPE
+// The dQ role's stages below the diagonal as the same kind of pipeline as the dK/dV role's: per 64-key
+// stage (tiles a, b) the MFMA stream S/dP(a) 16 | dQ += previous b 8 | S/dP(b) 16 | dQ += a 8, and
+// each tile's softmax (16 elements: p = 2^(c2 S - L2), dS = p (dP - delta), L2 and delta per lane)
+// spread over the 24 MFMAs between its S/dP and its dQ product: tile a over gaps 16-39, tile b over
+// gaps 40-47 and the next stage's 0-15.  The 32 half-operations (p of an element, dS of an element:
+// p0 p1 s0 p2 s1 ... p15 s14 s15) go to window gap (3 j) / 4.  The order of the dQ accumulation is
+// the pair loop's (dq_acc), so the results are its bit for bit.
+template <int J>
+struct DqOp {  // half-operation J of a tile's softmax: kind 0 = p of element e, 1 = dS of element e
+  static constexpr int kind = J == 0 ? 0 : (J == 31 ? 1 : ((J & 1) ? 0 : 1));
+  static constexpr int e = J == 0 ? 0 : (J == 31 ? 15 : ((J & 1) ? (J + 1) / 2 : J / 2 - 1));
+};
+template <bool PREV>
+struct DqIter {
+  static constexpr int LEAD = PRL_ATTN_PIPE_LEAD;
+  static constexpr bool live(int g) { return PREV || g < 16 || g >= 24; }  // MFMA g exists
+  const char *kpb, *ka, *va, *kb, *vb;  // tile images: previous b's K; a's and b's K and V
+  const bf16x8 *qf, *of;
+  int lane, hi;
+  float c2, lq, dlt;
+  f32x16 &Sa, &dPa, &Sb, &dPb;
+  bf16x8 *sa, *sb;
+  float* pv;  // p of tile b's elements carried over the stage seam
+  f32x16* dQt;
+  bf16x8 ring[LEAD];
+  float pa[16];
+
+  template <int G>
+  __device__ __forceinline__ bf16x8 operand() const {
+    if constexpr (G < 16 || (G >= 24 && G < 40)) {
+      constexpr int t = G < 16 ? G : G - 24;
+      return row_read((t & 1) ? (G < 16 ? va : vb) : (G < 16 ? ka : kb), lane & 31, 2 * (t >> 1) + hi);
+    } else {
+      constexpr int t = G < 24 ? G - 16 : G - 40;
+      return tr_operand(G < 24 ? kpb : ka, lane, t >> 1, t & 1);
+    }
+  }
+  // half-op J of the softmax of S / dP into p / dst
+  template <int J>
+  __device__ __forceinline__ void sm_op(const f32x16& S, const f32x16& dP, float* p, bf16x8* dst) {
+    constexpr int e = DqOp<J>::e;
+    if constexpr (DqOp<J>::kind == 0) p[e] = bexp2(__builtin_fmaf(S[e], c2, -lq));
+    else dst[e >> 3][e & 7] = (__bf16)(p[e] * (dP[e] - dlt));
+  }
+  // the half-ops whose window gap (3 j / 4) is U: tile a's window starts at gap 16, tile b's at 40
+  template <int U, int J = 0>
+  __device__ __forceinline__ void sm_gap(const f32x16& S, const f32x16& dP, float* p, bf16x8* dst) {
+    if constexpr (J < 32) {
+      if constexpr ((3 * J) / 4 == U) sm_op<J>(S, dP, p, dst);
+      sm_gap<U, J + 1>(S, dP, p, dst);
+    }
+  }
+  template <int G>
+  __device__ __forceinline__ void gap() {
+    if constexpr (live(G)) {
+      const bf16x8 op = ring[G % LEAD];
+      if constexpr (G < 16 || (G >= 24 && G < 40)) {
+        constexpr int t = G < 16 ? G : G - 24;
+        f32x16& S = G < 16 ? Sa : Sb;
+        f32x16& dP = G < 16 ? dPa : dPb;
+        if constexpr (t == 0) S = mfma(op, qf[0], f32x16{});
+        else if constexpr (t == 1) dP = mfma(op, of[0], f32x16{});
+        else if constexpr (t & 1) dP = mfma(op, of[t >> 1], dP);
+        else S = mfma(op, qf[t >> 1], S);
+      } else {
+        constexpr int t = G < 24 ? G - 16 : G - 40;
+        dQt[t >> 1] = mfma(op, (G < 24 ? sb : sa)[t & 1], dQt[t >> 1]);
+      }
+    }
+    if constexpr (G + LEAD < 48 && live(G + LEAD)) ring[(G + LEAD) % LEAD] = operand<G + LEAD>();
+    if constexpr (G < 16) {  // the previous tile b's window gaps 8 .. 23
+      if constexpr (PREV) sm_gap<G + 8>(Sb, dPb, pv, sb);
+    } else if constexpr (G < 40) {  // tile a's window gaps 0 .. 23
+      sm_gap<G - 16>(Sa, dPa, pa, sa);
+    } else {  // tile b's window gaps 0 .. 7
+      sm_gap<G - 40>(Sb, dPb, pv, sb);
+    }
+    sched_fence();
+  }
+  template <int... G>
+  __device__ __forceinline__ void prime(std::integer_sequence<int, G...>) {
+    ((live(G) ? (void)(ring[G] = operand<G>()) : (void)0), ...);
+  }
+  template <int... G>
+  __device__ __forceinline__ void run(std::integer_sequence<int, G...>) {
+    (gap<G>(), ...);
+  }
+  // the last tile b of the pipeline: the rest of its softmax (window gaps 8 .. 23), then dQ += b
+  template <int... U>
+  __device__ __forceinline__ void drain_sm(std::integer_sequence<int, U...>) {
+    (sm_gap<U + 8>(Sb, dPb, pv, sb), ...);
+  }
+};
+template <bool PREV>
+__device__ __forceinline__ void dq_iter(const char* kpb, const char* ka, const char* va, const char* kb,
+                                        const char* vb, const bf16x8* qf, const bf16x8* of, int lane, float c2,
+                                        float lq, float dlt, f32x16& Sa, f32x16& dPa, f32x16& Sb, f32x16& dPb,
+                                        bf16x8* sa, bf16x8* sb, float* pv, f32x16* dQt) {
+  DqIter<PREV> it{kpb, ka, va, kb, vb, qf, of, lane, lane >> 5, c2, lq, dlt, Sa, dPa, Sb, dPb, sa, sb, pv, dQt, {}, {}};
+  it.prime(std::make_integer_sequence<int, DqIter<PREV>::LEAD>{});
+  it.run(std::make_integer_sequence<int, 48>{});
+}
+__device__ __forceinline__ void dq_drain(const char* kpb, const bf16x8* qf, const bf16x8* of, int lane, float c2,
+                                         float lq, float dlt, f32x16& Sb, f32x16& dPb, bf16x8* sb, float* pv,
+                                         f32x16* dQt) {
+  f32x16 dummy;
+  DqIter<true> it{kpb, kpb, kpb, kpb, kpb, qf, of, lane, lane >> 5, c2, lq, dlt, dummy, dummy, Sb, dPb, sb, sb, pv,
+                  dQt, {}, {}};
+  it.drain_sm(std::make_integer_sequence<int, 16>{});
+  sched_fence();
+  dq_acc(kpb, lane, sb, dQt);
+}
+// one 64-key stage of K and V (kv head g, keys r0 .. r0 + 63) into an LDS slot by LDS-DMA, as stage_dma
+__device__ __forceinline__ void stage_dma_kv(const __bf16* __restrict__ k, const __bf16* __restrict__ v, int64_t rs,
+                                             int g, int r0, int r1, char* slot, const int* dvo, int w) {
+  const __amdgpu_buffer_rsrc_t rk = rows_rsrc(k, rs, r0, r1);
+  const DmaJob j{rk, rows_rsrc(v, rs, r0, r1), rk, slot, g * D * 2};  // (rl unused: no piece 8)
+  dma_piece<0>(j, dvo, w, 0);
+  dma_piece<1>(j, dvo, w, 0);
+  dma_piece<2>(j, dvo, w, 0);
+  dma_piece<3>(j, dvo, w, 0);
+  dma_piece<4>(j, dvo, w, 0);
+  dma_piece<5>(j, dvo, w, 0);
+  dma_piece<6>(j, dvo, w, 0);
+  dma_piece<7>(j, dvo, w, 0);
+}
+#endif
 __device__ __forceinline__ void attn_bwd_dq(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
                                                    const __bf16* __restrict__ v, const __bf16* __restrict__ dout,
                                                    const float* __restrict__ lse2, const float* __restrict__ delta,
@@ -1004,10 +1132,73 @@ __device__ __forceinline__ void attn_bwd_dq(const __bf16* __restrict__ q, const 
 #pragma unroll
   for (int i = 0; i < 4; ++i) dQt[i] = f32x16{};
   const int kend = (qb + 128 < s1 ? qb + 128 : s1);  // causal: keys <= the block's last query
+  PROBE(PhaseClock pc);
+#if PRL_ATTN_PIPE
+  {
+    // key stage m = keys s0 + 64 m in LDS slot m % 3 by LDS-DMA one stage ahead, one barrier per stage
+    // (as the dK/dV role); stages before the block's first query (m < np) are below the diagonal
+    // for every wave: the pipeline; the last two: the pair / masked-tile code
+    const int wu = __builtin_amdgcn_readfirstlane(w);
+    int dvo[4];
+    dma_lane_offsets(rsk, wu, lane, dvo);
+    const int nk = (kend - s0 + BSTAGE - 1) / BSTAGE, np = (qb - s0) / BSTAGE;
+    stage_dma_kv(k, v, rsk, g, s0, s1, sQO, dvo, wu);
+    int cs = 0;
+    auto begin_item = [&](int m) -> char* {
+      const int ns = cs == 2 ? 0 : cs + 1;
+      PROBE(pc.start(); pc.acc[5]++);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this stage's LDS-DMA (see the dK/dV role)
+      __syncthreads();
+      PROBE(pc.lap(0));
+      if (m + 1 < nk && !PRL_ATTN_EXP_NOLOAD)
+        stage_dma_kv(k, v, rsk, g, s0 + (m + 1) * BSTAGE, s1, sQO + ns * kSlot, dvo, wu);
+      sched_fence();
+      PROBE(pc.lap(2));
+      char* const cur = sQO + cs * kSlot;
+      cs = ns;
+      return cur;
+    };
+    if (np > 0) {
+      f32x16 Sa, dPa, Sb, dPb;
+      bf16x8 sa[2], sb[2];
+      float pv[16];
+      const char* cur = begin_item(0);
+      dq_iter<false>(cur, cur, cur + STAGE * 256, cur + TILE * 256, cur + STAGE * 256 + TILE * 256, qf, of, lane, c2,
+                     lq, dq_delta, Sa, dPa, Sb, dPb, sa, sb, pv, dQt);
+      PROBE(pc.lap(3));
+#pragma unroll 1
+      for (int m = 1; m < np; ++m) {
+        const char* kpb = cur + TILE * 256;
+        cur = begin_item(m);
+        dq_iter<true>(kpb, cur, cur + STAGE * 256, cur + TILE * 256, cur + STAGE * 256 + TILE * 256, qf, of, lane,
+                      c2, lq, dq_delta, Sa, dPa, Sb, dPb, sa, sb, pv, dQt);
+        PROBE(pc.lap(3));
+      }
+      dq_drain(cur + TILE * 256, qf, of, lane, c2, lq, dq_delta, Sb, dPb, sb, pv, dQt);
+    }
+#pragma unroll 1
+    for (int m = np; m < nk; ++m) {  // the diagonal stages
+      const char* const cur = begin_item(m);
+      const char *tK = cur, *tV = cur + STAGE * 256;
+      const int k00 = s0 + m * BSTAGE;
+      if (PRL_ATTN_INTERLEAVE && qw < s1 && k00 + BSTAGE - 1 <= qw && k00 + BSTAGE <= s1) {  // wave-uniform
+        dq_pair(tK, tV, qf, of, qq, qval, s1, lane, c2, lq, dq_delta, dQt PAIR_CLOCK_PASS);
+      } else {
+#pragma unroll 1
+        for (int half = 0; half < BSTAGE / TILE; ++half) {
+          const int k0 = k00 + TILE * half;
+          if (!dq_live(qw, k0, s1, kend)) continue;  // wave-uniform
+          dq_tile(tK + half * TILE * 256, tV + half * TILE * 256, k0, qf, of, qq, qval, s1, lane, c2, lq, dq_delta,
+                  dQt);
+        }
+      }
+      PROBE(pc.lap(4));
+    }
+  }
+#else
   const int vb = stage_vbase(rsk, g, tid);
   StageT<BSTAGE> nk = stage_load_rows<BSTAGE>(k, rsk, g, s0, s1, tid, vb),
                  nv = stage_load_rows<BSTAGE>(v, rsk, g, s0, s1, tid, vb);
-  PROBE(PhaseClock pc);
   for (int k00 = s0; k00 < kend; k00 += BSTAGE) {
     PROBE(pc.start(); pc.acc[5]++);
     __syncthreads();
@@ -1034,6 +1225,7 @@ __device__ __forceinline__ void attn_bwd_dq(const __bf16* __restrict__ q, const 
     }
     PROBE(pc.lap(4));
   }
+#endif
   PROBE(pc.store());
   if (!qval) return;
   __bf16* dqr = dq + (int64_t)qq * rs + h * D;
@@ -1117,7 +1309,8 @@ __global__ __launch_bounds__(256, PRL_ATTN_BWD_MINB) void attn_bwd_fused(const _
   } else {
     const int nd = n_split + n_kv * Hkv;
     const int lq = xcd_group_remap(b - nd, (int)gridDim.x - nd, rep);
-    attn_bwd_dq(q, k, v, dout, lse2, delta, q_items, dq, T, H, Hkv, c2, scale, lq / H, lq % H, s0, s1, sKV);
+    attn_bwd_dq(q, k, v, dout, lse2, delta, q_items, dq, T, H, Hkv, c2, scale, lq / H, lq % H, s0, s1,
+                PRL_ATTN_PIPE ? sPipe : sKV);
   }
 #if PRL_ATTN_CLOCK_PROBE
   clock_stamp(b, t0, r0);
