@@ -82,8 +82,15 @@ class WorkerExtension:
         elems = max(8, int(request.bucket_bytes) // 2)
         for a, b in layout.buckets(elems):
             comm.broadcast(flat[a:b], self.process_group, src=0)
+        self._apply_flat(flat, layout)
+
+    def _apply_flat(self, flat: torch.Tensor, layout) -> None:
+        """Load every parameter of a received flat buffer: one HIP unflatten pass straight into the
+        model's storage when it resolves every name to a writable bf16 region (32 tensors per
+        launch; for a fused-layout model the q / k / v and gate / up regions are row blocks of its
+        qkv_proj / gate_up_proj), else the per-name load_weights path (vllm1.py:89-93)."""
         targets = self._direct_targets(layout)
-        if targets is not None:  # parameters held directly: one HIP unflatten pass (32 tensors per launch)
+        if targets is not None:
             from .weight_update import HipFlatPacker
 
             HipFlatPacker().unflatten(flat, targets, layout.offsets)
@@ -92,20 +99,20 @@ class WorkerExtension:
             self._load_one(name, flat[off:off + n].view(shape))
 
     def _direct_targets(self, layout) -> list[torch.Tensor] | None:
-        """The destination tensors when the model holds every broadcast name as a plain
-        contiguous bf16 parameter of the same shape on this HIP device (the standalone actor's
-        ParamDictModel); None for models that remap names in load_weights (vLLM's fused qkv /
-        gate_up, vllm1.py:89-93), which keep the per-name load."""
-        params = getattr(self.model_runner.model, "params", None)
-        if not isinstance(params, dict) or self.device.type != "cuda":
+        """The destination region of every broadcast name, from the model's direct_target(name,
+        shape) (ParamDictModel: the parameter; StackedParamsModel: a row block of a fused
+        parameter), when each is a contiguous, 16-B aligned bf16 tensor on this HIP device; None
+        otherwise (models without direct_target keep the per-name load)."""
+        resolve = getattr(self.model_runner.model, "direct_target", None)
+        if resolve is None or self.device.type != "cuda":
             return None
         out = []
         for name, shape in zip(layout.names, layout.shapes):
-            p = params.get(name)
-            if (p is None or p.dtype != torch.bfloat16 or tuple(p.shape) != tuple(shape) or not p.is_contiguous()
-                    or p.device != self.device or p.data_ptr() % 16):
+            t = resolve(name, tuple(shape))
+            if (t is None or t.dtype != torch.bfloat16 or not t.is_contiguous() or t.device != self.device
+                    or t.data_ptr() % 16):
                 return None
-            out.append(p.detach())  # shares the version counter: the unflatten moves it
+            out.append(t)  # views share the parameter's version counter: the unflatten moves it
         return out
 
     def _load_one(self, name: str, tensor: torch.Tensor):
@@ -132,15 +139,82 @@ class ParamDictModel:
             loaded.add(name)
         return loaded
 
+    def direct_target(self, name: str, shape: tuple) -> torch.Tensor | None:
+        p = self.params.get(name)
+        return p.detach() if p is not None and tuple(p.shape) == shape else None
+
+
+# vLLM's fused projections (vllm/model_executor/models/qwen2.py, vLLM 0.8.5, Qwen2Model.load_weights:
+# stacked_params_mapping, applied by the reference actor's load_weights call, vllm1.py:89-93): the
+# trainer's q / k / v projections are row blocks of one qkv_proj (QKVParallelLinear shard ids "q",
+# "k", "v"), gate / up of one gate_up_proj (MergedColumnParallelLinear shards 0, 1), in that order;
+# at tensor parallel 1 a shard's rows are contiguous.  vLLM is not importable here: the layout and the
+# loader are restated from its source, and the trainer-side names are pinned by F4.
+STACKED_PARAMS = (("qkv_proj", "q_proj", "q"), ("qkv_proj", "k_proj", "k"), ("qkv_proj", "v_proj", "v"),
+                  ("gate_up_proj", "gate_proj", 0), ("gate_up_proj", "up_proj", 1))
+_SHARD_ORDER = {"q": 0, "k": 1, "v": 2, 0: 0, 1: 1}
+
+
+class StackedParamsModel:
+    """An inference model in vLLM's fused parameter layout, built from a trainer-layout module:
+    load_weights(name -> copy into the shard's rows, returns the fused names loaded) as vLLM's
+    Qwen2 model does, and direct_target(name, shape) -> the shard's row block, so the bucketed
+    receive unflattens straight into qkv_proj / gate_up_proj with no per-name copy."""
+
+    def __init__(self, module: torch.nn.Module):
+        self.params: dict[str, torch.Tensor] = {}
+        self.shards: dict[str, tuple[str, int, int]] = {}  # trainer name -> (fused name, first row, rows)
+        groups: dict[str, list] = {}
+        for name, p in module.named_parameters():
+            for fused, part, shard in STACKED_PARAMS:
+                if f".{part}." in name:
+                    groups.setdefault(name.replace(f".{part}.", f".{fused}."), []).append((shard, name, p))
+                    break
+            else:
+                self.params[name] = p.detach()
+        for fname, members in groups.items():
+            members.sort(key=lambda m: _SHARD_ORDER[m[0]])
+            self.params[fname] = torch.cat([p.detach() for _, _, p in members], dim=0).contiguous()
+            row = 0
+            for _, name, p in members:
+                self.shards[name] = (fname, row, p.shape[0])
+                row += p.shape[0]
+
+    def _region(self, name: str) -> torch.Tensor | None:
+        if name in self.shards:
+            fname, r0, n = self.shards[name]
+            return self.params[fname][r0:r0 + n]
+        return self.params.get(name)
+
+    def load_weights(self, weights):
+        loaded = set()
+        for name, t in weights:
+            if "rotary_emb.inv_freq" in name:
+                continue
+            dst = self._region(name)
+            if dst is None or tuple(dst.shape) != tuple(t.shape):
+                continue
+            with torch.no_grad():
+                dst.copy_(t.to(dst.dtype))
+            loaded.add(self.shards[name][0] if name in self.shards else name)
+        return loaded
+
+    def direct_target(self, name: str, shape: tuple) -> torch.Tensor | None:
+        t = self._region(name)
+        return t if t is not None and tuple(t.shape) == shape else None
+
 
 class StandaloneWorker(WorkerExtension):
     def __init__(self, module: torch.nn.Module, rank: int = 0, device: str | torch.device = "cpu",
-                 backend: str = "nccl"):
+                 backend: str = "nccl", layout: str = "trainer"):
         self.rank = rank
         self.device = torch.device(device)
+        if self.device.type == "cuda" and self.device.index is None:  # compare equal to the tensors' devices
+            self.device = torch.device("cuda", torch.cuda.current_device())
         self.actor_group_backend = backend
         module.to(self.device)
-        self.model_runner = types.SimpleNamespace(model=ParamDictModel(module))
+        model = StackedParamsModel(module) if layout == "vllm" else ParamDictModel(module)
+        self.model_runner = types.SimpleNamespace(model=model)
         self.model_config = types.SimpleNamespace(dtype=next(module.parameters()).dtype)
 
 
@@ -179,13 +253,15 @@ def main(argv=None):
     ap.add_argument("--backend", default="nccl")
     ap.add_argument("--device", default="cuda" if torch.cuda.is_available() else "cpu")
     ap.add_argument("--model-config", required=True, help="HF config dir/json of the model to hold")
+    ap.add_argument("--layout", choices=("trainer", "vllm"), default="trainer",
+                    help="parameter layout held: the trainer's names, or vLLM's fused qkv_proj / gate_up_proj")
     args = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO)
     from transformers import AutoConfig, AutoModelForCausalLM
 
     cfg = AutoConfig.from_pretrained(args.model_config)
     module = AutoModelForCausalLM.from_config(cfg, torch_dtype=torch.bfloat16)
-    worker = StandaloneWorker(module, rank=0, device=args.device, backend=args.backend)
+    worker = StandaloneWorker(module, rank=0, device=args.device, backend=args.backend, layout=args.layout)
     app = build_app(worker)
     if not args.disable_weight_updates:
         t = threading.Thread(target=worker.init_actor_update_group,

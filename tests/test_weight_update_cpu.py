@@ -43,7 +43,17 @@ def make_model(seed):
     return m.to(torch.bfloat16)
 
 
-def _trainer(port, world, transport, exp, versions, use_reference_pg):
+def make_qwen2(seed):
+    """A tiny Qwen2 (the trainer's parameter names: q/k/v_proj, gate/up_proj, GQA 2/1)."""
+    from transformers import Qwen2Config, Qwen2ForCausalLM
+
+    torch.manual_seed(seed)
+    cfg = Qwen2Config(vocab_size=37, hidden_size=16, intermediate_size=24, num_hidden_layers=2,
+                      num_attention_heads=2, num_key_value_heads=1, tie_word_embeddings=False)
+    return Qwen2ForCausalLM(cfg).to(torch.bfloat16)
+
+
+def _trainer(port, world, transport, exp, versions, use_reference_pg, qwen=False):
     sys.path[:0] = [str(ROOT), str(ROOT / "pipelinerl-swe_amd")]
     from pipelinerl_amd import torch_utils
     from pipelinerl_amd.streams import SingleStreamSpec, reset_streams_backend, set_streams_backend
@@ -51,7 +61,7 @@ def _trainer(port, world, transport, exp, versions, use_reference_pg):
 
     reset_streams_backend()
     set_streams_backend("files")
-    model = make_model(0)
+    model = make_qwen2(0) if qwen else make_model(0)
     pg = torch_utils.init_extra_process_group(group_name="actor", backend="gloo",
                                               init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=world)
     stream = SingleStreamSpec(exp_path=Path(exp), topic="weight_update_request")
@@ -66,11 +76,24 @@ def _trainer(port, world, transport, exp, versions, use_reference_pg):
     torch.save({n: p.detach().clone() for n, p in model.named_parameters()}, Path(exp) / "trainer_params.pt")
 
 
-def _actor(port, world, idx, transport, exp, nupdates, use_reference_pg):
+def _actor(port, world, idx, transport, exp, nupdates, use_reference_pg, qwen=False):
     sys.path[:0] = [str(ROOT), str(ROOT / "pipelinerl-swe_amd")]
     from pipelinerl_amd.actor import StandaloneWorker
     from pipelinerl_amd.weight_update import ParameterInfo, WeightUpdateRequest
 
+    if qwen:  # vLLM's fused layout at the actor; the request carries the trainer's names
+        module = make_qwen2(100 + idx)
+        names = [(n, list(p.shape)) for n, p in module.named_parameters()]
+        worker = StandaloneWorker(module, rank=0, device="cpu", backend="gloo", layout="vllm")
+        worker.init_actor_update_group(idx, 1, f"tcp://127.0.0.1:{port}", world)
+        infos = [ParameterInfo(name=n, shape=s, dtype=str(torch.bfloat16)) for n, s in names]
+        for v in range(nupdates):
+            worker.receive_weight_update(WeightUpdateRequest(version=v, parameters_info=infos, transport=transport,
+                                                             bucket_bytes=1000 if transport == "bucketed" else 0))
+        m = worker.model_runner.model
+        torch.save({"by_name": {n: m.direct_target(n, tuple(s)).clone() for n, s in names},
+                    "fused": {n: p.clone() for n, p in m.params.items()}}, Path(exp) / f"actor{idx}_params.pt")
+        return
     worker = StandaloneWorker(make_model(100 + idx), rank=0, device="cpu", backend="gloo")
     if use_reference_pg:  # join with the REFERENCE's group helper: pins the store-key layout
         sys.path.insert(0, "/root/reference")
@@ -90,12 +113,12 @@ def _actor(port, world, idx, transport, exp, nupdates, use_reference_pg):
                Path(exp) / f"actor{idx}_params.pt")
 
 
-def _run(rank, port, world, transport, exp, use_reference_pg):
+def _run(rank, port, world, transport, exp, use_reference_pg, qwen=False):
     os.environ["OMP_NUM_THREADS"] = "1"
     if rank == 0:
-        _trainer(port, world, transport, exp, [3, 7], use_reference_pg)
+        _trainer(port, world, transport, exp, [3, 7], use_reference_pg, qwen)
     else:
-        _actor(port, world, rank - 1, transport, exp, 2, use_reference_pg)
+        _actor(port, world, rank - 1, transport, exp, 2, use_reference_pg, qwen)
 
 
 @pytest.mark.parametrize("transport,world", [("per_tensor", 2), ("bucketed", 2), ("bucketed", 3)])
@@ -111,6 +134,48 @@ def test_broadcast_roundtrip(tmp_path, transport, world):
     lines = (tmp_path / "streams" / "weight_update_request" / "0" / "0" / "0.jsonl").read_text().splitlines()
     msgs = [json.loads(x) for x in lines]
     assert [m["version"] for m in msgs if m["kind"] == "weight_update_success"] == [3, 7]
+
+
+@pytest.mark.parametrize("transport", ["per_tensor", "bucketed"])
+def test_broadcast_into_vllm_fused_layout(tmp_path, transport):
+    """An actor holding vLLM's fused qkv_proj / gate_up_proj receives the trainer's per-projection
+    names: every q / k / v and gate / up tensor lands in its row block, the rest by name, and each
+    fused parameter is the concatenation of the trainer's shards in vLLM's order."""
+    port = free_port()
+    mp.spawn(_run, args=(port, 2, transport, str(tmp_path), False, True), nprocs=2, join=True)
+    want = torch.load(tmp_path / "trainer_params.pt")
+    got = torch.load(tmp_path / "actor0_params.pt")
+    assert set(got["by_name"]) == set(want)
+    for n in want:
+        assert torch.equal(got["by_name"][n], want[n]), n
+    fused = got["fused"]
+    assert not any(".q_proj." in n or ".gate_proj." in n for n in fused)
+    for i in range(2):
+        pre = f"model.layers.{i}."
+        assert torch.equal(fused[pre + "self_attn.qkv_proj.weight"],
+                           torch.cat([want[pre + f"self_attn.{x}_proj.weight"] for x in "qkv"]))
+        assert torch.equal(fused[pre + "self_attn.qkv_proj.bias"],
+                           torch.cat([want[pre + f"self_attn.{x}_proj.bias"] for x in "qkv"]))
+        assert torch.equal(fused[pre + "mlp.gate_up_proj.weight"],
+                           torch.cat([want[pre + "mlp.gate_proj.weight"], want[pre + "mlp.up_proj.weight"]]))
+
+
+def test_vllm_layout_load_weights_returns_the_fused_name():
+    """The reference actor raises unless load_weights reports exactly one loaded parameter
+    (vllm1.py:91-93); for a shard that is the fused parameter's name, as in vLLM."""
+    sys.path[:0] = [str(ROOT), str(ROOT / "pipelinerl-swe_amd")]
+    from pipelinerl_amd.actor import StackedParamsModel
+
+    src = make_qwen2(1)
+    m = StackedParamsModel(make_qwen2(2))
+    w = dict(src.named_parameters())
+    assert m.load_weights([("model.layers.0.self_attn.k_proj.weight", w["model.layers.0.self_attn.k_proj.weight"])]) \
+        == {"model.layers.0.self_attn.qkv_proj.weight"}
+    assert m.load_weights([("model.norm.weight", w["model.norm.weight"])]) == {"model.norm.weight"}
+    assert m.load_weights([("model.layers.0.self_attn.rotary_emb.inv_freq", torch.ones(4))]) == set()
+    assert m.load_weights([("no.such.param", torch.ones(4))]) == set()
+    assert torch.equal(m.params["model.layers.0.self_attn.qkv_proj.weight"][16:24],
+                       w["model.layers.0.self_attn.k_proj.weight"].detach())
 
 
 @pytest.mark.skipif(not Path("/root/reference/pipelinerl/torch_utils.py").exists(),
