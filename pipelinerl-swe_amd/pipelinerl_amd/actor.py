@@ -155,6 +155,30 @@ STACKED_PARAMS = (("qkv_proj", "q_proj", "q"), ("qkv_proj", "k_proj", "k"), ("qk
 _SHARD_ORDER = {"q": 0, "k": 1, "v": 2, 0: 0, 1: 1}
 
 
+def fused_direct_target(params: dict[str, torch.Tensor], config):
+    """direct_target(name, shape) over a model already in vLLM's fused layout (its named_parameters
+    and its HF config): the trainer's q / k / v or gate / up name -> that shard's row block of the
+    fused parameter (QKVParallelLinear / MergedColumnParallelLinear row offsets at tensor parallel 1),
+    any other name -> the parameter of that name; None when the shape differs or the name is unknown."""
+    hd = getattr(config, "head_dim", None) or config.hidden_size // config.num_attention_heads
+    rows = {"q": config.num_attention_heads * hd, "k": config.num_key_value_heads * hd,
+            "v": config.num_key_value_heads * hd, 0: config.intermediate_size, 1: config.intermediate_size}
+
+    def direct_target(name: str, shape: tuple) -> torch.Tensor | None:
+        for fused, part, shard in STACKED_PARAMS:
+            if f".{part}." in name:
+                p = params.get(name.replace(f".{part}.", f".{fused}."))
+                if p is None:
+                    return None
+                r0 = sum(rows[s] for f, _, s in STACKED_PARAMS if f == fused and _SHARD_ORDER[s] < _SHARD_ORDER[shard])
+                t = p.detach()[r0:r0 + rows[shard]]
+                return t if tuple(t.shape) == shape else None
+        p = params.get(name)
+        return p.detach() if p is not None and tuple(p.shape) == shape else None
+
+    return direct_target
+
+
 class StackedParamsModel:
     """An inference model in vLLM's fused parameter layout, built from a trainer-layout module:
     load_weights(name -> copy into the shard's rows, returns the fused names loaded) as vLLM's

@@ -178,6 +178,23 @@ def test_vllm_layout_load_weights_returns_the_fused_name():
                        w["model.layers.0.self_attn.k_proj.weight"].detach())
 
 
+def test_fused_direct_target_matches_the_stand_in():
+    """fused_direct_target (the adapter a vLLM worker attaches to its model) over
+    a fused-layout model's parameters and config resolves every trainer name to the same storage as
+    StackedParamsModel's own shard map."""
+    sys.path[:0] = [str(ROOT), str(ROOT / "pipelinerl-swe_amd")]
+    from pipelinerl_amd.actor import StackedParamsModel, fused_direct_target
+
+    trainer = make_qwen2(3)
+    m = StackedParamsModel(make_qwen2(4))
+    resolve = fused_direct_target(m.params, trainer.config)
+    for n, p in trainer.named_parameters():
+        a, b = resolve(n, tuple(p.shape)), m.direct_target(n, tuple(p.shape))
+        assert a is not None and a.data_ptr() == b.data_ptr() and a.shape == b.shape, n
+    assert resolve("model.layers.0.self_attn.q_proj.weight", (3, 3)) is None
+    assert resolve("no.such.param", (1,)) is None
+
+
 @pytest.mark.skipif(not Path("/root/reference/pipelinerl/torch_utils.py").exists(),
                     reason="reference checkout not present (wire-compat check runs in the build container)")
 def test_actor_group_interoperates_with_reference_helper(tmp_path):
