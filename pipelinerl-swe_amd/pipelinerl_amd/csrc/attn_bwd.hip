@@ -378,6 +378,9 @@ __device__ __forceinline__ void dkdv_pair(const char* tQ, const char* tdO, const
   PAIR_LAP(pair_lap(3));
 }
 
+#ifndef PRL_ATTN_BWD_MINB
+#define PRL_ATTN_BWD_MINB 1  // A/B: 2 = two workgroups per CU (<= 256 registers per lane)
+#endif
 #ifndef PRL_ATTN_PIPE
 #define PRL_ATTN_PIPE 1  // 0: every stage through the two-barrier pair loop above (A/B, tools/build_variants.py attn_nopipe)
 #endif
@@ -394,6 +397,10 @@ __device__ __forceinline__ void dkdv_pair(const char* tQ, const char* tdO, const
 // before that barrier.  The accumulation order of dK^T / dV^T is the tile order, as in the pair
 // loop, so results are bit-identical to it.
 constexpr int kSlot = 2 * STAGE * D * 2 + 2 * STAGE * 4;  // Q image, dO image, L2, delta of one 64-row stage
+static_assert(!PRL_ATTN_PIPE || (PRL_ATTN_KV_LDS == 0 && PRL_ATTN_INTERLEAVE && BSTAGE == 2 * TILE &&
+                                 PRL_ATTN_BWD_MINB == 1),
+              "the tile pipelines assume K / V (Q / dO) in registers, 64-row stages, paired tiles and one "
+              "workgroup per CU (3 stage slots = 97.5 KiB of LDS): build those A/B variants with PRL_ATTN_PIPE=0");
 __device__ __forceinline__ void pipe_store(const StageT<BSTAGE>& nq, const StageT<BSTAGE>& nd, float nl, float ndl,
                                            char* slot, int tid) {
   stage_store(nq, slot, tid);
@@ -1262,9 +1269,6 @@ __device__ __forceinline__ int xcd_group_remap(int b, int n, int G) {
 // partials to parts + slot * 2 * 128 * 128), [n_split, n_split + n_kv * Hkv) compute dK/dV of a
 // (key block, kv head) over the whole query-head group, the rest dQ of a (query block, query
 // head), so the lighter dQ workgroups fill the causal tail.
-#ifndef PRL_ATTN_BWD_MINB
-#define PRL_ATTN_BWD_MINB 1  // A/B: 2 = two workgroups per CU (<= 256 registers per lane)
-#endif
 __global__ __launch_bounds__(256, PRL_ATTN_BWD_MINB) void attn_bwd_fused(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
                                                       const __bf16* __restrict__ v, const __bf16* __restrict__ dout,
                                                       const float* __restrict__ lse2, const float* __restrict__ delta,

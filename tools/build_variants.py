@@ -19,12 +19,12 @@ VARIANTS = {
     "f32_wg2": {"PRL_STREAM_F32_WG_PER_CU": "2"},
     "swiglu_u2": {"SWIGLU_UNROLL": "2"},
     "attn_fwd_1wave": {"PRL_ATTN_FWD_MINB": "1"},
-    "attn_serial": {"PRL_ATTN_INTERLEAVE": "0"},
+    "attn_serial": {"PRL_ATTN_PIPE": "0", "PRL_ATTN_INTERLEAVE": "0"},
     "attn_exp_noload": {"PRL_ATTN_EXP_NOLOAD": "1"},
     "attn_exp_noexp": {"PRL_ATTN_EXP_NOEXP": "1"},
     "attn_exp_noload_noexp": {"PRL_ATTN_EXP_NOLOAD": "1", "PRL_ATTN_EXP_NOEXP": "1"},
-    "attn_kv_regs": {"PRL_ATTN_KV_LDS": "0"},
-    "attn_vgpr_form": {"PRL_ATTN_KV_LDS": "1", "__flags__": "-mllvm --amdgpu-mfma-vgpr-form=1"},
+    "attn_kv_regs": {"PRL_ATTN_PIPE": "0", "PRL_ATTN_KV_LDS": "0"},
+    "attn_vgpr_form": {"PRL_ATTN_PIPE": "0", "PRL_ATTN_KV_LDS": "1", "__flags__": "-mllvm --amdgpu-mfma-vgpr-form=1"},
     "norm_dres_early": {"PRL_NORM_WIDE_DRES_EARLY": "1"},
     "norm_grid1536": {"PRL_NORM_GRID": "1536"},
     "norm_grid3072_early": {"PRL_NORM_GRID": "3072", "PRL_NORM_WIDE_DRES_EARLY": "1"},
@@ -42,9 +42,9 @@ VARIANTS = {
     "swiglu_gridstride": {"PRL_SWIGLU_PHASED": "0"},
     "swiglu_phased_wg2": {"PRL_SWIGLU_PHASED": "1", "PRL_SWIGLU_PHASED_WG": "2"},
     "swiglu_rows_phased": {"PRL_SWIGLU_ROWS_PHASED": "1"},
-    "attn_2wg": {"PRL_ATTN_BWD_MINB": "2", "PRL_ATTN_KV_LDS": "2", "PRL_ATTN_INTERLEAVE": "0", "PRL_ATTN_BSTAGE": "32"},
-    "attn_v_lds": {"PRL_ATTN_KV_LDS": "2"},
-    "attn_bstage32": {"PRL_ATTN_INTERLEAVE": "0", "PRL_ATTN_BSTAGE": "32"},
+    "attn_2wg": {"PRL_ATTN_PIPE": "0", "PRL_ATTN_BWD_MINB": "2", "PRL_ATTN_KV_LDS": "2", "PRL_ATTN_INTERLEAVE": "0", "PRL_ATTN_BSTAGE": "32"},
+    "attn_v_lds": {"PRL_ATTN_PIPE": "0", "PRL_ATTN_KV_LDS": "2"},
+    "attn_bstage32": {"PRL_ATTN_PIPE": "0", "PRL_ATTN_INTERLEAVE": "0", "PRL_ATTN_BSTAGE": "32"},
     "phased_nowait": {"PRL_PHASED": "2"},
     "attn_nopipe": {"PRL_ATTN_PIPE": "0"},
     "attn_clock_nopipe": {"PRL_ATTN_CLOCK_PROBE": "1", "PRL_ATTN_PIPE": "0"},
