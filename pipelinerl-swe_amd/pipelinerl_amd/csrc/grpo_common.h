@@ -192,19 +192,52 @@ __device__ __forceinline__ double stat_fold(int i, double acc, double v) {
   return acc + v;
 }
 
-__device__ __forceinline__ TokVals token_values(const KArgs& a, int64_t tok, float lp, float H) {
+// Loads of the per-token inputs (never written by the loss kernels).  VecLd: plain vector loads,
+// any index.  SclLd: a wave-uniform index read through the scalar cache (s_load into SGPRs): no
+// VGPRs, and counted by lgkmcnt, so waiting for it never waits for the row's vector loads in
+// flight (a vector load of a token input behind the row's 19 buffer loads had to wait for all of them).
+struct VecLd {
+  template <typename T>
+  static __device__ __forceinline__ T ld(const T* p, int64_t i) { return p[i]; }
+};
+struct SclLd {
+  template <typename T>
+  static __device__ __forceinline__ T ld(const T* p, int64_t i) {
+    return ((const __attribute__((address_space(4))) T*)p)[i];
+  }
+};
+
+// the per-token inputs token_values reads (rl/__init__.py:212-248)
+struct TokIn {
+  int64_t label;
+  float reward, ref, old, gt, ovf, advsrc;
+};
+template <typename LD>
+__device__ __forceinline__ TokIn tok_in(const KArgs& a, int64_t tok) {
+  TokIn t;
+  t.label = LD::ld(a.labels, tok);
+  t.reward = LD::ld(a.rewards, tok);
+  t.ref = LD::ld(a.ref_lp, tok);
+  t.old = LD::ld(a.old_lp, tok);
+  t.gt = a.group_norm ? LD::ld(a.group_tokens, tok) : 1.0f;
+  t.ovf = a.overlong ? LD::ld(a.overflow, tok) : 0.0f;
+  t.advsrc = a.values != nullptr ? LD::ld(a.values, tok - 1) : LD::ld(a.advantages, tok);  // values unshifted
+  return t;
+}
+
+__device__ __forceinline__ TokVals token_values(const KArgs& a, const TokIn& in, float lp, float H) {
   TokVals v;
-  v.m = a.labels[tok] != -100;
-  const float reward = a.rewards[tok];
-  const float ref = a.ref_lp[tok];
-  const float old = a.old_lp[tok];
+  v.m = in.label != -100;
+  const float reward = in.reward;
+  const float ref = in.ref;
+  const float old = in.old;
   const bool has_v = a.values != nullptr;
-  float w = a.group_norm ? 1.0f / a.group_tokens[tok] : 1.0f / a.batch_size;  // :220-225
-  if (a.overlong) w = w * (1.0f - a.overflow[tok]);                            // :227-230
+  float w = a.group_norm ? 1.0f / in.gt : 1.0f / a.batch_size;  // :220-225
+  if (a.overlong) w = w * (1.0f - in.ovf);                      // :227-230
   v.w = w;
   v.ratio = expf(lp - old);  // :234-236
   v.lrrn = ref - lp;
-  v.adv = has_v ? reward - a.values[tok - 1] : a.advantages[tok];  // :239-248 (values unshifted)
+  v.adv = has_v ? reward - in.advsrc : in.advsrc;  // :239-248
   float lpw = a.use_adv ? v.adv : reward;                          // :250-252
   if (a.relu) lpw = lpw < 0.f ? 0.f : lpw;
   v.lpw = lpw;
@@ -228,6 +261,9 @@ __device__ __forceinline__ TokVals token_values(const KArgs& a, int64_t tok, flo
   }
   v.tl = ((v.pol - a.kl_c * v.kl) + a.ent_c * H) * w;  // :286-290
   return v;
+}
+__device__ __forceinline__ TokVals token_values(const KArgs& a, int64_t tok, float lp, float H) {
+  return token_values(a, tok_in<VecLd>(a, tok), lp, H);
 }
 
 // d final / d new_lp and d final / d entropy for one row (analytic backward with torch's
@@ -273,9 +309,10 @@ __device__ __forceinline__ void row_of(const KArgs& a, int64_t q, int64_t& lrow,
 __device__ __forceinline__ int64_t fwd_rows(const KArgs& a) { return a.row_ids ? a.nsel : a.B * (a.L - 1); }
 
 // logits row i -> (logits row offset, token index, output row q)
+template <typename LD = VecLd>
 __device__ __forceinline__ void map_row(const KArgs& a, int64_t i, int64_t& lrow, int64_t& tok, int64_t& q) {
   if (a.row_ids) {
-    q = a.row_ids[i];
+    q = LD::ld(a.row_ids, i);
     int64_t full;
     row_of(a, q, full, tok);
     lrow = i;

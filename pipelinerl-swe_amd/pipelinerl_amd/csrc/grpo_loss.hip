@@ -54,9 +54,9 @@ __device__ __forceinline__ Lse block_combine(const float (*red)[3], float c) {
 
 // per-row epilogue shared by the forward kernels: every lane computes the (uniform) token
 // values and gradient coefficients; `writer` stores the per-row outputs.
-__device__ __forceinline__ TokGrad row_epilogue(const KArgs& a, int64_t q, int64_t tok, float lp,
+__device__ __forceinline__ TokGrad row_epilogue(const KArgs& a, int64_t q, const TokIn& tin, float lp,
                                                 float H, float lse, float m, float l2s, bool writer) {
-  const TokVals v = token_values(a, tok, lp, H);
+  const TokVals v = token_values(a, tin, lp, H);
   const TokGrad g = token_grad(a, v);
   if (writer) {
     a.o_lp[q] = lp;
@@ -71,18 +71,56 @@ __device__ __forceinline__ TokGrad row_epilogue(const KArgs& a, int64_t q, int64
   return g;
 }
 
+#ifndef PRL_SCALAR_ROW_INPUTS
+#define PRL_SCALAR_ROW_INPUTS 1  // 0: the round-1..3 vector loads (A/B: tools/build_variants.py vec_row_inputs)
+#endif
+#if PRL_SCALAR_ROW_INPUTS
+using RowLd = SclLd;
+#else
+using RowLd = VecLd;
+#endif
+
+// the target logit of a row, read through the scalar cache as the aligned dword holding it (no
+// 16-bit scalar load on gfx950; rows of the streaming kernels may start 2-B aligned); j must be a
+// valid column
+__device__ __forceinline__ float row_logit_scl(const uint16_t* row, int64_t j) {
+  const uintptr_t ad = reinterpret_cast<uintptr_t>(row + j);
+  const uint32_t w = SclLd::ld(reinterpret_cast<const uint32_t*>(ad & ~(uintptr_t)3), 0);
+  return __uint_as_float((ad & 2) ? (w & 0xffff0000u) : (w << 16));
+}
+__device__ __forceinline__ float row_logit_scl(const float* row, int64_t j) { return SclLd::ld(row, j); }
+__device__ __forceinline__ float row_logit(const uint16_t* row, int64_t j) {
+  return PRL_SCALAR_ROW_INPUTS ? row_logit_scl(row, j) : bf_to_f(row[j]);
+}
+__device__ __forceinline__ float row_logit(const float* row, int64_t j) {
+  return PRL_SCALAR_ROW_INPUTS ? row_logit_scl(row, j) : row[j];
+}
+
+// Pin scalar-loaded row inputs to this point of the program: the scheduler otherwise sinks the
+// s_loads to their first use after the row reduction and waits for them in front of the barrier.
+// Here (the row's vector loads just issued) the wait costs nothing: pass 1 waits for the row anyway.
+__device__ __forceinline__ void pin_sgpr(TokIn& t, float& x) {
+  if constexpr (PRL_SCALAR_ROW_INPUTS)
+    asm volatile("" : "+s"(t.label), "+s"(t.reward), "+s"(t.ref), "+s"(t.old), "+s"(t.gt), "+s"(t.ovf),
+                 "+s"(t.advsrc), "+s"(x));
+}
+
 // buffer descriptor over one row (wave-uniform inputs only); out-of-range lanes read 0 and
 // their stores are dropped by the hardware bounds check
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void* p, int64_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
 }
-// cache policy of the row stream (aux bits of buffer_load/store: 2 = nt).  The logits and
-// dlogits are touched once per launch; the build can override for A/B experiments.
+// cache policy of the row stream (aux bits of buffer_load/store on gfx950: 1 = sc0, 2 = nt,
+// 16 = sc1).  The logits and dlogits are touched once per launch; the build can override for A/B
+// experiments.  Stores are nt sc1 (round 3): an sc1 store drops its line from the XCD's L2 instead
+// of keeping it dirty there, so the dlogits stream does not evict through L2 write-backs; alternated
+// on two boxes, 7.11 -> 6.97 and 7.40 -> 7.35 ms per C2 launch against nt alone (sc1 without nt,
+// and sc0 sc1, were slower; the load policy made no difference: profiles/r03_loss_cache_policy_ab.jsonl).
 #ifndef PRL_LOAD_AUX
 #define PRL_LOAD_AUX 2
 #endif
 #ifndef PRL_STORE_AUX
-#define PRL_STORE_AUX 2
+#define PRL_STORE_AUX 18
 #endif
 constexpr int kLoadAux = PRL_LOAD_AUX;
 constexpr int kStoreAux = PRL_STORE_AUX;
@@ -170,12 +208,19 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
   }
   int par = 0;
   for (; q < nrows; q += gridDim.x, par ^= 1) {
+    // The row's token inputs and its target logit come through the scalar cache while the row's
+    // vector loads are in flight: nothing here waits for them, and the epilogue after the
+    // barrier finds its inputs in SGPRs (with vector loads this was a chain of four waits per
+    // row, each for every load outstanding on the CU).
     int64_t lrow, tok, qo;
-    map_row(a, perm_row(q, nrows), lrow, tok, qo);
-    const int64_t tid_raw = a.input_ids[tok];
+    map_row<RowLd>(a, perm_row(q, nrows), lrow, tok, qo);
+    const int64_t tid_raw = RowLd::ld(a.input_ids, tok);
+    TokIn tin = tok_in<RowLd>(a, tok);
     const bool bad_id = (uint64_t)tid_raw >= (uint64_t)a.V;
     const int64_t tgt = bad_id ? -1 : tid_raw;  // -1: never matches a column below
-    const float xt = bad_id ? __builtin_nanf("") : bf_to_f(lg[lrow * a.ld + tgt]);
+    float xr = row_logit(lg + lrow * a.ld, bad_id ? 0 : tid_raw);
+    pin_sgpr(tin, xr);  // issue (and land) them here, not in front of the barrier
+    const float xt = bad_id ? __builtin_nanf("") : xr;
 
     // ---- pass 1: row statistics from registers
     Lse st = lse_empty();
@@ -204,7 +249,7 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
     const float lse = M * inv_t + kLn2 * l2s;
     const float H = kLn2 * (l2s - tot.w / tot.s);
     const float lp = (xt - M) * inv_t - kLn2 * l2s;
-    const TokGrad core = row_epilogue(a, qo, tok, lp, H, lse, M, l2s, tid == 0);
+    const TokGrad core = row_epilogue(a, qo, tin, lp, H, lse, M, l2s, tid == 0);
     // Make the packed row opaque here so the compiler re-unpacks it in pass 2 instead of
     // keeping pass 1's unpacked floats alive (8 instead of 4 VGPRs per vector -> spills).
 #pragma unroll
@@ -216,7 +261,7 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
     int64_t nlrow = lrow;
     if (has_next) {
       int64_t nt, nq;
-      map_row(a, perm_row(qn, nrows), nlrow, nt, nq);
+      map_row<RowLd>(a, perm_row(qn, nrows), nlrow, nt, nq);
     }
     const auto rn = row_rsrc(lg + nlrow * a.ld, has_next ? row_bytes : 0);
     if (a.write_grad) {
@@ -321,12 +366,6 @@ struct RowIO<float, 1> {
   static __device__ __forceinline__ void store(float* row, int64_t gv, const float (&d)[1]) { row[gv] = d[0]; }
 };
 
-template <typename T>
-__device__ __forceinline__ float scalar_logit(const T* row, int64_t j);
-template <>
-__device__ __forceinline__ float scalar_logit<uint16_t>(const uint16_t* row, int64_t j) { return bf_to_f(row[j]); }
-template <>
-__device__ __forceinline__ float scalar_logit<float>(const float* row, int64_t j) { return row[j]; }
 
 // gradient of one vector: d_j = p_j (alpha + beta t_j) (+ gadd at the target column)
 template <int VEC>
@@ -365,12 +404,14 @@ __global__ __launch_bounds__(BLOCK) void grpo_fwd_stream(KArgs a) {
   int par = 0;
   for (int64_t i = blockIdx.x; i < nrows; i += gridDim.x, par ^= 1) {
     int64_t lrow, tok, q;
-    map_row(a, i, lrow, tok, q);
+    map_row<RowLd>(a, i, lrow, tok, q);
     const T* row = lg + lrow * a.ld;
-    const int64_t tid_raw = a.input_ids[tok];
+    const int64_t tid_raw = RowLd::ld(a.input_ids, tok);
+    const TokIn tin = tok_in<RowLd>(a, tok);
     const bool bad_id = (uint64_t)tid_raw >= (uint64_t)a.V;
     const int64_t tgt = bad_id ? -1 : tid_raw;
-    const float xt = bad_id ? __builtin_nanf("") : scalar_logit<T>(row, tgt);
+    const float xr = row_logit(row, bad_id ? 0 : tid_raw);
+    const float xt = bad_id ? __builtin_nanf("") : xr;
     Lse st = lse_empty();
     int64_t gv = tid;
     for (; gv + (U - 1) * BLOCK < nvec; gv += U * BLOCK) {
@@ -398,7 +439,7 @@ __global__ __launch_bounds__(BLOCK) void grpo_fwd_stream(KArgs a) {
     const float lse = M * inv_t + kLn2 * l2s;
     const float H = kLn2 * (l2s - tot.w / tot.s);
     const float lp = (xt - M) * inv_t - kLn2 * l2s;
-    const TokGrad core = row_epilogue(a, q, tok, lp, H, lse, M, l2s, tid == 0);
+    const TokGrad core = row_epilogue(a, q, tin, lp, H, lse, M, l2s, tid == 0);
     if (a.write_grad) {
       T* drow = dl + lrow * a.ld;
       const float alpha = -(core.g_lp + core.g_h * H) * inv_t;

@@ -7,7 +7,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "pipelinerl-swe_amd
 from pipelinerl_amd._build import build, build_variant  # noqa: E402
 
 VARIANTS = {
-    "ld_nt_st_nt": {"PRL_LOAD_AUX": "2", "PRL_STORE_AUX": "2"},
+    "ld_nt_st_nt": {"PRL_LOAD_AUX": "2", "PRL_STORE_AUX": "2"},  # the round-1..3 default
     "ld_def_st_nt": {"PRL_LOAD_AUX": "0", "PRL_STORE_AUX": "2"},
     "ld_nt_st_def": {"PRL_LOAD_AUX": "2", "PRL_STORE_AUX": "0"},
     "ld_def_st_def": {"PRL_LOAD_AUX": "0", "PRL_STORE_AUX": "0"},
@@ -50,6 +50,14 @@ VARIANTS = {
     "attn_clock_nopipe": {"PRL_ATTN_CLOCK_PROBE": "1", "PRL_ATTN_PIPE": "0"},
     "attn_pipe_sgb": {"PRL_ATTN_PIPE_SCHED": "0"},
     "attn_pipe_lead6": {"PRL_ATTN_PIPE_LEAD": "6"},
+    "vec_row_inputs": {"PRL_SCALAR_ROW_INPUTS": "0"},
+    "st_sc1": {"PRL_STORE_AUX": "16"},
+    "st_sc1_nt": {"PRL_STORE_AUX": "18"},
+    "st_sc0_sc1": {"PRL_STORE_AUX": "17"},
+    "st_sc0_sc1_nt": {"PRL_STORE_AUX": "19"},
+    "ld_sc1_nt_st_sc1_nt": {"PRL_LOAD_AUX": "18", "PRL_STORE_AUX": "18"},
+    "ld_sc1_st_sc1_nt": {"PRL_LOAD_AUX": "16", "PRL_STORE_AUX": "18"},
+    "ld_def_st_sc1_nt": {"PRL_LOAD_AUX": "0", "PRL_STORE_AUX": "18"},
 }
 
 if __name__ == "__main__":
