@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
 #include <utility>
 
 #include "grpo_common.h"
@@ -159,6 +160,12 @@ __device__ __forceinline__ void store_row_b128(u32x4 o, __amdgpu_buffer_rsrc_t r
 // on the GPU (tests/test_grpo_edge_gpu.py::test_vocab_size_limits; the interleaved schedule
 // passes it; cause not found), so rows that large keep the interleaved schedule.  Qwen2.5's
 // vocabularies are NV = 19, covered by tests/test_grpo_edge_gpu.py::test_multi_row_per_workgroup.
+#ifndef PRL_TARGET_FIXUP
+#define PRL_TARGET_FIXUP 1
+#endif
+#ifndef PRL_NOENT_FORM
+#define PRL_NOENT_FORM 1  // beta == 0 rows (no entropy term) take the form without it
+#endif
 #ifndef PRL_PHASED_MAX_NV
 #define PRL_PHASED_MAX_NV 20
 #endif
@@ -184,6 +191,16 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
   constexpr int BLOCK = 1024, NW = BLOCK / 64;
   constexpr int VSTRIDE = BLOCK * 16;  // bytes between a lane's consecutive vectors
   constexpr bool kPhased = PRL_PHASED != 0 && NV <= kPhasedMaxNV;
+  // The target column's extra g_lp/temperature term: the owner lane rewrites that one element
+  // after the row's stores retired (phased schedule), instead of 8 selects per vector in every
+  // lane (190 v_cndmask per row and wave in the ISA).
+  constexpr bool kTargetFixup = PRL_TARGET_FIXUP != 0 && kPhased && PRL_PHASED == 1;
+  constexpr bool kNoEntropyForm = PRL_NOENT_FORM != 0;
+#ifdef PRL_COPY_CEILING
+  constexpr bool kCopyCeiling = true;
+#else
+  constexpr bool kCopyCeiling = false;
+#endif
   __shared__ float red[2][NW][3];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int64_t nrows = fwd_rows(a);
@@ -274,40 +291,97 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
       const int kt = tv < 0 ? -1 : tv / BLOCK;
       const int lt = tv - (kt < 0 ? 0 : kt) * BLOCK;
       const bool zero_row = (core.g_lp == 0.f && core.g_h == 0.f);
+      // The row's stores, in one of three forms chosen per row (wave-uniform, so each form is its
+      // own unrolled loop): kMode 0 a zero row, 1 no entropy term (beta == 0: the reference's default
+      // entropy_bonus 0, one packed FMA fewer per element pair), 2 the general form.  Forms 1 and 2
+      // agree bit for bit where beta == 0 but for the sign of a zero.
+      auto row_pass = [&](auto mode) {
+        constexpr int kMode = decltype(mode)::value;
 #pragma unroll
-      for (int k = 0; k < NV; ++k) {
-        u32x4 o;
-#ifdef PRL_COPY_CEILING
-        if (true) {  // structural ceiling experiment: same traffic and schedule, no gradient math
-          o = buf[k];
-        } else
-#endif
-        if (zero_row) {
-          o = u32x4{0u, 0u, 0u, 0u};
-        } else {
-          float d[8];
+        for (int k = 0; k < NV; ++k) {
+          u32x4 o;
+          if constexpr (kCopyCeiling) {  // structural ceiling experiment: same traffic and schedule, no gradient math
+            o = buf[k];
+          } else if constexpr (kMode == 0) {
+            o = u32x4{0u, 0u, 0u, 0u};
+          } else {
+            float d[8];
+            // opaque per form, so the unpack shared by forms 1 and 2 is not hoisted above the
+            // form branch (8 instead of 4 live VGPRs per vector: spills)
+            u32x4 v = buf[k];
+            asm volatile("" : "+v"(v));
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const float x0 = bf_lo(buf[k][j]), x1 = bf_hi(buf[k][j]);
-            const float t0 = __builtin_fmaf(x0 - M, c, -l2s), t1 = __builtin_fmaf(x1 - M, c, -l2s);
-            const float p0 = fexp2(t0), p1 = fexp2(t1);
-            d[2 * j] = p0 * __builtin_fmaf(beta, t0, alpha);
-            d[2 * j + 1] = p1 * __builtin_fmaf(beta, t1, alpha);
+            for (int j = 0; j < 4; ++j) {
+              const float x0 = bf_lo(v[j]), x1 = bf_hi(v[j]);
+              const float t0 = __builtin_fmaf(x0 - M, c, -l2s), t1 = __builtin_fmaf(x1 - M, c, -l2s);
+              const float p0 = fexp2(t0), p1 = fexp2(t1);
+              if constexpr (kMode == 1) {
+                d[2 * j] = p0 * alpha;
+                d[2 * j + 1] = p1 * alpha;
+              } else {
+                d[2 * j] = p0 * __builtin_fmaf(beta, t0, alpha);
+                d[2 * j + 1] = p1 * __builtin_fmaf(beta, t1, alpha);
+              }
+            }
+            if constexpr (!kTargetFixup) {
+              if (k == kt && tid == lt) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) d[j] += (j == te) ? gadd : 0.f;
+              }
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(d[2 * j], d[2 * j + 1]);
           }
-          if (k == kt && tid == lt) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) d[j] += (j == te) ? gadd : 0.f;
-          }
-#pragma unroll
-          for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(d[2 * j], d[2 * j + 1]);
+          store_row_b128(o, ws, voff, k * VSTRIDE);
         }
-        store_row_b128(o, ws, voff, k * VSTRIDE);
-        if constexpr (!kPhased)
+      };
+      if constexpr (!kPhased) {
+        // interleaved schedule (NV > 20): one form (three forms spill there), the next row's
+        // vector k loaded right behind the store of vector k
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+          u32x4 o;
+          if (zero_row) {
+            o = u32x4{0u, 0u, 0u, 0u};
+          } else {
+            float d[8];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const float x0 = bf_lo(buf[k][j]), x1 = bf_hi(buf[k][j]);
+              const float t0 = __builtin_fmaf(x0 - M, c, -l2s), t1 = __builtin_fmaf(x1 - M, c, -l2s);
+              const float p0 = fexp2(t0), p1 = fexp2(t1);
+              d[2 * j] = p0 * __builtin_fmaf(beta, t0, alpha);
+              d[2 * j + 1] = p1 * __builtin_fmaf(beta, t1, alpha);
+            }
+            if (k == kt && tid == lt) {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) d[j] += (j == te) ? gadd : 0.f;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(d[2 * j], d[2 * j + 1]);
+          }
+          store_row_b128(o, ws, voff, k * VSTRIDE);
           buf[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rn, voff, k * VSTRIDE, kLoadAux));
-      }
+        }
+      } else if (zero_row)
+        row_pass(std::integral_constant<int, 0>{});
+      else if (kNoEntropyForm && beta == 0.f)
+        row_pass(std::integral_constant<int, 1>{});
+      else
+        row_pass(std::integral_constant<int, 2>{});
       if constexpr (kPhased) {
         // the whole row's stores retire before the next row's loads start (PRL_PHASED above)
         if constexpr (PRL_PHASED == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if constexpr (kTargetFixup) {
+          // the target column's g_lp term, by its one owner lane after the row's stores retired
+          // (so this 2-B store lands after the 16-B store of the same bytes): the same operations
+          // as the vector loop on the same bf16 value, rounded the same way (no contraction)
+          if (tid == lt && !zero_row) {
+            const float tt = __builtin_fmaf(xt - M, c, -l2s);
+            const float dm = __fmul_rn(fexp2(tt), beta == 0.f ? alpha : __builtin_fmaf(beta, tt, alpha));
+            dl[lrow * a.ld + tgt] = f_to_bf(__fadd_rn(dm, gadd));
+          }
+        }
         if (has_next) {
 #pragma unroll
           for (int k = 0; k < NV; ++k)

@@ -51,6 +51,8 @@ VARIANTS = {
     "attn_pipe_sgb": {"PRL_ATTN_PIPE_SCHED": "0"},
     "attn_pipe_lead6": {"PRL_ATTN_PIPE_LEAD": "6"},
     "vec_row_inputs": {"PRL_SCALAR_ROW_INPUTS": "0"},
+    "target_select": {"PRL_TARGET_FIXUP": "0"},
+    "noent_form_off": {"PRL_NOENT_FORM": "0"},
     "st_sc1": {"PRL_STORE_AUX": "16"},
     "st_sc1_nt": {"PRL_STORE_AUX": "18"},
     "st_sc0_sc1": {"PRL_STORE_AUX": "17"},
