@@ -177,3 +177,26 @@ def test_multi_row_per_workgroup():
     _, d1 = _cmp(lg, b)
     _, _, d2 = _run(lg, b)
     assert np.array_equal(d1, d2)
+
+
+@pytest.mark.parametrize("ent", [0.0, 0.01])
+def test_target_columns_at_vector_edges(ent):
+    """Targets on the edges of the register-resident row layout (Qwen2.5's V = 151 936: 19 vectors
+    per lane, the last one partial): the target term is added by the owner lane after the row's
+    stores (PRL_TARGET_FIXUP), and entropy 0 takes the form without the entropy term."""
+    T, V = 12, 151936
+    b = _batch(T, V, seed=7, lens=[T], prompts=[1])
+    cols = [0, 1, 7, 8, 8191, 8192, 147455, 147456, 147457, V - 8, V - 1]
+    for r, col in enumerate(cols):
+        b["input_ids"][0, 1 + r] = col
+        if b["labels"][0, 1 + r] != -100:
+            b["labels"][0, 1 + r] = col
+    lg = synth.to_bf16(np.random.default_rng(7).normal(0, 2, (1, T, V))).astype(np.float32)
+    cfg = dict(CFG, entropy_bonus=ent, final_entropy_bonus=ent)
+    _, d = _cmp(lg, b, cfg)
+    o = grpo_oracle.rl_step_oracle(lg, b, cfg, 0, 10)
+    rows = [r for r in range(len(cols)) if b["labels"][0, 1 + r] != -100]
+    assert len(rows) >= 8
+    for r in rows:
+        got, want = d[0, r, cols[r]], o["dlogits"][0, r, cols[r]]
+        assert abs(got - want) <= 1e-2 * abs(want) + 1e-8, (r, cols[r], got, want)
