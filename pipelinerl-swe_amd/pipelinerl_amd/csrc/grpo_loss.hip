@@ -156,10 +156,10 @@ __device__ __forceinline__ void store_row_b128(u32x4 o, __amdgpu_buffer_rsrc_t r
 #define PRL_PHASED 1
 #endif
 // The phased schedule keeps pass 2's gradient vectors and the row in registers at once: above
-// NV = 20 (V > 163 840) it spills row vectors to scratch, and at NV = 24 its dlogits were wrong
-// on the GPU (tests/test_grpo_edge_gpu.py::test_vocab_size_limits; the interleaved schedule
-// passes it; cause not found), so rows that large keep the interleaved schedule.  Qwen2.5's
-// vocabularies are NV = 19, covered by tests/test_grpo_edge_gpu.py::test_multi_row_per_workgroup.
+// NV = 20 (V > 163 840) it spills row vectors to scratch, so rows that large keep the interleaved
+// schedule.  (Its round-2 wrong dlogits at NV = 24 were the store-data hazard fenced in
+// store_row_b128 below; both schedules are correct at every NV since.)  Qwen2.5's vocabularies are
+// NV = 19, covered by tests/test_grpo_edge_gpu.py::test_multi_row_per_workgroup.
 #ifndef PRL_TARGET_FIXUP
 #define PRL_TARGET_FIXUP 1
 #endif
