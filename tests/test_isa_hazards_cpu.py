@@ -46,3 +46,33 @@ def test_scanner_finds_the_unfenced_store():
     fns = {h["function"] for h in hits}
     assert any("grpo_fwd_residentILi24E" in f for f in fns), fns
     assert all(h["soffset_sgpr"] for h in hits)
+
+
+def _function(isa: str, name: str) -> str:
+    start = isa.index(f"\n{name}:")
+    return isa[start:isa.index("s_endpgm", start)]
+
+
+def test_resident_loss_head_reads_row_inputs_through_the_scalar_cache():
+    """Round-3 schedule guard for grpo_fwd_resident<19> (Qwen2.5's vocabulary): the row's token
+    inputs and target logit are scalar loads, so the only vector loads are the row's own 16-B buffer
+    loads and no `s_waitcnt vmcnt(0)` sits between a row's first load and its stores (the vector
+    version waited for the whole row, then for a dependent target-logit load, then for the
+    epilogue's inputs); the target column is one 2-B store after the row's stores; the dlogits
+    are stored nt sc1.  (The vector-load build, PRL_SCALAR_ROW_INPUTS=0, has 10 global loads in
+    this function and 2 vmcnt waits between the barrier and the first store: it fails here.)"""
+    from isa_store_hazard_scan import compile_isa
+
+    isa = compile_isa(CSRC / "grpo_loss.hip", {}, include=[ROOT / "include", CSRC])
+    fn = _function(isa, "_ZN3prl17grpo_fwd_residentILi19EEEvNS_5KArgsE")
+    lines = [ln.strip() for ln in fn.splitlines()]
+    vloads = [ln for ln in lines if ln.startswith(("global_load", "flat_load", "buffer_load"))]
+    assert vloads and all(ln.startswith("buffer_load_dwordx4") for ln in vloads), vloads[:4]
+    assert any(ln.startswith("s_load_dwordx2") for ln in lines) and any(ln.startswith("s_load_dword ") for ln in lines)
+    stores = [ln for ln in lines if ln.startswith("buffer_store_dwordx4")]
+    assert stores and all(ln.endswith("nt sc1") for ln in stores), stores[:2]
+    assert sum(ln.startswith("global_store_short") for ln in lines) == 1
+    # between the barrier and the first row store: no wait on vector memory
+    b = next(i for i, ln in enumerate(lines) if ln.startswith("s_barrier"))
+    s = next(i for i, ln in enumerate(lines) if ln.startswith("buffer_store_dwordx4"))
+    assert b < s and not any(ln.startswith("s_waitcnt vmcnt") for ln in lines[b:s]), lines[b:s][:5]
