@@ -1408,11 +1408,26 @@ __device__ __forceinline__ void fwd_tile(const char* tK, const char* tV, int k0,
     for (int ks = 0; ks < 2; ++ks) Ot[dc] = mfma(tr_operand(tV, lane, dc, ks), pb[ks], Ot[dc]);
 }
 
+#ifndef PRL_ATTN_FWD_DMA
+#define PRL_ATTN_FWD_DMA 1
+#endif
+#if PRL_ATTN_FWD_DMA && !PRL_ATTN_PIPE
+#error "PRL_ATTN_FWD_DMA uses the pipeline's LDS-DMA stage loads (PRL_ATTN_PIPE)"
+#endif
 __global__ __launch_bounds__(256, PRL_ATTN_FWD_MINB) void attn_fwd(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
                                                 const __bf16* __restrict__ v, const int32_t* __restrict__ items,
                                                 __bf16* __restrict__ out, float* __restrict__ lse2, int64_t T, int H,
                                                 int Hkv, float c2) {
+#if PRL_ATTN_FWD_DMA
+  // two K/V stage slots (64 KiB per workgroup, two workgroups per CU) filled by LDS-DMA one stage
+  // ahead: one barrier per stage, no staging registers, no store pass.  Two separate arrays and a
+  // loop unrolled by two, so every stage reads one array while the next stage's DMA writes the other
+  // and the compiler can tell them apart (with one runtime-indexed array it waited for the in-flight
+  // DMA, vmcnt(0), before the stage's first transposed read).
+  __shared__ __attribute__((aligned(16))) char sKVa[2 * STAGE * D * 2], sKVb[2 * STAGE * D * 2];
+#else
   __shared__ __attribute__((aligned(16))) char sK[STAGE * D * 2], sV[STAGE * D * 2];
+#endif
   const int tid = threadIdx.x;
   const int lb = xcd_group_remap(blockIdx.x, gridDim.x, H / Hkv);
   const int it = lb / H, h = lb % H;
@@ -1431,6 +1446,39 @@ __global__ __launch_bounds__(256, PRL_ATTN_FWD_MINB) void attn_fwd(const __bf16*
   for (int i = 0; i < 4; ++i) Ot[i] = f32x16{};
   float m = -1e30f, l = 0.f;  // running max (base-2 units) and sum for query qq
   const int kend = (qb + 128 < s1 ? qb + 128 : s1);
+  // the stage's two 32-key tiles (keys k00 .. k00 + 63) from the K / V images in LDS
+  auto tiles = [&](int k00, const char* sK, const char* sV) {
+#pragma unroll
+    for (int half = 0; half < STAGE / TILE; ++half) {
+      const int k0 = k00 + TILE * half;
+      if (qw >= s1 || k0 > qw + TILE - 1 || k0 >= kend) continue;  // wave-uniform
+      // every key of the tile visible to every query of the wave: the unmasked body (all but the
+      // diagonal tile of each wave); wave-uniform, two separate code paths
+      if (k0 + TILE - 1 <= qw && k0 + TILE <= s1)
+        fwd_tile<false>(sK + half * TILE * 256, sV + half * TILE * 256, k0, qf, qq, qval, s1, lane, c2, m, l, Ot);
+      else
+        fwd_tile<true>(sK + half * TILE * 256, sV + half * TILE * 256, k0, qf, qq, qval, s1, lane, c2, m, l, Ot);
+    }
+  };
+#if PRL_ATTN_FWD_DMA
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  int dvo[4];
+  dma_lane_offsets(rsk, wu, lane, dvo);
+  stage_dma_kv(k, v, rsk, g, s0, s1, sKVa, dvo, wu);
+  auto stage = [&](int k00, const char* cur, char* nxt) {
+    // this wave's DMA of the stage landed (vmcnt), then every wave's (barrier); every wave is also
+    // done with the other array's stage, which the next DMA overwrites
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (k00 + STAGE < kend) stage_dma_kv(k, v, rsk, g, k00 + STAGE, s1, nxt, dvo, wu);
+    sched_fence();
+    tiles(k00, cur, cur + STAGE * D * 2);
+  };
+  for (int k00 = s0; k00 < kend; k00 += 2 * STAGE) {
+    stage(k00, sKVa, sKVb);
+    if (k00 + STAGE < kend) stage(k00 + STAGE, sKVb, sKVa);
+  }
+#else
   const int vb = stage_vbase(rsk, g, tid);
   Stage nk = stage_load_rows(k, rsk, g, s0, s1, tid, vb), nv = stage_load_rows(v, rsk, g, s0, s1, tid, vb);
   for (int k00 = s0; k00 < kend; k00 += STAGE) {
@@ -1442,18 +1490,9 @@ __global__ __launch_bounds__(256, PRL_ATTN_FWD_MINB) void attn_fwd(const __bf16*
       nk = stage_load_rows(k, rsk, g, k00 + STAGE, s1, tid, vb);
       nv = stage_load_rows(v, rsk, g, k00 + STAGE, s1, tid, vb);
     }
-#pragma unroll 1
-    for (int half = 0; half < STAGE / TILE; ++half) {
-      const int k0 = k00 + TILE * half;
-      if (qw >= s1 || k0 > qw + TILE - 1 || k0 >= kend) continue;  // wave-uniform
-      // every key of the tile visible to every query of the wave: the unmasked body (all but the
-      // diagonal tile of each wave); wave-uniform, two separate code paths
-      if (k0 + TILE - 1 <= qw && k0 + TILE <= s1)
-        fwd_tile<false>(sK + half * TILE * 256, sV + half * TILE * 256, k0, qf, qq, qval, s1, lane, c2, m, l, Ot);
-      else
-        fwd_tile<true>(sK + half * TILE * 256, sV + half * TILE * 256, k0, qf, qq, qval, s1, lane, c2, m, l, Ot);
-    }
+    tiles(k00, sK, sV);
   }
+#endif
   if (!qval) return;
   const float inv = 1.0f / l;
   __bf16* orow = out + (int64_t)qq * rs + h * D;
