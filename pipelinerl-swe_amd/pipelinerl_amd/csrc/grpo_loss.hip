@@ -83,7 +83,8 @@ using RowLd = VecLd;
 
 // the target logit of a row, read through the scalar cache as the aligned dword holding it (no
 // 16-bit scalar load on gfx950; rows of the streaming kernels may start 2-B aligned); j must be a
-// valid column
+// valid column.  The dword can reach 2 B past the tensor's last element (odd V, last row), never
+// past the 4-B-aligned granule holding it, so never into an unmapped page.
 __device__ __forceinline__ float row_logit_scl(const uint16_t* row, int64_t j) {
   const uintptr_t ad = reinterpret_cast<uintptr_t>(row + j);
   const uint32_t w = SclLd::ld(reinterpret_cast<const uint32_t*>(ad & ~(uintptr_t)3), 0);
