@@ -1414,6 +1414,60 @@ __device__ __forceinline__ void fwd_tile(const char* tK, const char* tV, int k0,
 #if PRL_ATTN_FWD_DMA && !PRL_ATTN_PIPE
 #error "PRL_ATTN_FWD_DMA uses the pipeline's LDS-DMA stage loads (PRL_ATTN_PIPE)"
 #endif
+#ifndef PRL_ATTN_FWD_PAIR
+#define PRL_ATTN_FWD_PAIR 1
+#endif
+// both 32-key tiles of a stage every key of which is visible to every query of the wave: S of both
+// tiles (16 MFMAs back to back), one running-max / lazy-rescale decision over the 64 keys (one
+// cross-half exchange instead of two), then both tiles' P and O^T += V^T P (16 MFMAs).  Same
+// arithmetic per element as fwd_tile; the rescale points can differ (decided per 64 keys), so the
+// results match the per-tile form to rounding, not bit for bit.
+__device__ __forceinline__ void fwd_pair(const char* tK, const char* tV, const bf16x8* qf, int lane, float c2, float& m,
+                                         float& l, f32x16* Ot) {
+  const int hi = lane >> 5, l32 = lane & 31;
+  f32x16 Sa = f32x16{}, Sb = f32x16{};
+#pragma unroll
+  for (int c = 0; c < 8; ++c) Sa = mfma(row_read(tK, l32, 2 * c + hi), qf[c], Sa);
+#pragma unroll
+  for (int c = 0; c < 8; ++c) Sb = mfma(row_read(tK + TILE * 256, l32, 2 * c + hi), qf[c], Sb);
+  float tmax = fmaxf(Sa[0], Sb[0]);
+#pragma unroll
+  for (int r = 1; r < 16; ++r) tmax = fmaxf(tmax, fmaxf(Sa[r], Sb[r]));
+  tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * c2;
+  if (tmax > m + kRescale) {
+    const float f = fexp2(m - tmax);
+    l *= f;
+#pragma unroll
+    for (int dc = 0; dc < 4; ++dc)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) Ot[dc][r] *= f;
+    m = tmax;
+  }
+  bf16x8 pa[2], pb[2];
+  float ps = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float p = fexp2(__builtin_fmaf(Sa[r], c2, -m));
+    ps += p;
+    pa[r >> 3][r & 7] = (__bf16)p;
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float p = fexp2(__builtin_fmaf(Sb[r], c2, -m));
+    ps += p;
+    pb[r >> 3][r & 7] = (__bf16)p;
+  }
+  l += ps + __shfl_xor(ps, 32, 64);
+#pragma unroll
+  for (int dc = 0; dc < 4; ++dc)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) Ot[dc] = mfma(tr_operand(tV, lane, dc, ks), pa[ks], Ot[dc]);
+#pragma unroll
+  for (int dc = 0; dc < 4; ++dc)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) Ot[dc] = mfma(tr_operand(tV + TILE * 256, lane, dc, ks), pb[ks], Ot[dc]);
+}
+
 __global__ __launch_bounds__(256, PRL_ATTN_FWD_MINB) void attn_fwd(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
                                                 const __bf16* __restrict__ v, const int32_t* __restrict__ items,
                                                 __bf16* __restrict__ out, float* __restrict__ lse2, int64_t T, int H,
@@ -1448,6 +1502,10 @@ __global__ __launch_bounds__(256, PRL_ATTN_FWD_MINB) void attn_fwd(const __bf16*
   const int kend = (qb + 128 < s1 ? qb + 128 : s1);
   // the stage's two 32-key tiles (keys k00 .. k00 + 63) from the K / V images in LDS
   auto tiles = [&](int k00, const char* sK, const char* sV) {
+    if (PRL_ATTN_FWD_PAIR && qw < s1 && k00 + STAGE - 1 <= qw && k00 + STAGE <= s1) {  // wave-uniform
+      fwd_pair(sK, sV, qf, lane, c2, m, l, Ot);
+      return;
+    }
 #pragma unroll
     for (int half = 0; half < STAGE / TILE; ++half) {
       const int k0 = k00 + TILE * half;

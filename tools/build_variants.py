@@ -50,6 +50,7 @@ VARIANTS = {
     "attn_clock_nopipe": {"PRL_ATTN_CLOCK_PROBE": "1", "PRL_ATTN_PIPE": "0"},
     "attn_pipe_sgb": {"PRL_ATTN_PIPE_SCHED": "0"},
     "attn_pipe_lead6": {"PRL_ATTN_PIPE_LEAD": "6"},
+    "attn_fwd_tiles": {"PRL_ATTN_FWD_PAIR": "0"},
     "vec_row_inputs": {"PRL_SCALAR_ROW_INPUTS": "0"},
     "target_select": {"PRL_TARGET_FIXUP": "0"},
     "noent_form_off": {"PRL_NOENT_FORM": "0"},
