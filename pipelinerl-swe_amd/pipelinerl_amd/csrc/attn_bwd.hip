@@ -1417,6 +1417,9 @@ __device__ __forceinline__ void fwd_tile(const char* tK, const char* tV, int k0,
 #ifndef PRL_ATTN_FWD_PAIR
 #define PRL_ATTN_FWD_PAIR 1
 #endif
+#ifndef PRL_ATTN_FWD_PAIR_SPREAD
+#define PRL_ATTN_FWD_PAIR_SPREAD 1  // tile b's softmax spread over tile a's P.V MFMAs (A/B: 0)
+#endif
 // both 32-key tiles of a stage every key of which is visible to every query of the wave: S of both
 // tiles (16 MFMAs back to back), one running-max / lazy-rescale decision over the 64 keys (one
 // cross-half exchange instead of two), then both tiles' P and O^T += V^T P (16 MFMAs).  Same
@@ -1430,9 +1433,11 @@ __device__ __forceinline__ void fwd_pair(const char* tK, const char* tV, const b
   for (int c = 0; c < 8; ++c) Sa = mfma(row_read(tK, l32, 2 * c + hi), qf[c], Sa);
 #pragma unroll
   for (int c = 0; c < 8; ++c) Sb = mfma(row_read(tK + TILE * 256, l32, 2 * c + hi), qf[c], Sb);
+  // the max of the 32 scores by v_max3_f32 (fmaxf put a canonicalizing v_max beside almost every
+  // max of MFMA results: 54 instructions for 31 maxima)
   float tmax = fmaxf(Sa[0], Sb[0]);
 #pragma unroll
-  for (int r = 1; r < 16; ++r) tmax = fmaxf(tmax, fmaxf(Sa[r], Sb[r]));
+  for (int r = 1; r < 16; ++r) asm("v_max3_f32 %0, %1, %2, %3" : "=v"(tmax) : "v"(tmax), "v"(Sa[r]), "v"(Sb[r]));
   tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * c2;
   if (tmax > m + kRescale) {
     const float f = fexp2(m - tmax);
@@ -1451,6 +1456,35 @@ __device__ __forceinline__ void fwd_pair(const char* tK, const char* tV, const b
     ps += p;
     pa[r >> 3][r & 7] = (__bf16)p;
   }
+#if PRL_ATTN_FWD_PAIR_SPREAD
+  // tile b's probabilities two elements per gap of tile a's P.V MFMAs (the V operand read two MFMAs
+  // ahead), fenced per gap so the compiler keeps the spread; same operations and summation order
+  float pbv[16];
+  bf16x8 ring[2] = {tr_operand(tV, lane, 0, 0), tr_operand(tV, lane, 0, 1)};
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const bf16x8 op = ring[i & 1];
+    if (i + 2 < 16) {
+      const int j = i + 2;
+      ring[i & 1] = tr_operand(tV + (j >> 3) * TILE * 256, lane, (j & 7) >> 1, j & 1);
+    }
+    if (i < 8) {
+      Ot[i >> 1] = mfma(op, pa[i & 1], Ot[i >> 1]);
+#pragma unroll
+      for (int e = 2 * i; e < 2 * i + 2; ++e) pbv[e] = fexp2(__builtin_fmaf(Sb[e], c2, -m));
+      pb[i >> 2][(2 * i) & 7] = (__bf16)pbv[2 * i];
+      pb[i >> 2][(2 * i + 1) & 7] = (__bf16)pbv[2 * i + 1];
+    } else {
+      if (i == 8) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) ps += pbv[e];
+      }
+      Ot[(i - 8) >> 1] = mfma(op, pb[i & 1], Ot[(i - 8) >> 1]);
+    }
+    sched_fence();
+  }
+  l += ps + __shfl_xor(ps, 32, 64);
+#else
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const float p = fexp2(__builtin_fmaf(Sb[r], c2, -m));
@@ -1466,6 +1500,7 @@ __device__ __forceinline__ void fwd_pair(const char* tK, const char* tV, const b
   for (int dc = 0; dc < 4; ++dc)
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) Ot[dc] = mfma(tr_operand(tV + TILE * 256, lane, dc, ks), pb[ks], Ot[dc]);
+#endif
 }
 
 __global__ __launch_bounds__(256, PRL_ATTN_FWD_MINB) void attn_fwd(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
