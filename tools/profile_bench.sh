@@ -3,7 +3,7 @@
 # Outputs (small CSVs only) under gpurun_out/prof_bench, gpurun_out/pmc_fetch, gpurun_out/pmc_write.
 set -u
 export TMPDIR=/tmp
-B="bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-trainer-step --no-c3"
+B="bench.py --steps 47 --warmup 3 --no-cpu-baseline --no-trainer-step --no-c3"
 bash tools/prof_stats.sh prof_bench 240 $B || exit $?
 for c in FETCH_SIZE WRITE_SIZE; do
   d=pmc_$( [ $c = FETCH_SIZE ] && echo fetch || echo write )
