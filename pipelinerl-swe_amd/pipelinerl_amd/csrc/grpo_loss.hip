@@ -399,6 +399,20 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
 
 // ---------------------------------------------------------------------------------------
 // generic streaming path: T = float (PRL_F32) or uint16_t (bf16); VEC elements per access
+#ifndef PRL_STREAM_STORE_SC1
+#define PRL_STREAM_STORE_SC1 1  // the 16-B row stores as the resident kernel's (kStoreAux); 0: plain nt
+#endif
+// a 16-B store into a wave-uniform row through a buffer descriptor (soffset 0: the hardware wait
+// state for the store data is emitted), with the resident kernel's cache policy
+__device__ __forceinline__ void store_row16(void* row, int64_t gv, u32x4 o) {
+#if PRL_STREAM_STORE_SC1
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(row, 0, 0x7fffffff, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, o), rs,
+                                         (int)(gv * 16), 0, kStoreAux);
+#else
+  __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(row) + gv);
+#endif
+}
 template <typename T, int VEC>
 struct RowIO;
 template <>
@@ -415,7 +429,7 @@ struct RowIO<uint16_t, 8> {
     u32x4 o;
 #pragma unroll
     for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(d[2 * j], d[2 * j + 1]);
-    __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(row) + gv);
+    store_row16(row, gv, o);
   }
 };
 template <>
@@ -427,7 +441,7 @@ struct RowIO<float, 4> {
   }
   static __device__ __forceinline__ void store(float* row, int64_t gv, const float (&d)[4]) {
     f32x4 o = {d[0], d[1], d[2], d[3]};
-    __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(row) + gv);
+    store_row16(row, gv, __builtin_bit_cast(u32x4, o));
   }
 };
 template <>

@@ -51,6 +51,7 @@ VARIANTS = {
     "attn_pipe_sgb": {"PRL_ATTN_PIPE_SCHED": "0"},
     "attn_pipe_lead6": {"PRL_ATTN_PIPE_LEAD": "6"},
     "attn_fwd_tiles": {"PRL_ATTN_FWD_PAIR": "0"},
+    "stream_store_nt": {"PRL_STREAM_STORE_SC1": "0"},
     "vec_row_inputs": {"PRL_SCALAR_ROW_INPUTS": "0"},
     "target_select": {"PRL_TARGET_FIXUP": "0"},
     "noent_form_off": {"PRL_NOENT_FORM": "0"},
