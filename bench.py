@@ -172,18 +172,49 @@ T_START = time.perf_counter()
 
 class ProbeRunner:
     """Runs the bench's side probes independently: a probe that raises is reported as an error
-    (its traceback on this rank's stderr) and the next one still runs; the ranks agree over the CPU
-    control group ``ctrl`` whether a probe failed anywhere (``error_on_another_rank``); every
-    result carries its wall time (``wall`` collects them).  A device that no longer synchronises
-    ends the probing (SystemExit) rather than queueing more work on it."""
+    (its traceback on this rank's stderr); the ranks agree over the CPU control group ``ctrl``
+    whether a probe failed anywhere (``error_on_another_rank``) BEFORE any of them synchronises the
+    device; every result carries its wall time (``wall`` collects them).
+
+    A failure on EVERY rank (the same probe failing the same way, e.g. out of memory) leaves the
+    collectives matched and the next probe runs.  A failure on SOME ranks only may leave the other
+    ranks' RCCL collectives without partners: those ranks then skip their device synchronise,
+    abort the default RCCL group (so its queued collectives return instead of hanging), and every
+    later probe is skipped with the reason.  An agreement that times out counts as such a failure.
+    A device that no longer synchronises ends the probing (SystemExit)."""
 
     def __init__(self, rank: int, device, ctrl=None):
         self.rank, self.device, self.ctrl = rank, torch.device(device), ctrl
         self.wall: dict[str, float] = {}
+        self.poisoned: str | None = None
+
+    def _agree(self, failed: int) -> tuple[int, int]:
+        """(ranks that failed, ranks in ctrl); (-1, n) when the agreement itself failed."""
+        if self.ctrl is None:
+            return failed, 1
+        n = dist.get_world_size(self.ctrl)
+        try:
+            flag = torch.tensor([failed], dtype=torch.int64)
+            dist.all_reduce(flag, group=self.ctrl)
+            return int(flag), n
+        except Exception as e:  # noqa: BLE001 - a peer never arrived (stuck or dead)
+            print(f"[rank {self.rank}] probe agreement failed: {type(e).__name__}: {e}", file=sys.stderr, flush=True)
+            return -1, n
+
+    def _abort_rccl(self) -> None:
+        try:
+            if dist.is_initialized() and "nccl" in str(dist.get_backend()):
+                dist.distributed_c10d._abort_process_group()
+        except Exception as e:  # noqa: BLE001
+            print(f"[rank {self.rank}] aborting the RCCL group failed: {e}", file=sys.stderr, flush=True)
 
     def run(self, name: str, fn):
         t0 = time.perf_counter()
-        res, ok = None, 1
+        if self.poisoned is not None:
+            self.wall[name] = 0.0
+            return {"skipped": f"probe {self.poisoned} failed on some ranks only: its collectives may be unmatched",
+                    "wall_s": 0.0}
+        res, failed = None, 0
         done = threading.Event()
         if self.rank == 0:  # progress on stderr (a silent multi-minute probe looks hung to a watchdog)
             print(f"[bench] probe {name} started", file=sys.stderr, flush=True)
@@ -198,9 +229,17 @@ class ProbeRunner:
         except Exception as e:  # noqa: BLE001
             import traceback
 
-            ok = 0
+            failed = 1
             print(f"[rank {self.rank}] probe {name} failed:\n{traceback.format_exc()}", file=sys.stderr, flush=True)
             res = {"error": f"{type(e).__name__}: {e}"[:400]}
+        nfail, n = self._agree(failed)  # before any device synchronise
+        partial = nfail < 0 or 0 < nfail < n
+        if nfail != 0 and not failed:
+            res = dict(res or {}, error_on_another_rank=True)
+        if partial:
+            self.poisoned = name
+            self._abort_rccl()
+        ok = 1
         # the probe's memory back before the next one: Python garbage first (reference cycles can
         # hold a probe's model and optimizer state), then torch's cached device blocks and pinned host
         # buffers (gloo stages CUDA tensors through pinned host memory in the one-GPU rehearsal,
@@ -208,7 +247,7 @@ class ProbeRunner:
         import gc
 
         gc.collect()
-        if self.device.type == "cuda":
+        if self.device.type == "cuda" and not partial:
             try:
                 torch.cuda.synchronize(self.device)
                 torch.cuda.empty_cache()
@@ -222,21 +261,15 @@ class ProbeRunner:
             rss = round(psutil.Process().memory_info().rss / 2 ** 30, 2)
         except Exception:  # noqa: BLE001
             rss = None
-        if self.ctrl is not None:  # every rank learns whether the probe failed anywhere
-            flag = torch.tensor([ok], dtype=torch.int64)
-            dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.ctrl)
-            if int(flag) < 1 and ok == 1:
-                res = dict(res or {}, error_on_another_rank=True)
-            ok = min(ok, int(flag))
         done.set()
         self.wall[name] = round(time.perf_counter() - t0, 1)
         if self.rank == 0:
-            print(f"[bench] probe {name} done in {self.wall[name]} s ({'ok' if ok == 1 else 'failed'})", file=sys.stderr,
-                  flush=True)
+            state = "ok" if nfail == 0 else ("failed on every rank" if nfail == n else "failed on some ranks")
+            print(f"[bench] probe {name} done in {self.wall[name]} s ({state})", file=sys.stderr, flush=True)
         if isinstance(res, dict):
             res["wall_s"] = self.wall[name]
             res["host_rss_gib_after"] = rss
-            if self.device.type == "cuda" and ok >= 0:
+            if self.device.type == "cuda" and ok >= 0 and not partial:
                 res["device_free_gib_after"] = round(torch.cuda.mem_get_info(self.device)[0] / 2 ** 30, 2)
         if ok < 0:
             raise SystemExit(f"device failure in probe {name}")
@@ -333,20 +366,42 @@ def main():
     # microbenchmarks), so a driver lease that runs out loses the least important ones.
     import datetime
 
-    ctrl = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=900)) if world > 1 else None
+    ctrl = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=300)) if world > 1 else None
     runner = ProbeRunner(rank, dev, ctrl)
     optional, probe_wall = runner.run, runner.wall
 
     logits = fields = None
     torch.cuda.empty_cache()
+    census = None
+    if world > 1:
+        # every communicator of the run reports the size it was meant to have (and that many ranks
+        # take part in an all-reduce over it) before any probe relies on it
+        from pipelinerl_amd import comm_probe
+
+        def communicators():
+            groups = {"dp": (None, world), "ctrl": (ctrl, world)}
+            rc = None
+            if not rehearse:  # a prl_comm RCCL communicator needs one GPU per rank
+                from pipelinerl_amd.comm import RcclComm
+
+                rc = RcclComm.from_group(ctrl, dev)
+                groups["prl_comm_dp"] = (rc, world)
+            try:
+                return comm_probe.group_census(groups, dev)
+            finally:
+                if rc is not None:
+                    rc.close()
+
+        census = optional("communicators", communicators)
     c3 = None
     if not args.no_c3:
         # configs[2] (C3): Qwen2.5-7B DP trainer step on C3's packed math rollouts, with the full
-        # bucketed 15.23 GB gradient all-reduce at N > 1 (local / DP / all-reduce-alone timings)
+        # bucketed 15.23 GB gradient all-reduce at N > 1 (local / DP / all-reduce-alone timings),
+        # then the same step with the weight-update snapshot in flight on its side stream
         from pipelinerl_amd.trainer_probe import dp_step_probe
 
         c3 = optional("c3_dp", lambda: dp_step_probe("c3", micro_batches=4, steps=2, warmup=1, device=dev,
-                                                      layers=4 if rehearse else None))
+                                                      layers=4 if rehearse else None, snapshot=True))
     trainer = None
     if not args.no_trainer_step:
         # the whole optimizer step the loss head sits in
@@ -443,15 +498,22 @@ def main():
         scaling = dp_scaling(world, c3, trainer)
         if scaling is not None:
             out["dp_scaling"] = scaling
-        for key, res in (("c3_dp", c3), ("trainer_step", trainer), ("fsdp_32b", fsdp), ("split_pipeline", split),
-                         ("exchange", comm)):
+        if isinstance(c3, dict) and "snapshot_overlap" in c3:
+            # the trainer-side half of "weight broadcast fully overlapped": C3's 7B step with and
+            # without WeightUpdateManager's snapshot in flight on its side stream
+            out["snapshot_overlap"] = dict(c3.pop("snapshot_overlap"), step="c3_dp (Qwen2.5-7B, 4 micro-batches)")
+        for key, res in (("communicators", census), ("c3_dp", c3), ("trainer_step", trainer), ("fsdp_32b", fsdp),
+                         ("split_pipeline", split), ("exchange", comm)):
             if res is not None:
                 out[key] = res
         out["probe_wall_s"] = probe_wall
         out["wall_total_s"] = round(time.perf_counter() - T_START, 1)
         print(json.dumps(out), flush=True)
     if world > 1:
-        dist.destroy_process_group()
+        try:
+            dist.destroy_process_group()
+        except Exception as e:  # noqa: BLE001 - an aborted RCCL group (see ProbeRunner)
+            print(f"[rank {rank}] destroy_process_group: {e}", file=sys.stderr, flush=True)
 
 
 if __name__ == "__main__":

@@ -50,6 +50,7 @@ int prl_comm_broadcast_buckets(void* comm, void* buf, size_t bytes, size_t bucke
 /* In-place all-reduce of `count` elements. */
 int prl_comm_allreduce(void* comm, void* buf, size_t count, int dtype, int op, void* stream);
 
+/* This rank / the communicator's size as RCCL reports them (ncclCommUserRank / ncclCommCount). */
 int prl_comm_rank(void* comm, int* rank);
 int prl_comm_size(void* comm, int* world);
 int prl_comm_destroy(void* comm);

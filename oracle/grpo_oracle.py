@@ -136,7 +136,8 @@ def _rows_parallel(fn, n_rows: int, chunk: int, threads: int):
 def rl_step_oracle(logits: np.ndarray, batch: dict, config: dict, current_step: int,
                    max_step: int, values: np.ndarray | None = None, grad_out: float = 1.0,
                    compute_grad: bool = True, dtype=np.float64, threads: int = 1,
-                   row_chunk: int = 64, grad_rows: np.ndarray | None = None) -> dict[str, Any]:
+                   row_chunk: int = 64, grad_rows: np.ndarray | None = None,
+                   rows: dict[str, np.ndarray] | None = None) -> dict[str, Any]:
     """Restatement of rl_step (rl/__init__.py:130-377) on fixed logits.
 
     ``logits``: [B, L, V] (any float dtype, e.g. float32 or bf16 values held in float32).
@@ -147,7 +148,10 @@ def rl_step_oracle(logits: np.ndarray, batch: dict, config: dict, current_step: 
     Returns loss, stats, new_logprobs/entropy [B, L-1], and (optionally) dlogits [B, L, V]
     and dvalues [B, L] for upstream gradient ``grad_out``.  ``grad_rows``: flat loss rows
     q = b*(L-1)+t; when given, only those rows' gradients are formed (``dlogits_rows`` [len, V],
-    for full-size checks where [B, L, V] in float64 would not fit).
+    for full-size checks where [B, L, V] in float64 would not fit).  ``rows``: the per-row
+    (lse, entropy, new_logprobs) of an earlier call on the same logits (its returned arrays):
+    the pass over [B, L-1, V] is skipped and only the token arithmetic is redone (a full-size
+    test reruns it with perturbed parameters to show its tolerance detects the change).
     Raises AssertionError / ValueError exactly where the reference does.
     """
     cfg = dict(RL_DEFAULTS)
@@ -171,10 +175,13 @@ def rl_step_oracle(logits: np.ndarray, batch: dict, config: dict, current_step: 
     def _stats(a, b):
         return row_stats(flat_logits[a:b], flat_tgt[a:b], None, temperature, dtype)
 
-    parts = _rows_parallel(_stats, R, row_chunk, threads)
-    lse = np.concatenate([p[0] for p in parts]).reshape(B, L - 1)
-    entropy = np.concatenate([p[1] for p in parts]).reshape(B, L - 1)
-    new_lp = np.concatenate([p[2] for p in parts]).reshape(B, L - 1)
+    if rows is not None:
+        lse, entropy, new_lp = (np.asarray(rows[k]).reshape(B, L - 1) for k in ("lse", "entropy", "new_logprobs"))
+    else:
+        parts = _rows_parallel(_stats, R, row_chunk, threads)
+        lse = np.concatenate([p[0] for p in parts]).reshape(B, L - 1)
+        entropy = np.concatenate([p[1] for p in parts]).reshape(B, L - 1)
+        new_lp = np.concatenate([p[2] for p in parts]).reshape(B, L - 1)
     if not np.isfinite(new_lp).all():  # :209
         raise AssertionError(f"new_logprobs is not finite: {new_lp}")
 

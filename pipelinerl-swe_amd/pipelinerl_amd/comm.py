@@ -113,6 +113,42 @@ class RcclComm:
         _check(lib.prl_comm_init(idbuf, rank, world, idx, ctypes.byref(h)), "prl_comm_init")
         return cls(h, rank, world, torch.device("cuda", idx), store)
 
+    @classmethod
+    def from_group(cls, group, device: torch.device | str | int) -> "RcclComm":
+        """Collective over the ranks of an initialised torch process group (e.g. a gloo control
+        group): rank 0 of ``group`` creates the RCCL unique id and shares it with
+        ``broadcast_object_list``; every rank's communicator rank is its rank in ``group``."""
+        lib = load()
+        device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+        if device.type != "cuda":
+            raise CommError("RcclComm needs a HIP device")
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        box = [None]
+        if rank == 0:
+            buf = (ctypes.c_uint8 * ID_BYTES)()
+            _check(lib.prl_comm_get_unique_id(buf), "prl_comm_get_unique_id")
+            box[0] = bytes(buf)
+        dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        if not isinstance(box[0], bytes) or len(box[0]) != ID_BYTES:
+            raise CommError("malformed RCCL unique id from the group broadcast")
+        idbuf = (ctypes.c_uint8 * ID_BYTES).from_buffer_copy(box[0])
+        h = ctypes.c_void_p()
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        _check(lib.prl_comm_init(idbuf, rank, world, idx, ctypes.byref(h)), "prl_comm_init")
+        return cls(h, rank, world, torch.device("cuda", idx))
+
+    def reported_size(self) -> int:
+        """The communicator's size as RCCL reports it (ncclCommCount through prl_comm_size)."""
+        n = ctypes.c_int(-1)
+        _check(load().prl_comm_size(self._h, ctypes.byref(n)), "prl_comm_size")
+        return int(n.value)
+
+    def reported_rank(self) -> int:
+        """This rank in the communicator as RCCL reports it (ncclCommUserRank)."""
+        r = ctypes.c_int(-1)
+        _check(load().prl_comm_rank(self._h, ctypes.byref(r)), "prl_comm_rank")
+        return int(r.value)
+
     def broadcast(self, t: torch.Tensor, src: int = 0, bucket_bytes: int = 0) -> None:
         if not t.is_contiguous() or t.device.type != "cuda":
             raise CommError("broadcast needs a contiguous HIP tensor")

@@ -80,6 +80,37 @@ def _sync(device: torch.device) -> None:
         torch.cuda.synchronize(device)
 
 
+def group_census(groups: dict, device) -> dict:
+    """The size every communicator of a multi-rank run reports, against the intended rank count.
+
+    ``groups``: name -> (torch process group | comm.RcclComm | None for the default group,
+    intended ranks).  Per entry: the size the communicator itself reports (``ncclCommCount`` /
+    ``ncclCommUserRank`` through prl_comm for an RcclComm; ``dist.get_world_size(group)`` and the
+    backend for a torch group) and the sum of an all-reduce of ones over it, i.e. the ranks that
+    actually took part.  Collective over each group's members (non-members pass the group's entry
+    as absent).  Raises AssertionError when any reported size or participant count differs from
+    the intended one (launch.py:147-150 / world.py:184: the actor group is 1 + actor GPUs)."""
+    from .comm import RcclComm
+
+    out = {}
+    for name, (group, intended) in groups.items():
+        ones = torch.ones(1, dtype=torch.float32, device=device)
+        if isinstance(group, RcclComm):
+            entry = {"kind": "prl_comm (RCCL)", "reported": group.reported_size(), "rank": group.reported_rank()}
+            group.all_reduce(ones)
+        else:
+            entry = {"kind": f"torch {dist.get_backend(group)}", "reported": dist.get_world_size(group),
+                     "rank": dist.get_rank(group)}
+            dist.all_reduce(ones, group=group)
+        _sync(torch.device(device))
+        entry.update(intended=int(intended), participants=int(ones.item()))
+        entry["ok"] = entry["reported"] == entry["participants"] == int(intended)
+        out[name] = entry
+    bad = {k: v for k, v in out.items() if not v["ok"]}
+    assert not bad, f"communicator sizes differ from the intended rank counts: {bad}"
+    return out
+
+
 def grad_allreduce_probe(shapes, device, iters: int = 5, bucket_bytes: int = 256 << 20, group=None,
                          dtype=torch.bfloat16) -> dict:
     from .finetune.grad_sync import GradBuckets

@@ -39,7 +39,7 @@ struct AdamWHyper {
 
 // one element: torch's adam_math (kParamIdx..kExpAvgSqIdx), float opmath, doubles where it has them.
 // The multiply-adds are spelled out as the fused form torch's build contracts them to (measured
-// element by element, tools/adamw_debug.py: beta1 m + (1 - beta1) g is fma(beta1, m, (1 - beta1) g),
+// element by element, tools/adamw_debug.py [round 1-3 tool, in git history]: beta1 m + (1 - beta1) g is fma(beta1, m, (1 - beta1) g),
 // not fma(1 - beta1, g, beta1 m) as this compiler would choose); nothing else is contracted.
 __device__ __forceinline__ void adamw_elem(float& param, float grad, float& exp_avg, float& exp_avg_sq,
                                            const AdamWHyper& h, float bias_correction1, float bias_correction2_sqrt) {

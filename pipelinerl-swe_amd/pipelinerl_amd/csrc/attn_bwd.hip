@@ -14,7 +14,7 @@
 //                  behind the current tile's MFMAs)
 //   attn_bwd_dq    one workgroup = 128 queries; each wave owns 32 queries (dQ^T in accumulators)
 //                  and sweeps the causal key tiles
-// MFMA: v_mfma_f32_32x32x16_bf16.  Lane layouts (probed, tools/mfma_layout_probe.hip):
+// MFMA: v_mfma_f32_32x32x16_bf16.  Lane layouts (probed, tools/mfma_layout_probe.hip [round 1-3 tool, in git history]):
 //   A[m][k]: lane l holds A[l%32][8(l/32)+i];  B[k][n]: lane l holds B[8(l/32)+i][l%32];
 //   C[m][n]: lane l, reg r holds C[8(r/4)+4(l/32)+(r%4)][l%32].
 // S and dP are computed with the KEY (dK/dV kernel) or the QUERY (dQ kernel) on the lane, so
@@ -118,13 +118,18 @@ __device__ __forceinline__ void stage_store(const StageT<ROWS>& st, char* base, 
 // read 0 with no per-row test, and the per-thread offsets are computed once per head (vbase = the
 // thread's first chunk: row tid / 16, head h, 16-B chunk tid % 16; chunk j is 16 j rows further).
 // The flat form's 64-bit address arithmetic and per-row branches took 15-19 % of the backward's
-// cycles (tools/attn_clock.py); this form issues 8 loads and ~15 scalar instructions per stage and
+// cycles (tools/attn_clock.py [round 1-3 tool, in git history]); this form issues 8 loads and ~15 scalar instructions per stage and
 // runs the backward 3-7 % and the forward 3-6 % faster (profiles/r03_attn_buf_stage_ab.jsonl).
 // Spreading the 8 loads over the paired tiles' MFMAs instead of one burst after the barrier was
 // measured no faster (same file): the issue cycles moved into the tiles.
+// The descriptor spans at most the ROWS rows one stage reads (never the rest of the sequence): its
+// byte count stays far below 2^31 at any sequence length (a whole-sequence span overflowed int32
+// past ~2^31 / (rs * 2) rows, turning the bounds check off for the unmasked stages).
+template <int ROWS = STAGE>
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const __bf16* X, int64_t rs, int r0, int r1) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(X + (int64_t)r0 * rs), 0,
-                                           (int)((int64_t)(r1 > r0 ? r1 - r0 : 0) * rs * 2), 0x00020000);
+  const int n = r1 > r0 ? (r1 - r0 < ROWS ? r1 - r0 : ROWS) : 0;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(X + (int64_t)r0 * rs), 0, (int)((int64_t)n * rs * 2),
+                                           0x00020000);
 }
 __device__ __forceinline__ int stage_vbase(int64_t rs, int h, int tid) {
   return (tid >> 4) * (int)(rs * 2) + h * D * 2 + (tid & 15) * 16;
@@ -135,7 +140,7 @@ __device__ __forceinline__ StageT<ROWS> stage_load_rows(const __bf16* __restrict
 #if PRL_ATTN_BUF_STAGE
   (void)h;
   (void)tid;
-  const __amdgpu_buffer_rsrc_t rsrc = rows_rsrc(X, rs, r0, r1);
+  const __amdgpu_buffer_rsrc_t rsrc = rows_rsrc<ROWS>(X, rs, r0, r1);
   StageT<ROWS> st;
 #pragma unroll
   for (int j = 0; j < ROWS * 16 / 256; ++j)
@@ -202,7 +207,7 @@ __device__ __forceinline__ void interleave_seg() {
 #if PRL_ATTN_CLOCK_PROBE
 // (shader clock, 100 MHz real time) at a workgroup's start and end, and wave 0's shader cycles per
 // phase of the stage loop, into buffers of their own that nothing else reads (MI355X_MICROARCH.md,
-// DVFS item 6); read by prl_attn_clock_read (tools/attn_clock.py)
+// DVFS item 6); read by prl_attn_clock_read (tools/attn_clock.py [round 1-3 tool, in git history])
 constexpr int kClockSlots = 1 << 16;
 __device__ unsigned long long g_clock[4 * kClockSlots];
 __device__ unsigned long long g_phase[8 * kClockSlots];
@@ -387,7 +392,7 @@ __device__ __forceinline__ void dkdv_pair(const char* tQ, const char* tdO, const
 // The dK/dV role past the diagonal as one software pipeline over its 32-query tiles.  The pair loop
 // above puts a tile's whole softmax (~110 vector instructions) under the 16 MFMAs of the next
 // tile's S / dP, and both tiles' softmaxes under half of the pair's 64 MFMAs: those regions ran at
-// 76-79 cycles per MFMA against 38-42 for the MFMA-only ones (tools/attn_clock.py, pair regions).
+// 76-79 cycles per MFMA against 38-42 for the MFMA-only ones (tools/attn_clock.py [round 1-3 tool, in git history], pair regions).
 // Here the MFMA stream is S/dP(t), dV/dK += (t-1), S/dP(t+1), dV/dK += t, ... and the softmax of
 // tile t is split by accumulator rows into two halves, one under dV/dK += (t-1) and one under
 // S/dP(t+1): every 16-MFMA segment carries half a softmax.  Tile t's stage must stay in LDS until

@@ -109,18 +109,18 @@ int prl_comm_allreduce(void* comm, void* buf, size_t count, int dtype, int op, v
   return rc(ncclAllReduce(buf, buf, count, dt, o, c->comm, static_cast<hipStream_t>(stream)));
 }
 
+// rank / size as RCCL itself reports them (ncclCommUserRank / ncclCommCount), not the values
+// the caller passed to prl_comm_init: a census of a running job checks one against the other
 int prl_comm_rank(void* comm, int* rank) {
   Comm* c = static_cast<Comm*>(comm);
   if (!c || !rank) return PRL_COMM_E_INVALID;
-  *rank = c->rank;
-  return 0;
+  return rc(ncclCommUserRank(c->comm, rank));
 }
 
 int prl_comm_size(void* comm, int* world) {
   Comm* c = static_cast<Comm*>(comm);
   if (!c || !world) return PRL_COMM_E_INVALID;
-  *world = c->world;
-  return 0;
+  return rc(ncclCommCount(c->comm, world));
 }
 
 int prl_comm_destroy(void* comm) {

@@ -209,7 +209,7 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_narrow(const uint16_t* __rest
 
 // Wide rows (NV > 4, e.g. H = 3584): the dw partials of the 4 waves fold through ONE LDS row, in
 // wave order, so the block needs H floats of LDS instead of 4 H, and w / x / dy stay packed
-// between uses: 0.254 -> 0.217 ms at 16384 x 3584 (tools/ew_bench.py).  Narrow rows keep the
+// between uses: 0.254 -> 0.217 ms at 16384 x 3584 (tools/ew_bench.py [round 1-3 tool, in git history]).  Narrow rows keep the
 // 4-row fold (rmsnorm_bwd_narrow), which measured faster at H = 1536 (0.179 vs 0.193 ms).
 #ifndef PRL_NORM_WIDE_DRES_EARLY
 #define PRL_NORM_WIDE_DRES_EARLY 1  // A/B (add_rmsnorm 8192 x 3584 bwd incl. autograd): 0.144-0.148 -> 0.130 ms

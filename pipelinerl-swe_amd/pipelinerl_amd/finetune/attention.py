@@ -60,7 +60,7 @@ def _items(bounds: list[int], device) -> tuple:
 _SPLITS: dict[tuple, tuple] = {}
 SPLIT_MIN_RATIO = 1.2
 # part cap as a fraction of the target; None: chosen per packing by _makespan.  PRL_ATTN_SPLIT_CAP=1.0
-# is the round-2 rule (A/B), tools/attn_role_split.py sweeps it
+# is the round-2 rule (A/B), tools/attn_role_split.py [round 1-3 tool, in git history] sweeps it
 SPLIT_CAP_FRAC: float | None = float(os.environ["PRL_ATTN_SPLIT_CAP"]) if os.environ.get("PRL_ATTN_SPLIT_CAP") else None
 SPLIT_CAPS = (1.0, 0.5, 0.33)
 SPLIT_MARGIN = 0.04
@@ -166,7 +166,7 @@ def _split_items(bounds: list[int], heads: int, kv_heads: int, device) -> tuple:
 
 class PackedCausalAttention(torch.autograd.Function):
     """HIP flash-attention forward (prl_attn_fwd; PRL_ATTN_FWD=torch: torch's varlen forward, its
-    log-sum-exp converted) and HIP backward (prl_attn_bwd; tools/attn_backend_probe.py,
+    log-sum-exp converted) and HIP backward (prl_attn_bwd; tools/attn_backend_probe.py [round 1-3 tool, in git history],
     profiles/r01_attention_probe.jsonl).
     q: [T, H, 128], k / v: [T, Hkv, 128] bf16 (GQA native: no repeated k / v)."""
 
@@ -191,7 +191,7 @@ class PackedCausalAttention(torch.autograd.Function):
             return out
         out, lse, _, _, _ = torch.ops.aten._flash_attention_forward(q, k, v, cu, cu, mx, mx, 0.0, True, False)
         nseq = len(bounds) - 1
-        # torch's varlen log-sum-exp on ROCm: [nseq, H, max_len] (checked: tools/lse_layout_probe.py)
+        # torch's varlen log-sum-exp on ROCm: [nseq, H, max_len] (checked: tools/lse_layout_probe.py [round 1-3 tool, in git history])
         if not (lse.dim() == 3 and tuple(lse.shape[:2]) == (nseq, q.shape[1]) and lse.shape[2] >= mx
                 and lse.is_contiguous() and lse.dtype == torch.float32 and cu.numel() == nseq + 1):
             raise RuntimeError(f"unexpected flash-attention log-sum-exp layout {tuple(lse.shape)}")
@@ -262,7 +262,7 @@ def varlen_attention_forward(module, query, key, value, attention_mask, scaling=
     hip_bwd = bounds is not None and q.is_cuda and _hip_backward_ok(q, k)
     if Hkv != Hq and not hip_bwd:
         # GQA with the library backward: its native-GQA backward is slower than with repeated k / v
-        # (6.32 vs 5.64 ms at 2 x 8192, tools/attn_backend_probe.py); the HIP backward takes GQA as is
+        # (6.32 vs 5.64 ms at 2 x 8192, tools/attn_backend_probe.py [round 1-3 tool, in git history]); the HIP backward takes GQA as is
         k = k.repeat_interleave(Hq // Hkv, dim=1)
         v = v.repeat_interleave(Hq // Hkv, dim=1)
     default_scale = D ** -0.5

@@ -221,7 +221,7 @@ def _wgrad(dy, x, w):
 
 # Fused gate/up projection: one GEMM over the concatenated [2 I, H] weight instead of two over
 # [I, H] (7B at 8 192 tokens through prl_gemm: forward 1.82 -> 1.53 ms, dgrad 1.93 -> 1.65 ms,
-# wgrad 1.66 -> 1.58 ms per layer, tools/fused_proj_bench.py, profiles/r02_fused_proj_bench.jsonl).  The weights stay separate Parameters; the
+# wgrad 1.66 -> 1.58 ms per layer, tools/fused_proj_bench.py [round 1-3 tool, in git history], profiles/r02_fused_proj_bench.jsonl).  The weights stay separate Parameters; the
 # concatenation is cached and rebuilt only when a member's version counter moves (once per
 # optimizer step).  Off under FSDP (shard_model) and with PRL_FUSED_GATE_UP=0 (A/B).
 _FUSED_GATE_UP = os.environ.get("PRL_FUSED_GATE_UP", "1") != "0"
@@ -236,9 +236,12 @@ def disable_fused_projections() -> None:
     _FUSED_GATE_UP = _FUSED_QKV = False
 
 
-# Bumped by every writer the build knows of that changes weights in place (PrlAdamW.step,
-# HipFlatPacker.unflatten, load_weights_): a second key of the fused-weight caches beside the
-# version counters, which a write through ``p.data`` or a raw pointer does not move.
+# Bumped by the build's writers that change weights through raw pointers (PrlAdamW.step and
+# HipFlatPacker.unflatten; both also move the version counters): a second key of the fused-weight
+# caches beside the version counters, which a write through ``p.data`` or a raw pointer does not
+# move.  In-place torch writes (load_state_dict, torch's optimizers, ``copy_`` under no_grad) move
+# the version counters and need no call; any new raw-pointer or ``.data`` writer must call
+# weights_written().
 _WEIGHT_EPOCH = [0]
 
 

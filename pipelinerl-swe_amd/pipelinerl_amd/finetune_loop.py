@@ -309,6 +309,15 @@ def grad_scale_convention(cfg) -> str:
     mode = args.get("grad_scale")
     if mode is None:
         mode = "deepspeed" if cfg.get("use_deepspeed", False) and not cfg.get("use_fsdp", False) else "accelerate"
+        if (mode == "accelerate" and not cfg.get("use_deepspeed", False) and not cfg.get("use_fsdp", False)
+                and cfg.get("deepspeed_config")):
+            # the documented way to launch without DeepSpeed (use_deepspeed=false, launch.py:272-277)
+            # also flips this default: the clipped gradient becomes GAS x the reference default's
+            logger.warning(
+                f"use_deepspeed is false but the config still names deepspeed_config={cfg.get('deepspeed_config')}: "
+                "the reference's default run uses DeepSpeed's gradient-accumulation scale (every micro-batch loss "
+                "/ GAS); this run sums micro-batch gradients (accelerate). Set finetune.grad_scale=deepspeed to "
+                "keep the reference default's gradients, or finetune.grad_scale=accelerate to silence this warning")
     if mode not in ("accelerate", "deepspeed"):
         raise ValueError(f"finetune.grad_scale must be 'accelerate' or 'deepspeed', got {mode!r}")
     return mode

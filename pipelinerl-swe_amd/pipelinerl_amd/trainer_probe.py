@@ -298,9 +298,70 @@ def trainer_step_probe(name: str = "1.5b", tokens: int = 16384, seq: int = 2048,
     return out
 
 
+def _snapshot_only_group():
+    """An actor group with no receivers (measurement only): WeightUpdateManager takes its snapshot
+    exactly as for real actors (stream-ordered, as with an RcclComm); the broadcasts are no-ops."""
+    from .comm import RcclComm
+
+    class SnapshotOnlyGroup(RcclComm):
+        def __init__(self):
+            super().__init__(None, 0, 1, None)
+
+        def broadcast(self, t: torch.Tensor, src: int = 0, bucket_bytes: int = 0) -> None:
+            return None
+
+    return SnapshotOnlyGroup()
+
+
+def snapshot_overlap(ts: "TrainerStep", t_ref: float, steps: int, warmup: int, flatten_iters: int = 3) -> dict:
+    """The trainer-side half of "weight broadcast fully overlapped" (north_star), on this rank's GPU.
+
+    The same optimizer step as ``t_ref`` (seconds per step, measured just before on ``ts``), now with
+    WeightUpdateManager (weight_update.py) snapshotting every parameter into its bf16 staging buffer
+    on its side stream after each optimizer step (rank 0, as in the trainer loop; no receiver: the
+    broadcasts are no-ops), against the snapshot alone (the same prl_flatten_bf16 pass on the side
+    stream, HIP events, nothing else running).  ``exposed_ms`` = step time with the snapshot in
+    flight − step time without it (≥ 0; ``step_delta_ms`` keeps the sign, i.e. the run-to-run noise);
+    ``hidden_frac`` = 1 − exposed / snapshot.  The reference blocks the trainer for the whole
+    update instead (finetune_loop.py:174-215)."""
+    from .weight_update import FlatLayout, HipFlatPacker, WeightUpdateManager, parameters_info
+
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    wum = WeightUpdateManager([], ts.model, None, _snapshot_only_group(), transport="bucketed", overlap=True,
+                              is_main=rank == 0, write_message=lambda s, m: None)
+    t_snap = ts.timed(steps, warmup, wum=wum)
+    wum.close()
+    named = wum.named_parameters()
+    layout = FlatLayout.from_infos(parameters_info(named))
+    flat = wum._ensure_staging(layout.total, ts.device)
+    params = [p.detach() for _, p in named]
+    side = torch.cuda.Stream(device=ts.device)
+    side.wait_stream(torch.cuda.current_stream(ts.device))
+    evs = []
+    with torch.cuda.stream(side):
+        for _ in range(flatten_iters + 1):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(side)
+            HipFlatPacker().flatten(params, layout.offsets, flat)
+            e1.record(side)
+            evs.append((e0, e1))
+    _sync(ts.device)
+    snap_ms = sum(a.elapsed_time(b) for a, b in evs[1:]) / flatten_iters
+    nbytes = sum(p.numel() * p.element_size() for p in params) + 2 * sum(p.numel() for p in params)
+    wum._staging = None
+    delta_ms = (t_snap - t_ref) * 1e3
+    exposed = max(0.0, delta_ms)
+    return {"params": len(params), "snapshot_bytes": 2 * layout.total, "snapshot_ms": round(snap_ms, 3),
+            "snapshot_GBps": round(nbytes / (snap_ms * 1e-3) / 1e9, 1),
+            "ms_per_step_no_snapshot": round(t_ref * 1e3, 2), "ms_per_step_with_snapshot": round(t_snap * 1e3, 2),
+            "step_delta_ms": round(delta_ms, 3), "exposed_ms": round(exposed, 3),
+            "hidden_frac": round(1.0 - min(1.0, exposed / snap_ms), 4) if snap_ms > 0 else None,
+            "steps": steps, "warmup": warmup}
+
+
 def dp_step_probe(config: str = "c3", micro_batches: int = 4, steps: int = 2, warmup: int = 1, device=None,
                   samples_per_step: int = 4096, layers: int | None = None, batches: list | None = None,
-                  model=None, step_fn=None) -> dict:
+                  model=None, step_fn=None, snapshot: bool = False) -> dict:
     """BASELINE.json configs[2] (C3) data-parallel trainer step on this rank's GPU: the config's
     model shapes (Qwen2.5-7B), ``micro_batches`` packed micro-batches per rank from the config's
     rollout distribution (workloads.py: prompt U{64..512} + completion U{256..8192}, packing cap
@@ -316,7 +377,8 @@ def dp_step_probe(config: str = "c3", micro_batches: int = 4, steps: int = 2, wa
     measured per-micro-batch time, the optimizer tail taken out) + the exposed all-reduce + one
     optimizer tail (clip + AdamW + zeroing, timed with device events: ``optimizer_tail_ms``).
     Collective over the default group (every rank calls it).  ``batches`` / ``model`` /
-    ``step_fn`` are injectable (gloo tests on CPU)."""
+    ``step_fn`` are injectable (gloo tests on CPU).  ``snapshot``: also time the same step with the
+    weight-update snapshot in flight (``snapshot_overlap``, HIP devices only)."""
     from . import workloads
 
     device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
@@ -344,7 +406,8 @@ def dp_step_probe(config: str = "c3", micro_batches: int = 4, steps: int = 2, wa
         t_dp = ts.timed(steps, warmup)
         t_ar = ts.allreduce_alone()
     nbytes = sum(p.numel() * p.element_size() for p in ts.model.parameters())
-    peak = torch.cuda.max_memory_allocated(device) / 1e9 if on_gpu else 0.0
+    peak = torch.cuda.max_memory_allocated(device) / 1e9 if on_gpu else 0.0  # before the staging buffer
+    snap = snapshot_overlap(ts, t_dp, steps, warmup) if snapshot and on_gpu else None
     ts.close()
     stats = torch.tensor([n_tokens, n_samples, t_local], dtype=torch.float64, device=device)
     if world > 1:  # ranks drew different samples: sum tokens / samples, slowest replica's time
@@ -380,7 +443,8 @@ def dp_step_probe(config: str = "c3", micro_batches: int = 4, steps: int = 2, wa
                              "ms_per_micro_batch": round(per_mb * 1e3, 2),
                              "tokens_per_s_per_gpu": round(tok_per_mb * (mb_real / world) / t_real, 1),
                              "allreduce_share": round(exposed / t_real, 5)},
-            "peak_mem_gb": round(peak, 2), "steps": steps, "warmup": warmup, "world": world}
+            "peak_mem_gb": round(peak, 2), "steps": steps, "warmup": warmup, "world": world,
+            **({"snapshot_overlap": snap} if snap is not None else {})}
 
 
 def fsdp_step_probe(name: str = "32b", tokens: int = 4096, seq: int = 2048, prompt: int = 256,
@@ -434,6 +498,15 @@ def split_pipeline_probe(actors: int, steps: int = 2, warmup: int = 1, device=No
     bc_group = dist.new_group([0] + list(range(n_tr, world)))
     is_trainer = rank < n_tr
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    from .comm_probe import group_census
+
+    # both groups report (and carry) exactly the ranks the split intends, before any traffic
+    mine = {}
+    if is_trainer:
+        mine["split_dp"] = (dp_group, n_tr)
+    if rank == 0 or not is_trainer:
+        mine["actor"] = (bc_group, 1 + actors)  # world.py:184: 1 + actor GPUs
+    census = group_census(mine, dev)
     result = {}
     nupdates = warmup + steps
     if is_trainer:
@@ -453,7 +526,7 @@ def split_pipeline_probe(actors: int, steps: int = 2, warmup: int = 1, device=No
             lat = [wum.last_latency_s]
             wum.close()
         ts.close()
-        result = {"plain_s": sec_plain, "bcast_s": sec_bcast, "latency_s": lat[0] if lat else 0.0}
+        result = {"plain_s": sec_plain, "bcast_s": sec_bcast, "latency_s": lat[0] if lat else 0.0, "groups": census}
     else:
         holder = [None]
         dist.broadcast_object_list(holder, src=0, group=bc_group)
@@ -478,4 +551,5 @@ def split_pipeline_probe(actors: int, steps: int = 2, warmup: int = 1, device=No
             "ms_per_step_no_broadcast": round(r0["plain_s"] * 1e3, 2),
             "ms_per_step_with_broadcast": round(r0["bcast_s"] * 1e3, 2),
             "broadcast_latency_ms": round(lat * 1e3, 2), "broadcast_bytes": nbytes,
-            "hidden_frac": round(1.0 - min(1.0, extra / lat), 4) if lat > 0 else None}
+            "hidden_frac": round(1.0 - min(1.0, extra / lat), 4) if lat > 0 else None,
+            "groups": r0.get("groups")}

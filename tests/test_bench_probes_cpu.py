@@ -1,6 +1,8 @@
-"""bench.py's side-probe orchestration on a world-2 gloo group (CPU): a probe that fails on one
-rank only is reported on every rank and does not stop the next probe; wall times are recorded;
-the top-level DP scaling quantity is formed from the C3 probe's own local / DP timings."""
+"""bench.py's side-probe orchestration on a world-2 gloo group (CPU): a probe that fails on every
+rank is reported and the next probe still runs; a probe that fails on one rank only is reported on
+every rank and every later probe is skipped with the reason (its collectives may be unmatched);
+wall times are recorded; the top-level DP scaling quantity is formed from the C3 probe's own local /
+DP timings."""
 
 import json
 import os
@@ -26,6 +28,9 @@ def _main(rank, world, port, out):
     ctrl = dist.new_group(backend="gloo")
     r = bench.ProbeRunner(rank, "cpu", ctrl)
 
+    def everywhere():
+        raise RuntimeError(f"out of memory on rank {rank}")
+
     def flaky():
         if rank == 1:
             raise RuntimeError("out of memory on rank 1")
@@ -36,19 +41,22 @@ def _main(rank, world, port, out):
         dist.all_reduce(t)
         return {"sum": float(t)}
 
-    res = {"flaky": r.run("flaky", flaky), "after": r.run("after", collective), "wall": r.wall}
+    res = {"everywhere": r.run("everywhere", everywhere), "after_all": r.run("after_all", collective),
+           "flaky": r.run("flaky", flaky), "after": r.run("after", collective), "wall": r.wall}
     Path(out, f"r{rank}.json").write_text(json.dumps(res))
     dist.destroy_process_group()
 
 
-def test_probe_failure_is_shared_and_does_not_skip_later_probes(tmp_path):
+def test_probe_failures_shared_and_partial_failure_skips_later_probes(tmp_path):
     mp.spawn(_main, args=(2, free_port(), str(tmp_path)), nprocs=2, join=True)
     r0, r1 = (json.loads((tmp_path / f"r{r}.json").read_text()) for r in range(2))
+    for r in (r0, r1):
+        assert "out of memory" in r["everywhere"]["error"]
+        assert r["after_all"]["sum"] == 2.0  # a failure on every rank: the next probe still runs
+        assert set(r["wall"]) == {"everywhere", "after_all", "flaky", "after"} and r["after_all"]["wall_s"] >= 0
+        assert "flaky" in r["after"]["skipped"]  # a failure on one rank: later probes are skipped
     assert "error" in r1["flaky"] and "out of memory" in r1["flaky"]["error"]
     assert r0["flaky"]["error_on_another_rank"] is True and r0["flaky"]["value"] == 1
-    for r in (r0, r1):
-        assert r["after"]["sum"] == 2.0  # the next collective probe ran on both ranks
-        assert set(r["wall"]) == {"flaky", "after"} and r["after"]["wall_s"] >= 0
 
 
 def test_dp_scaling_from_the_c3_probe():

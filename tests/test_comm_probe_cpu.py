@@ -1,6 +1,7 @@
 """The bench's exchange-step probes (comm_probe.py) on a world-size-2 gloo group on CPU:
 the DP gradient all-reduce through GradBuckets and the trainer -> actor weight broadcast
-through WeightUpdateManager / WorkerExtension, each verifying its own result."""
+through WeightUpdateManager / WorkerExtension, each verifying its own result; the communicator
+census (every group reports, and carries, the intended number of ranks; a wrong size fails)."""
 
 import os
 import sys
@@ -27,7 +28,18 @@ def _run(rank, port, world, out):
     ar = comm_probe.grad_allreduce_probe(SHAPES, dev, iters=2, bucket_bytes=2048)
     bc = comm_probe.broadcast_probe(SHAPES, dev, iters=2, bucket_bytes=1000, packer=TorchFlatPacker())
     pt = comm_probe.broadcast_probe(SHAPES, dev, iters=1, packer=TorchFlatPacker(), transport="per_tensor")
-    torch.save({"ar": ar, "bc": bc, "pt": pt}, Path(out) / f"r{rank}.pt")
+    ctrl = dist.new_group(backend="gloo")
+    sub = dist.new_group([0, world - 1])
+    groups = {"dp": (None, world), "ctrl": (ctrl, world)}
+    if rank in (0, world - 1):
+        groups["actor"] = (sub, 2)
+    census = comm_probe.group_census(groups, dev)
+    try:  # a group that is not the size it should be fails the census on every member
+        comm_probe.group_census({"dp": (None, world + 1)}, dev)
+        wrong = None
+    except AssertionError as e:
+        wrong = str(e)
+    torch.save({"ar": ar, "bc": bc, "pt": pt, "census": census, "wrong": wrong}, Path(out) / f"r{rank}.pt")
     dist.destroy_process_group()
 
 
@@ -42,6 +54,13 @@ def test_probes_gloo(tmp_path, world):
         assert res["bc"]["correct"] and res["pt"]["correct"]
         assert res["bc"]["receivers"] == world - 1
         assert res["ar"]["bytes"] == sum(2 * torch.Size(s).numel() for _, s in SHAPES)
+        c = res["census"]
+        assert set(c) == ({"dp", "ctrl", "actor"} if r in (0, world - 1) else {"dp", "ctrl"})
+        for name, e in c.items():
+            assert e["ok"] and e["reported"] == e["participants"] == e["intended"], (name, e)
+            assert e["kind"] == "torch gloo"
+        assert c["dp"]["intended"] == world and ("actor" not in c or c["actor"]["reported"] == 2)
+        assert res["wrong"] and "intended" in res["wrong"]
 
 
 def test_qwen2_shapes_match_survey():

@@ -184,6 +184,35 @@ def test_grad_scale_convention_follows_the_backend():
     assert micro_batch_loss_scale(args, 4, "accelerate") == 1.0
 
 
+def test_launch_without_deepspeed_warns_about_the_grad_scale(caplog):
+    """The reference config (conf/base.yaml:94-95: use_deepspeed true, deepspeed_config named)
+    launched with the documented use_deepspeed=false (launch.py:272-277 then drops --use_deepspeed):
+    one WARNING that the default gradient convention changed, naming the override; both explicit
+    conventions resolve silently, and a config without deepspeed_config does not warn."""
+    import logging
+
+    from pipelinerl_amd.config import Cfg
+    from pipelinerl_amd.finetune_loop import grad_scale_convention
+
+    ref_default = {"use_deepspeed": False, "deepspeed_config": "deepspeed_stage3_bf16", "finetune": {}}
+    with caplog.at_level(logging.WARNING, logger="pipelinerl_amd.finetune_loop"):
+        assert grad_scale_convention(Cfg.wrap(ref_default)) == "accelerate"
+    warns = [r for r in caplog.records if r.levelno == logging.WARNING]
+    assert len(warns) == 1 and "finetune.grad_scale=deepspeed" in warns[0].getMessage()
+    for mode in ("deepspeed", "accelerate"):
+        caplog.clear()
+        with caplog.at_level(logging.WARNING, logger="pipelinerl_amd.finetune_loop"):
+            cfg = dict(ref_default, finetune={"grad_scale": mode})
+            assert grad_scale_convention(Cfg.wrap(cfg)) == mode
+        assert not caplog.records
+    caplog.clear()
+    with caplog.at_level(logging.WARNING, logger="pipelinerl_amd.finetune_loop"):
+        assert grad_scale_convention(Cfg.wrap({"use_deepspeed": False, "finetune": {}})) == "accelerate"
+        assert grad_scale_convention(Cfg.wrap({"use_deepspeed": True, "deepspeed_config": "x", "finetune": {}})) \
+            == "deepspeed"
+    assert not caplog.records
+
+
 def test_phase_trace_metrics(tmp_path):
     """finetune.trace_gpu_phases: per-step trace/<phase>_ms for forward, backward, all-reduce wait,
     clip and optimizer (summed over the step's micro-batches) and trace/gpu_step_ms in the logged

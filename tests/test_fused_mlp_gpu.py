@@ -193,7 +193,7 @@ def test_fused_gate_up_training_matches_separate(monkeypatch):
     """Three optimizer steps (native AdamW, lr 1e-3) of a 2-layer Qwen2.5-0.5B-shaped model with the
     fused gate/up projection vs the separate one: every MLP weight's total update agrees to bf16
     GEMM rounding (measured 0.05 relative; with the fused weight cache going stale after a step,
-    the bug fixed in optim.py, it was 0.24-0.28: tools/fused_training_check.py).  Bound 0.08: a third
+    the bug fixed in optim.py, it was 0.24-0.28: tools/fused_training_check.py [round 1-3 tool, in git history]).  Bound 0.08: a third
     of the bug signal, 1.6x the 0.046-0.049 measured in round 3."""
     from pipelinerl_amd.finetune import model_ops
     from pipelinerl_amd.trainer_probe import TrainerStep

@@ -193,37 +193,111 @@ def test_errors_match_reference():
     assert float(loss) == 0.0
 
 
-def test_c2_scale_properties():
-    """Config C2 size (65536 packed rows x 151936 vocab, bf16): sampled rows vs the oracle,
-    softmax-gradient rows sum to ~0, and the kernel is bitwise deterministic."""
-    from pipelinerl_amd.finetune.rl.fused import GrpoParams, grpo_loss, prepare_fields
-
-    T, V = 65536, 151936
+def _c2_inputs(T: int, V: int, seq: int):
+    """C2's packed micro-batch (T rows = T/seq rollouts of seq tokens, 256-token prompts) with
+    per-token fields drawn so every branch of the token arithmetic is taken at full size:
+    old = ATen log-prob of the target + N(0, 0.3²) (PPO clip engaged on both sides at eps 0.2),
+    ref = old + N(0, 0.05²) with 1 % of the rows pushed ±6 beyond the KL clamp (C = 5), group
+    advantages N(0, 1), 1 sequence in 8 overflowing (overlong filter on)."""
     g = torch.Generator(device=DEV).manual_seed(0)
-    logits = (torch.randn((1, T, V), generator=g, device=DEV, dtype=torch.float32) * 3).to(torch.bfloat16)
-    logits.requires_grad_(True)
-    seq = 2048
+    logits = torch.empty((1, T, V), device=DEV, dtype=torch.bfloat16)
+    for a in range(0, T, 8192):
+        logits[0, a:a + 8192] = (torch.randn((min(8192, T - a), V), generator=g, device=DEV) * 3).to(torch.bfloat16)
     nseq = T // seq
     pos = torch.arange(T, device=DEV) % seq
     ids = torch.randint(0, 151643, (1, T), generator=g, device=DEV)
     labels = torch.where(pos[None] >= 256, ids, torch.full_like(ids, -100))
+    # an independent (ATen) target log-prob, only to centre old_logprobs near the policy's own
+    lp = torch.zeros((1, T), device=DEV)
+    for a in range(0, T - 1, 4096):
+        b = min(a + 4096, T - 1)
+        ls = torch.log_softmax(logits[0, a:b].float(), dim=-1)
+        lp[0, a + 1:b + 1] = ls.gather(1, ids[0, a + 1:b + 1, None])[:, 0]
+        del ls
+    per_seq = lambda x: torch.repeat_interleave(x, seq)[None]  # noqa: E731
+    old = lp + 0.3 * torch.randn((1, T), generator=g, device=DEV)
+    far = (torch.rand((1, T), generator=g, device=DEV) < 0.01).float() * \
+        torch.where(torch.rand((1, T), generator=g, device=DEV) < 0.5, -6.0, 6.0)
+    ref = old + 0.05 * torch.randn((1, T), generator=g, device=DEV) + far
+    lab = labels != -100
     f = {"input_ids": ids, "labels": labels,
-         "rewards": torch.repeat_interleave(torch.randint(0, 2, (nseq,), device=DEV).float(), seq)[None],
-         "ref_logprobs": torch.randn((1, T), device=DEV) - 8, "old_logprobs": torch.randn((1, T), device=DEV) - 8,
+         "rewards": per_seq(torch.randint(0, 2, (nseq,), generator=g, device=DEV).float()),
+         "advantages": per_seq(torch.randn((nseq,), generator=g, device=DEV)),
+         "ref_logprobs": torch.where(lab, ref, 0.0), "old_logprobs": torch.where(lab, old, 0.0),
          "group_tokens": torch.full((1, T), float(seq), device=DEV),
-         "num_labels": torch.full((1, T), float(seq - 256), device=DEV), "overflow": torch.zeros((1, T), device=DEV)}
-    f["advantages"] = f["rewards"] - 0.5
-    f = {k: v.contiguous() for k, v in f.items()}
-    p = GrpoParams(policy_loss="ppo", epsilon=4.0, kl_coef=0.001, entropy_coef=0.0, clamp_log_ratio=5.0,
-                   batch_size=256.0)
-    loss1, stats1, rows1 = grpo_loss(logits, prepare_fields(f, logits.device), p)
+         "num_labels": torch.full((1, T), float(seq - 256), device=DEV),
+         "overflow": per_seq((torch.arange(nseq, device=DEV) % 8 == 3).float())}
+    return logits, {k: v.contiguous() for k, v in f.items()}, pos
+
+
+C2_CFG = dict(policy_loss="ppo", epsilon=0.2, kl_coef=0.001, final_kl_coef=0.001, entropy_bonus=0.001,
+              final_entropy_bonus=0.001, clamp_log_ratio_ref_new_value=5.0, batch_size=256, temperature=1.0,
+              overlong_filtering=True)
+
+
+def _c2_params(cfg: dict):
+    from pipelinerl_amd.finetune.rl.fused import GrpoParams
+
+    return GrpoParams(policy_loss=cfg["policy_loss"], epsilon=cfg["epsilon"], kl_coef=cfg["kl_coef"],
+                      entropy_coef=cfg["entropy_bonus"], clamp_log_ratio=cfg["clamp_log_ratio_ref_new_value"],
+                      batch_size=float(cfg["batch_size"]), temperature=cfg["temperature"],
+                      overlong_filtering=cfg["overlong_filtering"])
+
+
+def _c2_mismatches(loss: float, stats: dict, rows: np.ndarray, mask: np.ndarray, o: dict) -> list[str]:
+    """Every disagreement of the kernel's loss / statistics / per-row outputs with the oracle's
+    (1e-4 relative to max(1, |x|) on scalars; per row: log-prob / entropy / lse 1e-4, token loss
+    and the upstream row gradients g_lp / g_h 1e-4 relative + 1e-4 of their largest magnitude)."""
+    bad = []
+    if abs(loss - o["loss"]) > 1e-4 * max(1.0, abs(o["loss"])):
+        bad.append(f"loss {loss} vs {o['loss']}")
+    if set(stats) != set(o["stats"]):
+        bad.append(f"stat keys {set(stats) ^ set(o['stats'])}")
+    for k, v in o["stats"].items():
+        if k in stats and not abs(stats[k] - v) <= 1e-4 * max(1.0, abs(v)):
+            bad.append(f"stat {k}: {stats[k]} vs {v}")
+    for i, (name, want) in enumerate((("new_logprobs", o["new_logprobs"][0]), ("entropy", o["entropy"][0]),
+                                      ("lse", o["lse"][0]))):
+        ok, err = rel_close(rows[i], want, 1e-5, 1e-4)
+        if not ok:
+            bad.append(f"rows {name}: max err {err}")
+    for i, name, want in ((3, "token_loss", np.where(mask, o["token_loss"][0], 0.0)), (4, "g_lp", o["g_lp"][0]),
+                          (5, "g_h", o["g_h"][0])):
+        got = np.where(mask, rows[i], 0.0)
+        ok, err = rel_close(got, want, 1e-4, 1e-4 * float(np.abs(want).max()) + 1e-30)
+        if not ok:
+            bad.append(f"rows {name}: max err {err}")
+    return bad
+
+
+@pytest.mark.timeout(1200)
+def test_c2_full_size_vs_oracle():
+    """Config C2 at full size (65 536 packed rows x 151 936 vocab, bf16 logits, 19.9 GB) against the
+    oracle over EVERY row (rl/__init__.py:200-366): loss and all statistics at 1e-4; every row's
+    log-prob, entropy, lse, token loss and upstream gradients (g_lp, g_h); sampled rows' dlogits vs
+    the oracle's own gradient (its g_lp / g_h, not the kernel's) at the bf16 bar 1e-2.  Then:
+    softmax-gradient rows sum to ~0, the kernel is bitwise deterministic, and a negative control
+    (the kernel run with epsilon off by 1 %) must fail the same comparison."""
+    import time
+    import types as _types
+
+    from pipelinerl_amd.finetune.rl import build_stats
+    from pipelinerl_amd.finetune.rl.fused import grpo_loss, prepare_fields
+
+    T, V, seq = 65536, 151936, 2048
+    logits, f, pos = _c2_inputs(T, V, seq)
+    logits.requires_grad_(True)
+    p = _c2_params(C2_CFG)
+    fields = prepare_fields(f, logits.device)
+    loss1, stats1, rows1 = grpo_loss(logits, fields, p)
     loss1.backward()
     d1 = logits.grad
     logits.grad = None
-    loss2, stats2, rows2 = grpo_loss(logits, prepare_fields(f, logits.device), p)
+    loss2, stats2, rows2 = grpo_loss(logits, fields, p)
     loss2.backward()
     assert torch.equal(stats1, stats2) and torch.equal(rows1, rows2)
     assert torch.equal(d1, logits.grad)
+    logits.grad = None
     # sum_j d_j = 0 exactly for the softmax gradient; bf16 storage rounds each d_j by 2^-9
     df = d1[0].float()
     rowsum = df.sum(-1).abs()
@@ -231,21 +305,62 @@ def test_c2_scale_properties():
     assert bool(torch.all(rowsum <= 4e-3 * absum + 1e-12)), float((rowsum / (absum + 1e-30)).max())
     assert int((absum > 0).sum()) > 0
     assert torch.all(d1[0, T - 1] == 0)
-    sample = torch.tensor([0, 1, 255, 256, 257, 4095, 30000, 65534], device=DEV)
-    lg_np = logits.detach()[0, sample].float().cpu().numpy()
-    fn = {k: v.cpu().numpy() for k, v in f.items()}
-    s = sample.cpu().numpy()
-    for j, t in enumerate(s):
-        tok = t + 1
-        lse, H, tlp = grpo_oracle.row_stats(lg_np[j:j + 1], np.array([fn["input_ids"][0, tok]]), None, 1.0)
-        r = rows1[:, t].cpu().numpy()
-        assert abs(r[0] - tlp[0]) <= 1e-4 * max(1, abs(tlp[0])), (t, r[0], tlp[0])
-        assert abs(r[1] - H[0]) <= 1e-4 * max(1, abs(H[0])), (t, r[1], H[0])
-        assert abs(r[2] - lse[0]) <= 1e-4 * max(1, abs(lse[0]))
-        dref = grpo_oracle.row_grad(lg_np[j:j + 1], np.array([fn["input_ids"][0, tok]]), lse, H,
-                                    np.array([r[4]]), np.array([r[5]]), 1.0)[0]
-        ok, err = rel_close(d1[0, t].float().cpu().numpy(), dref, 1e-2, 1e-9)
-        assert ok, (t, err)
+    del df, rowsum, absum
+
+    nseq = T // seq
+    hb = {k: v.cpu().numpy() for k, v in f.items()} | {"position_ids": pos[None].cpu().numpy(), "is_packed": True}
+    meta = _types.SimpleNamespace(is_packed=True, input_ids=f["input_ids"])
+    stats = build_stats(stats1.cpu().numpy(), meta, p, p.kl_coef, p.entropy_coef, nseq, False)
+    # the bf16 logits in fp32 on the host (40 GB), copied in row blocks
+    lg = np.empty((1, T, V), dtype=np.float32)
+    with torch.no_grad():
+        for a in range(0, T, 4096):
+            lg[0, a:a + 4096] = logits[0, a:a + 4096].float().cpu().numpy()
+    mask = hb["labels"][0, 1:] != -100
+    t0 = time.time()
+    o = grpo_oracle.rl_step_oracle(lg, hb, C2_CFG, 0, 10, compute_grad=True, dtype=np.float32, threads=16,
+                                   row_chunk=64, grad_rows=np.array([0]))
+    t_oracle = time.time() - t0
+    r1 = rows1.cpu().numpy()
+    assert o["stats"]["num_output_tokens_sum"] == nseq * (seq - 256)
+    bad = _c2_mismatches(float(loss1.detach()), stats, r1, mask, o)
+    assert not bad, bad
+
+    # the branches the token arithmetic takes at this size (so the comparison above covers them)
+    ratio = np.exp(o["new_logprobs"][0] - hb["old_logprobs"][0, 1:])
+    lrrn = hb["ref_logprobs"][0, 1:] - o["new_logprobs"][0]
+    adv = hb["advantages"][0, 1:]
+    ovf = hb["overflow"][0, 1:] > 0
+    cats = {"clip_hi": mask & (ratio > 1.2) & (adv > 0), "clip_lo": mask & (ratio < 0.8) & (adv < 0),
+            "clip_hi_inactive": mask & (ratio > 1.2) & (adv < 0), "kl_clamp_hi": mask & (lrrn > 5),
+            "kl_clamp_lo": mask & (lrrn < -5), "overflow": mask & ovf, "plain": mask & ~ovf & (np.abs(lrrn) < 5)}
+    for k, c in cats.items():
+        assert c.sum() > 100, (k, int(c.sum()))
+    # sampled rows: the kernel's dlogits vs the ORACLE's gradient of the same logits
+    sample = np.unique(np.concatenate([[0, 1, 255, 256, 257, 4095, 30000, 65534]] +
+                                      [np.nonzero(c)[0][:3] for c in cats.values()]))
+    o_rows = grpo_oracle.rl_step_oracle(lg, hb, C2_CFG, 0, 10, compute_grad=True, dtype=np.float32,
+                                        grad_rows=sample, rows=o)
+    want = o_rows["dlogits_rows"]
+    got = d1[0, torch.tensor(sample, device=DEV)].float().cpu().numpy()
+    assert np.abs(want[mask[sample]]).max() > 0
+    ok, err = rel_close(got, want, 1e-2, 1e-9)
+    assert ok, ("sampled dlogits vs oracle", err)
+    del d1
+
+    # negative control: the kernel with epsilon off by 1 % must fail the same comparison
+    cfg_bad = dict(C2_CFG, epsilon=C2_CFG["epsilon"] * 1.01)
+    pb = _c2_params(cfg_bad)
+    lb, sb, rb = grpo_loss(logits.detach(), fields, pb)
+    stats_b = build_stats(sb.cpu().numpy(), meta, pb, pb.kl_coef, pb.entropy_coef, nseq, False)
+    bad_ctl = _c2_mismatches(float(lb), stats_b, rb.cpu().numpy(), mask, o)
+    assert bad_ctl, "epsilon x 1.01 went undetected"
+    # ... and the oracle with the same perturbation agrees with that kernel run (only the token
+    # arithmetic is redone: the per-row lse / entropy / log-prob of the first pass are reused)
+    ob = grpo_oracle.rl_step_oracle(lg, hb, cfg_bad, 0, 10, compute_grad=True, dtype=np.float32,
+                                    grad_rows=np.array([0]), rows=o)
+    assert not _c2_mismatches(float(lb), stats_b, rb.cpu().numpy(), mask, ob)
+    print(f"C2 full size: oracle {t_oracle:.1f} s over {T} x {V}; negative control caught: {bad_ctl[:3]}")
 
 
 def test_flatten_unflatten_and_sqnorm():

@@ -25,12 +25,14 @@ pytestmark = pytest.mark.skipif(not Path("/opt/rocm/bin/hipcc").exists() and not
 
 
 @pytest.mark.parametrize("src,defines", [("grpo_loss.hip", {}), ("grpo_loss.hip", {"PRL_PHASED_MAX_NV": "24"}),
-                                         ("model_ops.hip", {}), ("flat_pack.hip", {}), ("adamw.hip", {})])
+                                         ("model_ops.hip", {}), ("flat_pack.hip", {}), ("adamw.hip", {}),
+                                         ("attn_bwd.hip", {})])
 def test_no_store_data_hazard(src, defines):
     from isa_store_hazard_scan import compile_isa, scan
 
     isa = compile_isa(CSRC / src, defines, include=[ROOT / "include", CSRC])
     assert "grpo_fwd_resident" in isa or src != "grpo_loss.hip"
+    assert "attn_bwd" in isa or src != "attn_bwd.hip"
     hits = scan(isa)
     assert not hits, hits[:3]
 

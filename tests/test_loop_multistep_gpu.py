@@ -8,11 +8,14 @@ restatement of rl_step (tests/cpu_rl_step.py, pinned to the oracle by test_confi
 autograd accumulation, ``clip_grad_norm_(0.3)`` + ``torch.optim.AdamW`` + the cosine schedule
 (finetune_loop.py:700-719).
 
-Compared per step: every micro-batch's statistics, the pre-clip gradient norm, and each
-parameter's update (bf16 after - before) as one relative norm over the decoder weights.  A negative
-control re-runs the product with the fused gate/up weight cache frozen after its first build (the
-stale-weight bug fixed at the end of round 2) and requires the same comparison to fail by a wide
-margin, so the bounds here are known to catch that class of cross-step bug.
+Compared per step: every micro-batch's statistics, the pre-clip gradient norm, EVERY parameter's
+pre-clip gradient on its own (relative error ||g - g_ref|| / ||g_ref|| and the projected scale
+<g, g_ref> / ||g_ref||², which averages the bf16 noise away and so resolves a 1 % scale error even
+on an 896-element bias), and each parameter's update (bf16 after - before) as one relative norm
+over the decoder weights.  Two negative controls: the product re-run with the fused gate/up weight
+cache frozen after its first build (the stale-weight bug fixed at the end of round 2) must fail the
+update comparison by a wide margin, and a 1 % scale error injected into one bias gradient must fail
+the per-tensor gradient check on exactly that tensor.
 
 Shapes: Qwen2.5-0.5B with 4 of its 24 decoder layers (random init), C1's rollout generator
 (workloads.rollouts("c1", 96)) packed at 4096 tokens, 32 samples per optimizer step, lr 1e-3 (so a
@@ -33,6 +36,9 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 LAYERS, ROLLOUTS, PER_STEP, LR = 4, 96, 32, 1e-3
 UPDATE_BOUND = 0.15  # relative update error per step (below half the stale-cache signal, 0.38 / 0.58)
+STEP_BOUNDS = (0.08, 0.10, UPDATE_BOUND)  # per step, ~1.5x the round-3 measurement 0.048 / 0.061 / 0.117
+GRAD_REL_BOUND = 3e-2  # per tensor ||g - g_ref|| / ||g_ref|| (bf16 backward of the product vs eager HF)
+GRAD_SCALE_BOUND = 3e-3  # per tensor |<g, g_ref> / ||g_ref||² - 1|
 
 
 def _data(tmp_path):
@@ -63,22 +69,28 @@ def _data(tmp_path):
 
 def _product_run(tmp_path, init, stale_cache=False):
     """run_finetuning_loop on the product path; returns (per-step parameter snapshots [fp32 on
-    the device], per-micro-batch stats, per-step pre-clip grad norms)."""
+    the device], per-micro-batch stats, per-step pre-clip grad norms, per-step pre-clip
+    gradients).  PrlAdamW folds the clip multiply into its step, so a step pre-hook sees the
+    accumulated gradients unclipped."""
     from loop_helpers import loop_cfg
 
     import pipelinerl_amd.finetune.rl as rlmod
     from pipelinerl_amd import finetune_loop, workloads
     from pipelinerl_amd.finetune import model_ops
+    from pipelinerl_amd.finetune.optim import PrlAdamW
     from pipelinerl_amd.trainer_probe import qwen2_model
 
     model = qwen2_model("0.5b", torch.device(DEV), layers=LAYERS)
     model.load_state_dict(init)
     snaps = [{n: p.detach().float().clone() for n, p in model.named_parameters()}]
-    stats = []
+    stats, grads = [], []
     orig_get, orig_resolve, orig_fused = finetune_loop.get_optimizer, rlmod.RLStats.resolve, model_ops._fused_weight
 
     def get_optimizer(*a, **k):
         opt = orig_get(*a, **k)
+        assert isinstance(opt, PrlAdamW)  # the clip is deferred: .grad is pre-clip in the pre-hook
+        opt.register_step_pre_hook(lambda o, args, kw: grads.append(
+            {n: p.grad.detach().float().clone() for n, p in model.named_parameters() if p.grad is not None}))
         opt.register_step_post_hook(
             lambda o, args, kw: snaps.append({n: p.detach().float().clone() for n, p in model.named_parameters()}))
         return opt
@@ -117,7 +129,7 @@ def _product_run(tmp_path, init, stale_cache=False):
     norms = [ln["stats/grad_norm"] for ln in lines]
     del model
     torch.cuda.empty_cache()
-    return snaps, stats, norms
+    return snaps, stats, norms, grads
 
 
 def _reference_run(init, steps):
@@ -139,7 +151,7 @@ def _reference_run(init, steps):
         sched = get_scheduler("cosine", opt, 0, len(steps))
         rlc = workloads.rl_config("c1", PER_STEP)
         snaps = [{n: p.detach().float().clone() for n, p in ref.named_parameters()}]
-        stats, norms = [], []
+        stats, norms, grads = [], [], []
         for k, mbs in enumerate(steps):
             for b in mbs:
                 bd = copy.deepcopy(b).to_device(DEV)
@@ -147,6 +159,7 @@ def _reference_run(init, steps):
                 loss, st = cpu_rl_step(ref, bd, k, len(steps), rlc)
                 loss.backward()
                 stats.append(st)
+            grads.append({n: p.grad.detach().float().clone() for n, p in ref.named_parameters() if p.grad is not None})
             norms.append(float(torch.nn.utils.clip_grad_norm_(ref.parameters(), 0.3)))
             opt.step()
             opt.zero_grad(set_to_none=True)
@@ -157,7 +170,28 @@ def _reference_run(init, steps):
             os.environ.pop(k, None) if v is None else os.environ.__setitem__(k, v)
     del ref, opt
     torch.cuda.empty_cache()
-    return snaps, stats, norms
+    return snaps, stats, norms, grads
+
+
+def _grad_errors(got: dict, want: dict) -> dict[str, tuple[float, float]]:
+    """name -> (||g - g_ref|| / ||g_ref||, <g, g_ref> / ||g_ref||² - 1) for every tensor with a
+    non-zero reference gradient; a tensor with a gradient on one side only is an error (inf)."""
+    out = {}
+    for n in set(got) | set(want):
+        if n not in got or n not in want:
+            out[n] = (math.inf, math.inf)
+            continue
+        g, r = got[n].double(), want[n].double()
+        rr = float((r * r).sum())
+        if rr == 0.0:
+            out[n] = (0.0, 0.0) if float(g.abs().max()) == 0.0 else (math.inf, math.inf)
+            continue
+        out[n] = (math.sqrt(float(((g - r) ** 2).sum()) / rr), float((g * r).sum()) / rr - 1.0)
+    return out
+
+
+def _grad_failures(errs: dict) -> list[str]:
+    return sorted(n for n, (rel, sc) in errs.items() if not (rel <= GRAD_REL_BOUND and abs(sc) <= GRAD_SCALE_BOUND))
 
 
 def _update_error(a, b, k, names) -> float:
@@ -180,8 +214,8 @@ def test_c1_three_optimizer_steps_match_the_reference_step(tmp_path):
 
     steps = _data(tmp_path)
     init = {k: v.detach().clone() for k, v in qwen2_model("0.5b", torch.device(DEV), layers=LAYERS).state_dict().items()}
-    ref_snaps, ref_stats, ref_norms = _reference_run(init, steps)
-    snaps, stats, norms = _product_run(tmp_path, init)
+    ref_snaps, ref_stats, ref_norms, ref_grads = _reference_run(init, steps)
+    snaps, stats, norms, grads = _product_run(tmp_path, init)
     n_mb = sum(len(s) for s in steps)
     assert len(stats) == len(ref_stats) == n_mb and len(snaps) == len(ref_snaps) == len(steps) + 1
     layer_names = [n for n in snaps[0] if ".layers." in n and not n.endswith("norm.weight")]
@@ -195,14 +229,28 @@ def test_c1_three_optimizer_steps_match_the_reference_step(tmp_path):
     gn_err = [abs(a - b) / b for a, b in zip(norms, ref_norms)]
     for g, r in zip(stats, ref_stats):
         assert g["num_output_tokens_sum"] == r["num_output_tokens_sum"]
+    # per-tensor pre-clip gradients, step by step
+    assert len(grads) == len(ref_grads) == len(steps)
+    g_errs = [_grad_errors(g, r) for g, r in zip(grads, ref_grads)]
+    worst_rel = [max(e.items(), key=lambda kv: kv[1][0]) for e in g_errs]
+    worst_sc = [max(e.items(), key=lambda kv: abs(kv[1][1])) for e in g_errs]
+    # control: a 1 % scale error in one bias gradient of step 2 fails the check on that tensor only
+    bias = "model.layers.1.self_attn.k_proj.bias"
+    assert bias in grads[1]
+    injected = dict(grads[1])
+    injected[bias] = grads[1][bias] * 1.01
+    ctl = _grad_failures(_grad_errors(injected, ref_grads[1]))
+    del grads, ref_grads
     # negative control: the stale fused-weight cache (round-2 bug) on the same run
-    bad_snaps, bad_stats, bad_norms = _product_run(tmp_path, init, stale_cache=True)
+    bad_snaps, bad_stats, bad_norms, _ = _product_run(tmp_path, init, stale_cache=True)
     bad_upd_mlp = [_update_error(bad_snaps, ref_snaps, k, mlp_names) for k in range(1, len(steps) + 1)]
     bad_st = _stat_error(bad_stats[first:], ref_stats[first:])
     print(json.dumps({"update_rel_err_layers": upd, "update_rel_err_mlp": upd_mlp, "update_rel_err_all": upd_all,
                       "stat_err_step1_later": st_err, "grad_norm_rel_err": gn_err,
                       "stale_cache_update_rel_err_mlp": bad_upd_mlp, "stale_cache_stat_err_later": bad_st,
-                      "grad_norms": norms, "ref_grad_norms": ref_norms}))
+                      "grad_norms": norms, "ref_grad_norms": ref_norms,
+                      "grad_worst_rel_per_step": worst_rel, "grad_worst_scale_per_step": worst_sc,
+                      "grad_tensors_checked": [len(e) for e in g_errs], "injected_bias_control": ctl}))
     # the product's steps == the reference's, step by step.  Measured on MI355X (round 3): update
     # error 0.05 / 0.06 / 0.12 (it grows as the cosine schedule shrinks the step towards the bf16
     # quantum), statistics 2e-5, grad norm 4e-3; the stale cache: 0.05 / 0.38 / 0.58 from step 2
@@ -210,5 +258,9 @@ def test_c1_three_optimizer_steps_match_the_reference_step(tmp_path):
     assert max(st_err) <= 1e-3, st_err
     assert max(upd) <= UPDATE_BOUND and max(upd_mlp) <= UPDATE_BOUND, (upd, upd_mlp)
     assert max(upd_all) <= UPDATE_BOUND, upd_all
+    assert all(u <= b for u, b in zip(upd, STEP_BOUNDS)), (upd, STEP_BOUNDS)
+    for k, e in enumerate(g_errs):
+        assert not _grad_failures(e), (k, {n: e[n] for n in _grad_failures(e)})
+    assert ctl == [bias], ctl
     # ... and the same bound rejects the stale-cache bug at every step from the second on, by 2x
     assert min(bad_upd_mlp[1:]) >= 2 * UPDATE_BOUND, bad_upd_mlp

@@ -69,6 +69,10 @@ def test_split_pipeline_gloo(tmp_path, world, actors):
     assert r0["trainers"] == n_tr and r0["actors"] == actors and r0["updates"] == 3
     assert r0["broadcast_latency_ms"] > 0 and 0.0 <= r0["hidden_frac"] <= 1.0
     assert r0["broadcast_bytes"] == sum(2 * p.numel() for p in got[0]["params"].values())
+    # the census of both groups, as trainer rank 0 saw it: the DP group and the actor group (1 + actors)
+    g = r0["groups"]
+    assert g["split_dp"]["reported"] == g["split_dp"]["participants"] == n_tr
+    assert g["actor"]["reported"] == g["actor"]["participants"] == 1 + actors
     for r in range(n_tr, world):  # actors hold the trainer's last snapshot exactly
         for n, p in got[0]["params"].items():
             assert torch.equal(got[r]["params"][n], p), (r, n)

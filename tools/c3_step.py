@@ -3,7 +3,9 @@ rollouts (trainer_probe.dp_step_probe), for kernel profiles of that workload:
 
     rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c3 -o run -- python3 tools/c3_step.py
 
-Prints the probe's JSON line.
+``--snapshot`` also times the step with WeightUpdateManager's snapshot in flight
+(trainer_probe.snapshot_overlap; its kernel trace shows prl_flatten_bf16 beside the step's kernels,
+tools/kernel_overlap.py).  Prints the probe's JSON line.
 """
 
 from __future__ import annotations
@@ -24,6 +26,7 @@ def main():
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--layers", type=int, default=None)
+    ap.add_argument("--snapshot", action="store_true")
     a = ap.parse_args()
     import gc
     import time
@@ -62,7 +65,7 @@ def main():
     torch.cuda.set_device(0)
 
     r = dp_step_probe(a.config, micro_batches=a.micro_batches, steps=a.steps, warmup=a.warmup,
-                      device=torch.device("cuda", 0), layers=a.layers)
+                      device=torch.device("cuda", 0), layers=a.layers, snapshot=a.snapshot)
     r["host_gc"] = {f"gen{g}": {"n": n, "ms": round(ms, 1)} for g, (n, ms) in gcs.items()}
     print(json.dumps(r), flush=True)
 
