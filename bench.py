@@ -167,6 +167,28 @@ def dp_scaling(world: int, c3: dict | None, trainer: dict | None) -> dict | None
     return out
 
 
+def communicator_census(world: int, ctrl, device, prl_comm: bool = True) -> dict:
+    """The N > 1 line's ``communicators`` object: the default (DP) group, the CPU control group and,
+    with ``prl_comm``, an RCCL communicator of the prl_comm C ABI over all ranks (ncclCommCount), each
+    checked against ``world`` (comm_probe.group_census raises on a mismatch).  The split pipeline's
+    own DP and actor groups are checked inside its probe (``split_pipeline.groups``).  A prl_comm
+    communicator needs one GPU per rank: the one-GPU rehearsal passes ``prl_comm=False``."""
+    from pipelinerl_amd import comm_probe
+
+    groups = {"dp": (None, world), "ctrl": (ctrl, world)}
+    rc = None
+    if prl_comm:
+        from pipelinerl_amd.comm import RcclComm
+
+        rc = RcclComm.from_group(ctrl, device)
+        groups["prl_comm_dp"] = (rc, world)
+    try:
+        return comm_probe.group_census(groups, device)
+    finally:
+        if rc is not None:
+            rc.close()
+
+
 T_START = time.perf_counter()
 
 
@@ -376,23 +398,7 @@ def main():
     if world > 1:
         # every communicator of the run reports the size it was meant to have (and that many ranks
         # take part in an all-reduce over it) before any probe relies on it
-        from pipelinerl_amd import comm_probe
-
-        def communicators():
-            groups = {"dp": (None, world), "ctrl": (ctrl, world)}
-            rc = None
-            if not rehearse:  # a prl_comm RCCL communicator needs one GPU per rank
-                from pipelinerl_amd.comm import RcclComm
-
-                rc = RcclComm.from_group(ctrl, dev)
-                groups["prl_comm_dp"] = (rc, world)
-            try:
-                return comm_probe.group_census(groups, dev)
-            finally:
-                if rc is not None:
-                    rc.close()
-
-        census = optional("communicators", communicators)
+        census = optional("communicators", lambda: communicator_census(world, ctrl, dev, prl_comm=not rehearse))
     c3 = None
     if not args.no_c3:
         # configs[2] (C3): Qwen2.5-7B DP trainer step on C3's packed math rollouts, with the full

@@ -21,8 +21,11 @@ v, the attention output, the residual stream, gate, up and the SwiGLU output), t
 label-row logits chunk; the build's own long-lived buffers (the fused gate/up weight cache,
 2 I x H per layer when finetune/model_ops.py fuses the projection at this micro-batch size and the
 model is not FSDP-sharded; the lm_head weight gradient's staging, [V, H] bf16 from the single-chunk
-GEMM or an fp32 accumulator over several chunks, finetune/rl/fused_linear.py); 5 % of the device
-plus 4 GiB of headroom.
+GEMM or an fp32 accumulator over several chunks, finetune/rl/fused_linear.py); under FSDP, the
+unsharded working set of its largest unit (gathered parameters, unsharded gradients, reduce-scatter
+input) and of two decoder layers (fsdp_transient_bytes); 5 % of the device plus 4 GiB of headroom.
+Checked against the measured steady-state peak of a 32B-shaped FSDP model (tests/test_fsdp_32b_gpu.py:
+estimate without the headroom between 1x and 1.3x the measured peak).
 """
 
 from __future__ import annotations
@@ -85,9 +88,30 @@ def build_buffer_bytes(config, seq: int, chunk: int, shard_world: int, dtype_byt
         heads = int(getattr(config, "num_attention_heads", 1))
         kv = int(getattr(config, "num_key_value_heads", None) or heads) * (H // heads)
         out += (H + 2 * kv) * H * layers * dtype_bytes
-    # lm_head dW: bf16 from one GEMM (one chunk) or an fp32 accumulator (several chunks)
-    out += vocab * H * (dtype_bytes if seq <= chunk else 4)
+    # lm_head dW: bf16 from one GEMM (one chunk) or an fp32 accumulator (several chunks); an
+    # FSDP-sharded model takes the full-logits loss head (rl_step), its lm_head gradient is the
+    # root unit's unsharded gradient, counted in fsdp_transient_bytes
+    if shard_world <= 1:
+        out += vocab * H * (dtype_bytes if seq <= chunk else 4)
     return out
+
+
+def fsdp_transient_bytes(model, shard_world: int) -> int:
+    """FSDP2's unsharded working set at its peak (upper bound): the largest unit (the root: embedding,
+    lm_head and final norm, or one decoder layer) gathered, its unsharded gradients and the
+    reduce-scatter input FSDP copies them into (3 x its full size), plus one decoder layer in use and
+    the next one prefetched (2 x a layer).  0 when not sharded."""
+    if shard_world <= 1:
+        return 0
+    from .sharding import decoder_layers
+
+    def nbytes(params) -> int:
+        return sum(p.numel() * p.element_size() for p in params)
+
+    layers = decoder_layers(model)
+    layer = max((nbytes(m.parameters()) for m in layers), default=0)
+    root = nbytes(model.parameters()) - sum(nbytes(m.parameters()) for m in layers)
+    return 3 * max(root, layer) + 2 * layer
 
 
 def plan_gradient_checkpointing(args, model, device: torch.device, shard_world: int = 1,
@@ -118,7 +142,8 @@ def plan_gradient_checkpointing(args, model, device: torch.device, shard_world: 
     rl = args.get("rl", None) or {}
     chunk = min(int(seq), int(rl.get("lm_head_chunk_rows", 65536) or 65536))  # RLConfig default
     logits = chunk * vocab * pbytes
-    buffers = build_buffer_bytes(config, int(seq), chunk, int(shard_world), pbytes)
+    buffers = build_buffer_bytes(config, int(seq), chunk, int(shard_world), pbytes) + \
+        fsdp_transient_bytes(model, int(shard_world))
     need = state + act + logits + buffers + int(HEADROOM_FRAC * total) + HEADROOM_BYTES
     keep = need <= total
     plan = RecomputePlan(not keep, ("activations fit: no recompute" if keep else "activations do not fit: recompute"),

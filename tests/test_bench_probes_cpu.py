@@ -41,7 +41,8 @@ def _main(rank, world, port, out):
         dist.all_reduce(t)
         return {"sum": float(t)}
 
-    res = {"everywhere": r.run("everywhere", everywhere), "after_all": r.run("after_all", collective),
+    census = r.run("communicators", lambda: bench.communicator_census(world, ctrl, "cpu", prl_comm=False))
+    res = {"census": census, "everywhere": r.run("everywhere", everywhere), "after_all": r.run("after_all", collective),
            "flaky": r.run("flaky", flaky), "after": r.run("after", collective), "wall": r.wall}
     Path(out, f"r{rank}.json").write_text(json.dumps(res))
     dist.destroy_process_group()
@@ -53,7 +54,13 @@ def test_probe_failures_shared_and_partial_failure_skips_later_probes(tmp_path):
     for r in (r0, r1):
         assert "out of memory" in r["everywhere"]["error"]
         assert r["after_all"]["sum"] == 2.0  # a failure on every rank: the next probe still runs
-        assert set(r["wall"]) == {"everywhere", "after_all", "flaky", "after"} and r["after_all"]["wall_s"] >= 0
+        assert set(r["wall"]) == {"communicators", "everywhere", "after_all", "flaky", "after"}
+        assert r["after_all"]["wall_s"] >= 0
+        # the N > 1 line's communicator census: every group at the intended size
+        c = r["census"]
+        assert {k for k in c if not k.endswith("_s") and k != "host_rss_gib_after"} == {"dp", "ctrl"}, c
+        for k in ("dp", "ctrl"):
+            assert c[k]["reported"] == c[k]["participants"] == c[k]["intended"] == 2 and c[k]["ok"]
         assert "flaky" in r["after"]["skipped"]  # a failure on one rank: later probes are skipped
     assert "error" in r1["flaky"] and "out of memory" in r1["flaky"]["error"]
     assert r0["flaky"]["error_on_another_rank"] is True and r0["flaky"]["value"] == 1

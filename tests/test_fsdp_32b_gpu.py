@@ -18,9 +18,9 @@ parameters after the forward and gathers them again for the backward.  Each rank
      layout) and every received region is bit-identical to the trainer's gathered parameter;
   3. the gradient-checkpointing plan (finetune/recompute.py, ``gradient_checkpointing_policy:
      auto`` against conf/finetune/base.yaml:44-45): its estimate for this model at 4 096 tokens,
-     without the fixed headroom (5 % of the device + 4 GiB), is >= the measured peak
-     (torch.cuda.max_memory_allocated over forward + backward + AdamW step, no recompute) and
-     <= 1.3 x it.
+     without the fixed headroom (5 % of the device + 4 GiB), is >= the measured peak of the
+     steady-state step (torch.cuda.max_memory_allocated over the second step's forward + backward +
+     AdamW step, the moments resident, no recompute) and <= 1.3 x it.
 """
 
 from __future__ import annotations
@@ -75,34 +75,41 @@ def _run(rank: int, port: int, tmp: str):
     out: dict = {}
     model = shard_model(qwen2_model("32b", dev, layers=LAYERS))
     opt = get_optimizer("adamw_torch", model, 1e-6, 0.01)
+    batch = _batch(rank)
+
+    def step():
+        loss, stats = rl_step(model, batch, 0, 10, _cfg(), defer_stats=True)
+        loss.backward()
+        st = stats.resolve()
+        assert st["kl"] > 0 and st["num_output_tokens_sum"] == (T // SEQ) * (SEQ - PROMPT)
+
+    # step 1: the sharded gradients of the initial weights, gathered (collective) to the host
+    step()
+    grads = {}
+    for n, p in model.named_parameters():
+        full = p.grad.full_tensor()
+        if rank == 0:
+            grads[n] = full.float().cpu()
+        del full
+    clip_grad_norm(model.parameters(), 0.3, opt)
+    opt.step()
+    opt.zero_grad(set_to_none=True)
+    # step 2, the steady state (AdamW moments resident through the backward): its peak memory
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
     torch.cuda.reset_peak_memory_stats(dev)
-    base = torch.cuda.memory_allocated(dev)
-    loss, stats = rl_step(model, _batch(rank), 0, 10, _cfg(), defer_stats=True)
-    loss.backward()
-    st = stats.resolve()
-    assert st["kl"] > 0 and st["num_output_tokens_sum"] == (T // SEQ) * (SEQ - PROMPT)
-    grads_dt = {n: p.grad for n, p in model.named_parameters()}
+    out["base_bytes"] = int(torch.cuda.memory_allocated(dev))
+    step()
     clip_grad_norm(model.parameters(), 0.3, opt)
     opt.step()
+    opt.zero_grad(set_to_none=True)
     torch.cuda.synchronize()
     out["peak_bytes"] = int(torch.cuda.max_memory_allocated(dev))
-    out["base_bytes"] = int(base)
     args = {"gradient_checkpointing": True, "gradient_checkpointing_policy": "auto", "seq_length": T,
             "rl": {"lm_head_chunk_rows": 65536}}
     plan = plan_gradient_checkpointing(args, model, dev, shard_world=2)
     out["plan"] = plan.as_dict()
     out["estimate_bytes"] = plan.state_bytes + plan.activation_bytes + plan.logits_bytes + plan.buffer_bytes
-    # the sharded gradients, gathered (collective), to the host
-    grads = {}
-    for n, g in grads_dt.items():
-        full = g.full_tensor()
-        if rank == 0:
-            grads[n] = full.float().cpu()
-        del full
-    del grads_dt
-    opt.zero_grad(set_to_none=True)
 
     # ---- weight update: rank 0 trains and sends, rank 1 also holds the actor --------------------
     named = list(model.named_parameters())

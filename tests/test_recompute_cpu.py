@@ -89,7 +89,9 @@ def test_label_row_chunk_sizes_the_logits(m7b):
 def test_build_buffers_are_counted(m7b, monkeypatch):
     """The fused gate/up weight cache (2 I H per layer, when fused at this micro-batch size and not
     sharded) and the lm_head dW staging ([V, H]: bf16 for one chunk, fp32 over several) enter the
-    estimate: at the 7B shapes 7.6 GB + 1.1 GB; at 32B under FSDP only the dW term."""
+    estimate: at the 7B shapes 7.6 GB + 1.1 GB; at 32B under FSDP, FSDP's unsharded
+    working set instead (3 x the root unit — embedding, lm_head, norm — plus 2 decoder layers; the
+    lm_head gradient is the root's unsharded gradient there)."""
     from pipelinerl_amd.finetune import model_ops
     from pipelinerl_amd.finetune.recompute import plan_gradient_checkpointing
 
@@ -111,7 +113,9 @@ def test_build_buffers_are_counted(m7b, monkeypatch):
     base = p.state_bytes + p.activation_bytes + p.logits_bytes
     dev = int((base + (4 << 30) + cache // 2) / 0.95)
     assert plan_gradient_checkpointing(_args(), m7b, cuda, device_bytes=dev).checkpoint
-    # 32B under FSDP 4: no fused cache (off under sharding), the dW term only
+    # 32B under FSDP 4: no fused cache (off under sharding), FSDP's transients
     m32 = _meta_model("32b")
     p32 = plan_gradient_checkpointing(_args(seq_length=4096), m32, cuda, shard_world=4, device_bytes=288 * GB)
-    assert p32.buffer_bytes == 152064 * 5120 * 2 and not p32.checkpoint, p32.as_dict()
+    root = (2 * 152064 * 5120 + 5120) * 2
+    layer = (2 * 5120 * 5120 + 2 * 1024 * 5120 + 3 * 27648 * 5120 + 5120 + 2 * 1024 + 2 * 5120) * 2
+    assert p32.buffer_bytes == 3 * root + 2 * layer and not p32.checkpoint, p32.as_dict()
