@@ -22,8 +22,9 @@ label-row logits chunk; the build's own long-lived buffers (the fused gate/up we
 2 I x H per layer when finetune/model_ops.py fuses the projection at this micro-batch size and the
 model is not FSDP-sharded; the lm_head weight gradient's staging, [V, H] bf16 from the single-chunk
 GEMM or an fp32 accumulator over several chunks, finetune/rl/fused_linear.py); under FSDP, the
-unsharded working set of its largest unit (gathered parameters, unsharded gradients, reduce-scatter
-input) and of two decoder layers (fsdp_transient_bytes); 5 % of the device plus 4 GiB of headroom.
+larger of its two unsharded working sets (fsdp_transient_bytes: the start of the backward with the
+logits' gradient, the root unit gathered, the lm_head's unsharded gradient and two decoder layers;
+the root's reduce-scatter with 3 x the root); 5 % of the device plus 4 GiB of headroom.
 Checked against the measured steady-state peak of a 32B-shaped FSDP model (tests/test_fsdp_32b_gpu.py:
 estimate without the headroom between 1x and 1.3x the measured peak).
 """
@@ -96,13 +97,9 @@ def build_buffer_bytes(config, seq: int, chunk: int, shard_world: int, dtype_byt
     return out
 
 
-def fsdp_transient_bytes(model, shard_world: int) -> int:
-    """FSDP2's unsharded working set at its peak (upper bound): the largest unit (the root: embedding,
-    lm_head and final norm, or one decoder layer) gathered, its unsharded gradients and the
-    reduce-scatter input FSDP copies them into (3 x its full size), plus one decoder layer in use and
-    the next one prefetched (2 x a layer).  0 when not sharded."""
-    if shard_world <= 1:
-        return 0
+def fsdp_unit_bytes(model) -> tuple[int, int]:
+    """(root unit, largest decoder-layer unit) parameter bytes of an FSDP-wrapped model (or of the
+    model that will be wrapped): the root holds the embedding, lm_head and final norm."""
     from .sharding import decoder_layers
 
     def nbytes(params) -> int:
@@ -111,7 +108,23 @@ def fsdp_transient_bytes(model, shard_world: int) -> int:
     layers = decoder_layers(model)
     layer = max((nbytes(m.parameters()) for m in layers), default=0)
     root = nbytes(model.parameters()) - sum(nbytes(m.parameters()) for m in layers)
-    return 3 * max(root, layer) + 2 * layer
+    return root, layer
+
+
+def fsdp_transient_bytes(model, shard_world: int, act: int, logits: int, head_grad: int) -> int:
+    """FSDP2's unsharded working set beyond the activations (upper bound), the larger of its two
+    peaks in a step: (a) the start of the backward — every activation, the logits' gradient (the
+    full-logits loss head writes it beside the logits), the root unit gathered, the lm_head's
+    unsharded gradient and a decoder layer in use plus the next prefetched; (b) the root's
+    reduce-scatter at the end of the backward — the root gathered, its unsharded gradients and the
+    reduce-scatter input FSDP copies them into (3 x the root).  Returned as that peak minus ``act``
+    (the plan adds the activations itself).  0 when not sharded."""
+    if shard_world <= 1:
+        return 0
+    root, layer = fsdp_unit_bytes(model)
+    start = act + logits + root + head_grad + 2 * layer
+    end = 3 * root
+    return max(start, end) - act
 
 
 def plan_gradient_checkpointing(args, model, device: torch.device, shard_world: int = 1,
@@ -142,8 +155,9 @@ def plan_gradient_checkpointing(args, model, device: torch.device, shard_world: 
     rl = args.get("rl", None) or {}
     chunk = min(int(seq), int(rl.get("lm_head_chunk_rows", 65536) or 65536))  # RLConfig default
     logits = chunk * vocab * pbytes
+    head = 0 if getattr(config, "tie_word_embeddings", False) else vocab * int(config.hidden_size) * pbytes
     buffers = build_buffer_bytes(config, int(seq), chunk, int(shard_world), pbytes) + \
-        fsdp_transient_bytes(model, int(shard_world))
+        fsdp_transient_bytes(model, int(shard_world), act, logits, head)
     need = state + act + logits + buffers + int(HEADROOM_FRAC * total) + HEADROOM_BYTES
     keep = need <= total
     plan = RecomputePlan(not keep, ("activations fit: no recompute" if keep else "activations do not fit: recompute"),

@@ -12,8 +12,9 @@ same number of forward/backward passes, which FSDP's collectives require.
     boundary micro-batch only (the reference's ``no_sync``), unless
     ``fsdp_sync_every_micro_batch`` trades bandwidth for the unsharded gradient memory;
   * ``grad_reduce: sum`` sets the divide factor to 1 (sum instead of mean), as GradBuckets does;
-  * weight snapshot for the actors: parameters are gathered bucket by bucket (every rank takes
-    part in each all-gather), rank 0 packs them into its bf16 staging buffer (weight_update.py);
+  * weight snapshot for the actors: parameters are gathered FSDP unit by unit (one all-gather of
+    each unit's flat shard, every rank takes part), rank 0 packs them into its bf16 staging buffer
+    (weight_update.py);
   * checkpoints: full HF weights on rank 0 (``current/``) and the sharded optimizer state with
     torch.distributed.checkpoint (``training_state/optim/``).
 """
@@ -82,24 +83,49 @@ def set_gradient_sync(model, enabled: bool) -> None:
         model.set_requires_gradient_sync(enabled)
 
 
-def gather_buckets(named: list[tuple[str, torch.Tensor]], bucket_bytes: int
-                   ) -> Iterator[list[tuple[int, torch.Tensor]]]:
-    """Yield [(index, full tensor)] buckets of the (possibly DTensor-sharded) parameters; every
-    rank must iterate it (each full_tensor() is an all-gather)."""
-    from torch.distributed.tensor import DTensor
+def fsdp_units(model) -> list[tuple[str, torch.nn.Module, list[tuple[str, torch.nn.Parameter]]]]:
+    """The FSDP units of a sharded model (each decoder layer, then the root) with the parameters each
+    unit owns: [(unit prefix, unit, [(FQN, parameter)])], nested units' parameters excluded."""
+    from torch.distributed.fsdp import FSDPModule
 
-    cur: list[tuple[int, torch.Tensor]] = []
-    size = 0
-    for i, (_, p) in enumerate(named):
-        t = p.detach()
-        full = t.full_tensor() if isinstance(t, DTensor) else t
-        cur.append((i, full.contiguous()))
-        size += full.numel() * full.element_size()
-        if size >= bucket_bytes:
-            yield cur
-            cur, size = [], 0
-    if cur:
-        yield cur
+    units = [(name, m) for name, m in model.named_modules() if isinstance(m, FSDPModule)]
+    unit_ids = {id(m) for _, m in units}
+    out = []
+    for prefix, unit in units:
+        nested = [n + "." for n, sub in unit.named_modules() if sub is not unit and id(sub) in unit_ids]
+        own = []
+        for n, p in unit.named_parameters():
+            if not any(n.startswith(x) for x in nested):
+                own.append((f"{prefix}.{n}" if prefix else n, p))
+        out.append((prefix, unit, own))
+    out.sort(key=lambda u: u[0] == "")  # decoder layers first, the root (embedding, lm_head) last
+    return out
+
+
+def gather_units(model) -> Iterator[list[tuple[str, torch.Tensor]]]:
+    """Yield each FSDP unit's parameters unsharded, [(FQN, full tensor)], one unit at a time: ONE
+    all-gather per unit (``FSDPModule.unshard``, the same flat collective FSDP's forward issues;
+    ~65 for a 64-layer model instead of one per tensor), resharded when the caller asks for the next
+    unit.  The caller's reads of the tensors are enqueued on the current stream before the reshard;
+    the freed storage is recorded on that stream, so FSDP's next all-gather cannot reuse it early.
+    Every rank must iterate it to the end."""
+    stream = torch.cuda.current_stream() if torch.cuda.is_available() else None
+    for _, unit, own in fsdp_units(model):
+        unit.unshard()
+        try:
+            # after unshard the modules hold the unsharded parameters under the same names
+            full = []
+            for n, _ in own:
+                mod_name, _, attr = n.rpartition(".")
+                mod = model.get_submodule(mod_name) if mod_name else model
+                full.append((n, getattr(mod, attr)))
+            yield [(n, t.detach()) for n, t in full]
+            if stream is not None:
+                for _, t in full:
+                    if t.is_cuda:
+                        t.record_stream(stream)
+        finally:
+            unit.reshard()
 
 
 def full_state_dict(model) -> dict:

@@ -241,14 +241,20 @@ class WeightUpdateManager:
         dev = named[0][1].device
         if sharded:
             # FSDP (finetune_loop.py:222-247 gathers a FULL_STATE_DICT): every rank takes part in
-            # the bucketed all-gathers, rank 0 packs each bucket into its staging buffer in
-            # stream order, so the snapshot precedes the next optimizer step without an event.
-            from .finetune.sharding import gather_buckets
+            # one all-gather per FSDP unit, rank 0 packs each unit's parameters into its staging
+            # buffer in stream order, so the snapshot precedes the next optimizer step without an event.
+            from .finetune.sharding import gather_units
 
             flat = self._ensure_staging(layout.total, dev) if self.is_main else None
-            for bucket in gather_buckets(named, self.bucket_bytes):
+            index = {n: i for i, (n, _) in enumerate(named)}
+            seen = set()
+            for unit in gather_units(unwrap_model(self.model)):
+                seen.update(n for n, _ in unit)
                 if self.is_main:
-                    self.packer.flatten([t for _, t in bucket], [layout.offsets[i] for i, _ in bucket], flat)
+                    self.packer.flatten([t for _, t in unit], [layout.offsets[index[n]] for n, _ in unit], flat)
+            if seen != set(index):
+                raise RuntimeError(f"FSDP units do not cover the model's parameters: missing {sorted(set(index) - seen)[:4]}, "
+                                   f"extra {sorted(seen - set(index))[:4]}")
             if not self.is_main:
                 return
         request = WeightUpdateRequest(version=version, parameters_info=infos, transport=self.transport,

@@ -11,11 +11,14 @@ parameters after the forward and gathers them again for the backward.  Each rank
   1. gradients: the sharded (reduce-scattered, mean over the ranks) gradient of every parameter
      equals one unsharded model's gradient of the mean of both ranks' losses, per tensor within
      the bf16 GEMM bar (relative norm 2e-2; the unsharded side runs the label-row lm_head, the
-     sharded side the full-logits loss head);
-  2. weight update: after the optimizer step, rank 0's WeightUpdateManager snapshot (bucketed
-     all-gathers, HIP flatten) is broadcast to an actor held by rank 1, once per transport
+     sharded side the full-logits loss head).  Each rank compares its own shards with the matching
+     rows of the unsharded gradient (which every rank computes), the test sums the parts: no
+     DTensor.full_tensor() gathers (gloo runs those at ~20 MB/s);
+  2. weight update: after the optimizer steps, rank 0's WeightUpdateManager snapshot (one FSDP
+     all-gather per unit, HIP flatten) is broadcast to an actor held by rank 1, once per transport
      (per_tensor into a trainer-layout actor, bucketed into vLLM's fused qkv_proj / gate_up_proj
-     layout) and every received region is bit-identical to the trainer's gathered parameter;
+     layout); every received region's bf16 bit-pattern digests (two integer sums, the second
+     position-weighted) equal the sum of the trainer's shard digests;
   3. the gradient-checkpointing plan (finetune/recompute.py, ``gradient_checkpointing_policy:
      auto`` against conf/finetune/base.yaml:44-45): its estimate for this model at 4 096 tokens,
      without the fixed headroom (5 % of the device + 4 GiB), is >= the measured peak of the
@@ -54,7 +57,22 @@ def _cfg():
     return rl_config(2 * (T // SEQ), kl_coef=0.001)
 
 
+def _say(rank: int, t0: float, what: str) -> None:
+    """Progress on stdout (a silent multi-minute GPU test looks hung to the box's watchdog)."""
+    import time
+
+    print(f"[rank {rank} +{time.time() - t0:.0f}s] {what}", flush=True)
+
+
 def _run(rank: int, port: int, tmp: str):
+    import time
+
+    import threading
+
+    t0 = time.time()
+    beat = threading.Event()
+    threading.Thread(target=lambda: [_say(rank, t0, "running") for _ in iter(lambda: beat.wait(60.0), True)],
+                     daemon=True).start()
     sys.path[:0] = [str(ROOT), str(ROOT / "pipelinerl-swe_amd"), str(ROOT / "tests")]
     os.environ["OMP_NUM_THREADS"] = "4"
     import torch.distributed as dist
@@ -76,6 +94,7 @@ def _run(rank: int, port: int, tmp: str):
     model = shard_model(qwen2_model("32b", dev, layers=LAYERS))
     opt = get_optimizer("adamw_torch", model, 1e-6, 0.01)
     batch = _batch(rank)
+    _say(rank, t0, "sharded model built")
 
     def step():
         loss, stats = rl_step(model, batch, 0, 10, _cfg(), defer_stats=True)
@@ -83,14 +102,11 @@ def _run(rank: int, port: int, tmp: str):
         st = stats.resolve()
         assert st["kl"] > 0 and st["num_output_tokens_sum"] == (T // SEQ) * (SEQ - PROMPT)
 
-    # step 1: the sharded gradients of the initial weights, gathered (collective) to the host
+    # step 1: this rank's shards of the gradients of the initial weights (kept on the device)
     step()
-    grads = {}
-    for n, p in model.named_parameters():
-        full = p.grad.full_tensor()
-        if rank == 0:
-            grads[n] = full.float().cpu()
-        del full
+    _say(rank, t0, "step 1 forward + backward")
+    # (to the host: the device holds only what the trainer itself holds while the peak is measured)
+    g_local = {n: (p.grad.to_local().detach().cpu(), _offset(p)) for n, p in model.named_parameters()}
     clip_grad_norm(model.parameters(), 0.3, opt)
     opt.step()
     opt.zero_grad(set_to_none=True)
@@ -105,6 +121,7 @@ def _run(rank: int, port: int, tmp: str):
     opt.zero_grad(set_to_none=True)
     torch.cuda.synchronize()
     out["peak_bytes"] = int(torch.cuda.max_memory_allocated(dev))
+    _say(rank, t0, f"step 2 done, peak {out['peak_bytes'] / 1e9:.2f} GB")
     args = {"gradient_checkpointing": True, "gradient_checkpointing_policy": "auto", "seq_length": T,
             "rl": {"lm_head_chunk_rows": 65536}}
     plan = plan_gradient_checkpointing(args, model, dev, shard_world=2)
@@ -114,7 +131,9 @@ def _run(rank: int, port: int, tmp: str):
     # ---- weight update: rank 0 trains and sends, rank 1 also holds the actor --------------------
     named = list(model.named_parameters())
     infos = parameters_info(named)
-    checks = {}
+    # this rank's share of every parameter's bit-pattern digest (sums over ranks = the full tensor's)
+    out["param_digest_part"] = {n: _digest(p.detach().to_local(), _offset(p)) for n, p in named}
+    out["actor_digest"] = {}
     for version, (transport, layout) in enumerate((("per_tensor", "trainer"), ("bucketed", "vllm")), start=1):
         wum = WeightUpdateManager([], model, None, dist.group.WORLD, transport=transport, bucket_bytes=256 << 20,
                                   overlap=True, is_main=rank == 0, write_message=lambda s, m: None)
@@ -125,46 +144,73 @@ def _run(rank: int, port: int, tmp: str):
                     p.zero_()
             worker = StandaloneWorker(actor, rank=0, device=dev, layout=layout)
             worker.process_group = dist.group.WORLD
-        wum.send_weight_update(version)  # every rank takes part in the bucketed all-gathers
+        wum.send_weight_update(version)  # every rank takes part in the per-unit all-gathers
         if rank == 1:
             worker.receive_weight_update(WeightUpdateRequest(
                 version=version, parameters_info=infos, transport=transport,
                 bucket_bytes=256 << 20 if transport == "bucketed" else 0))
+            held = worker.model_runner.model
+            out["actor_digest"][transport] = {i.name: _digest(held.direct_target(i.name, tuple(i.shape)), 0)
+                                              for i in infos}
+            del worker, actor, held
         else:
             wum.wait()
         wum.close()
         torch.cuda.synchronize()
-        equal, n = 0, 0
-        for name, p in named:
-            full = p.detach().full_tensor().to(torch.bfloat16)  # collective: both ranks
-            if rank == 1:
-                got = worker.model_runner.model.direct_target(name, tuple(full.shape))
-                n += 1
-                equal += int(got is not None and torch.equal(got, full))
-        if rank == 1:
-            checks[transport] = {"equal": equal, "tensors": n, "layout": layout}
-            del worker, actor
-            torch.cuda.empty_cache()
-    out["weight_update"] = checks
+        torch.cuda.empty_cache()
+        _say(rank, t0, f"weight update {transport} done")
 
-    if rank == 0:  # unsharded model, same init: gradient of the mean of both ranks' losses
-        ref = qwen2_model("32b", dev, layers=LAYERS)
-        total = None
-        for r in range(2):
-            lo, _ = rl_step(ref, _batch(r), 0, 10, _cfg())
-            total = lo * 0.5 if total is None else total + lo * 0.5
-        total.backward()
-        errs = {}
-        for name, p in ref.named_parameters():
-            r, g = p.grad.float().cpu().double(), grads[name].double()
-            rr = float((r * r).sum())
-            errs[name] = math.sqrt(float(((g - r) ** 2).sum()) / rr) if rr > 0 else float(g.abs().max())
-        out["grad_rel_err"] = errs
-        del ref
+    # ---- the unsharded model, same init, on every rank: the gradient of the mean of both ranks'
+    # losses; each rank compares its own gradient shards with the matching rows
+    del opt
+    model = None
+    torch.cuda.empty_cache()
+    ref = qwen2_model("32b", dev, layers=LAYERS)
+    total = None
+    for r in range(2):
+        lo, _ = rl_step(ref, _batch(r), 0, 10, _cfg())
+        total = lo * 0.5 if total is None else total + lo * 0.5
+    total.backward()
+    parts = {}
+    for name, p in ref.named_parameters():
+        g, off = g_local[name]
+        rows = p.grad.reshape(p.shape[0], -1)[off // max(1, p[0].numel()):][:g.shape[0]].double().reshape(g.shape)
+        g = g.to(dev).double()
+        parts[name] = [float((g * rows).sum()), float((rows * rows).sum()), float(((g - rows) ** 2).sum()),
+                       g.numel()]
+    out["grad_part"] = parts
+    del ref
+    _say(rank, t0, "unsharded reference gradients compared")
     with open(Path(tmp) / f"rank{rank}.json", "w") as f:
         json.dump(out, f)
+    beat.set()
     dist.barrier()
     dist.destroy_process_group()
+
+
+def _offset(p) -> int:
+    """Flat element offset of this rank's shard of the (Shard(0)) DTensor ``p`` in the full tensor."""
+    from torch.distributed.tensor._utils import compute_local_shape_and_global_offset
+
+    _, goff = compute_local_shape_and_global_offset(p.shape, p.device_mesh, p.placements)
+    row = 1
+    for d in p.shape[1:]:
+        row *= d
+    assert all(o == 0 for o in goff[1:]), goff
+    return int(goff[0]) * row
+
+
+def _digest(t: torch.Tensor, offset: int) -> list[int]:
+    """Two integer sums over a bf16 tensor's bit patterns, the second weighted by each element's flat
+    position in the full tensor (``offset`` + local index): additive over the shards of one tensor."""
+    x = t.detach().to(torch.bfloat16).contiguous().reshape(-1).view(torch.int16)
+    s0 = s1 = 0
+    for a in range(0, x.numel(), 1 << 26):
+        c = x[a:a + (1 << 26)].to(torch.int64)
+        w = (torch.arange(offset + a, offset + a + c.numel(), device=c.device, dtype=torch.int64) % 1000003) + 1
+        s0 += int(c.sum())
+        s1 += int((c * w).sum())
+    return [s0, s1]
 
 
 @pytest.mark.timeout(900)
@@ -172,16 +218,26 @@ def test_c5_32b_shapes_fsdp_grads_snapshot_and_memory_plan(tmp_path):
     from test_weight_update_cpu import free_port
 
     mp.spawn(_run, args=(free_port(), str(tmp_path)), nprocs=2, join=True)
-    r0 = json.loads((tmp_path / "rank0.json").read_text())
-    r1 = json.loads((tmp_path / "rank1.json").read_text())
-    errs = r0["grad_rel_err"]
+    r = [json.loads((tmp_path / f"rank{i}.json").read_text()) for i in range(2)]
+    # gradients: per tensor, summed over the two ranks' shards
+    errs, numel = {}, {}
+    for name in r[0]["grad_part"]:
+        gr, rr, dd, n = (sum(x["grad_part"][name][k] for x in r) for k in range(4))
+        errs[name] = math.sqrt(dd / rr) if rr > 0 else math.sqrt(dd)
+        numel[name] = n
     worst = sorted(errs.items(), key=lambda kv: -kv[1])[:5]
-    mem = {r: (d["peak_bytes"] / 1e9, d["estimate_bytes"] / 1e9) for r, d in (("rank0", r0), ("rank1", r1))}
+    # weight update: the actor's copy of every tensor == the trainer's (digests of the shards summed)
+    want = {n: [r[0]["param_digest_part"][n][k] + r[1]["param_digest_part"][n][k] for k in range(2)]
+            for n in r[0]["param_digest_part"]}
+    equal = {t: sum(int(d[n] == want[n]) for n in want) for t, d in r[1]["actor_digest"].items()}
+    mem = {f"rank{i}": (x["peak_bytes"] / 1e9, x["estimate_bytes"] / 1e9) for i, x in enumerate(r)}
     print(json.dumps({"worst_grad_rel_err": worst, "tensors": len(errs), "peak_vs_estimate_gb": mem,
-                      "plan": r1["plan"], "weight_update": r1["weight_update"]}))
+                      "plan": r[1]["plan"], "actor_tensors_equal": equal}))
     assert len(errs) == 3 + LAYERS * 12, len(errs)  # embed, norm, lm_head + 12 per decoder layer
+    assert numel["lm_head.weight"] == 152064 * 5120 and numel["model.layers.0.mlp.gate_proj.weight"] == 27648 * 5120
     assert worst[0][1] <= GRAD_REL, worst
-    for transport, c in r1["weight_update"].items():
-        assert c["equal"] == c["tensors"] == len(errs), (transport, c)
-    for r, (peak, est) in mem.items():
-        assert peak <= est <= 1.3 * peak, (r, peak, est, r1["plan"])
+    assert set(equal) == {"per_tensor", "bucketed"}
+    for transport, n in equal.items():
+        assert n == len(want), (transport, n, len(want))
+    for who, (peak, est) in mem.items():
+        assert peak <= est <= 1.3 * peak, (who, peak, est, r[1]["plan"])
