@@ -313,24 +313,24 @@ def _snapshot_only_group():
     return SnapshotOnlyGroup()
 
 
-def snapshot_overlap(ts: "TrainerStep", t_ref: float, steps: int, warmup: int, flatten_iters: int = 3) -> dict:
+def snapshot_overlap(ts: "TrainerStep", t_ref: float, steps: int, warmup: int, flatten_iters: int = 3,
+                     rounds: int = 2) -> dict:
     """The trainer-side half of "weight broadcast fully overlapped" (north_star), on this rank's GPU.
 
-    The same optimizer step as ``t_ref`` (seconds per step, measured just before on ``ts``), now with
-    WeightUpdateManager (weight_update.py) snapshotting every parameter into its bf16 staging buffer
-    on its side stream after each optimizer step (rank 0, as in the trainer loop; no receiver: the
-    broadcasts are no-ops), against the snapshot alone (the same prl_flatten_bf16 pass on the side
-    stream, HIP events, nothing else running).  ``exposed_ms`` = step time with the snapshot in
-    flight − step time without it (≥ 0; ``step_delta_ms`` keeps the sign, i.e. the run-to-run noise);
-    ``hidden_frac`` = 1 − exposed / snapshot.  The reference blocks the trainer for the whole
-    update instead (finetune_loop.py:174-215)."""
+    First the snapshot alone: WeightUpdateManager's prl_flatten_bf16 pass over every parameter into
+    its bf16 staging buffer, on a side stream, HIP events, nothing else running (``snapshot_ms``).
+    Then the same optimizer step as ``t_ref`` (seconds per step, measured just before on ``ts``) with
+    and without WeightUpdateManager (weight_update.py) snapshotting after each optimizer step (rank 0,
+    as in the trainer loop; no receiver: the broadcasts are no-ops), ``rounds`` alternated rounds of
+    ``steps`` steps per arm (the step-to-step noise of a ~1.4 s step is a few ms, the snapshot's
+    whole cost ~6 ms).  ``exposed_ms`` = mean step time with the snapshot in flight − without (≥ 0;
+    ``step_delta_ms`` keeps the sign); ``hidden_frac`` = 1 − exposed / snapshot.  The reference
+    blocks the trainer for the whole update instead (finetune_loop.py:174-215)."""
     from .weight_update import FlatLayout, HipFlatPacker, WeightUpdateManager, parameters_info
 
     rank = dist.get_rank() if dist.is_initialized() else 0
     wum = WeightUpdateManager([], ts.model, None, _snapshot_only_group(), transport="bucketed", overlap=True,
                               is_main=rank == 0, write_message=lambda s, m: None)
-    t_snap = ts.timed(steps, warmup, wum=wum)
-    wum.close()
     named = wum.named_parameters()
     layout = FlatLayout.from_infos(parameters_info(named))
     flat = wum._ensure_staging(layout.total, ts.device)
@@ -348,15 +348,23 @@ def snapshot_overlap(ts: "TrainerStep", t_ref: float, steps: int, warmup: int, f
     _sync(ts.device)
     snap_ms = sum(a.elapsed_time(b) for a, b in evs[1:]) / flatten_iters
     nbytes = sum(p.numel() * p.element_size() for p in params) + 2 * sum(p.numel() for p in params)
+    plain, snap = [t_ref], []
+    for r in range(rounds):
+        snap.append(ts.timed(steps, warmup if r == 0 else 0, wum=wum))
+        if r < rounds - 1:
+            plain.append(ts.timed(steps, 0))
+    wum.close()
     wum._staging = None
-    delta_ms = (t_snap - t_ref) * 1e3
+    t_plain, t_snap = sum(plain) / len(plain), sum(snap) / len(snap)
+    delta_ms = (t_snap - t_plain) * 1e3
     exposed = max(0.0, delta_ms)
     return {"params": len(params), "snapshot_bytes": 2 * layout.total, "snapshot_ms": round(snap_ms, 3),
             "snapshot_GBps": round(nbytes / (snap_ms * 1e-3) / 1e9, 1),
-            "ms_per_step_no_snapshot": round(t_ref * 1e3, 2), "ms_per_step_with_snapshot": round(t_snap * 1e3, 2),
+            "ms_per_step_no_snapshot": round(t_plain * 1e3, 2), "ms_per_step_with_snapshot": round(t_snap * 1e3, 2),
+            "arms_ms": {"no_snapshot": [round(x * 1e3, 2) for x in plain], "with_snapshot": [round(x * 1e3, 2) for x in snap]},
             "step_delta_ms": round(delta_ms, 3), "exposed_ms": round(exposed, 3),
             "hidden_frac": round(1.0 - min(1.0, exposed / snap_ms), 4) if snap_ms > 0 else None,
-            "steps": steps, "warmup": warmup}
+            "steps_per_arm": steps, "rounds": rounds}
 
 
 def dp_step_probe(config: str = "c3", micro_batches: int = 4, steps: int = 2, warmup: int = 1, device=None,
