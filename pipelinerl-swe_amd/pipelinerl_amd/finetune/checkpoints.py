@@ -118,6 +118,10 @@ def save_model_and_tokenizer(output_dir: Path, model, tokenizer, *, safe_seriali
     with temporary_folder_and_move(output_dir, group) as tmp:
         if _rank() == 0:
             m = getattr(model, "module", model)
+            if sd is None and getattr(getattr(m, "pretrained_model", m), "_prl_flat_params", False):
+                # parameters re-homed into one buffer for in-place weight broadcasts
+                # (weight_update.py): save host copies, which share no storage
+                sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
             if sd is not None:
                 if getattr(getattr(m, "config", None), "tie_word_embeddings", False):
                     sd.pop("lm_head.weight", None)  # tied copy (finetune_loop.py:228-231)

@@ -252,7 +252,8 @@ def run_finetuning_loop(cfg, step_fn: Callable = rl_step, model=None, tokenizer=
                       bucket_bytes=int(args.get("weight_bucket_mb", 256)) << 20,
                       overlap=bool(args.get("overlap_weight_updates", True)), is_main=ctx.is_main,
                       timeout_s=args.get("weight_update_timeout_s", 900.0),
-                      http_timeout_s=args.get("weight_update_http_timeout_s", 600.0))
+                      http_timeout_s=args.get("weight_update_http_timeout_s", 600.0),
+                      snapshot=args.get("weight_snapshot", "zero_copy"))
         wum.send_weight_update(metrics.samples)
 
     batch_queue: Queue = Queue(maxsize=1)

@@ -317,23 +317,25 @@ def snapshot_overlap(ts: "TrainerStep", t_ref: float, steps: int, warmup: int, f
                      rounds: int = 2) -> dict:
     """The trainer-side half of "weight broadcast fully overlapped" (north_star), on this rank's GPU.
 
-    First the snapshot alone: WeightUpdateManager's prl_flatten_bf16 pass over every parameter into
-    its bf16 staging buffer, on a side stream, HIP events, nothing else running (``snapshot_ms``).
-    Then the same optimizer step as ``t_ref`` (seconds per step, measured just before on ``ts``) with
-    and without WeightUpdateManager (weight_update.py) snapshotting after each optimizer step (rank 0,
-    as in the trainer loop; no receiver: the broadcasts are no-ops), ``rounds`` alternated rounds of
-    ``steps`` steps per arm (the step-to-step noise of a ~1.4 s step is a few ms, the snapshot's
-    whole cost ~6 ms).  ``exposed_ms`` = mean step time with the snapshot in flight − without (≥ 0;
-    ``step_delta_ms`` keeps the sign); ``hidden_frac`` = 1 − exposed / snapshot.  The reference
-    blocks the trainer for the whole update instead (finetune_loop.py:174-215)."""
+    First the staging copy alone: prl_flatten_bf16 over every parameter into a bf16 buffer on a side
+    stream, HIP events, nothing else running (``snapshot_ms``).  Then the same optimizer step as
+    ``t_ref`` (seconds per step, measured just before on ``ts``) in three arms, ``rounds`` alternated
+    rounds of ``steps`` steps each: no weight update; WeightUpdateManager (weight_update.py, rank 0)
+    with ``snapshot="copy"`` (the staging copy on its side stream after each optimizer step); and with
+    ``snapshot="zero_copy"`` (the default: parameters re-homed once into the broadcast layout, read in
+    place).  No receiver: the broadcasts are no-ops, so the arms price the trainer-side snapshot alone
+    (the broadcast's own cost needs actors: ``split_pipeline`` at N > 1).  ``exposed_ms`` = mean step
+    time of an arm − the no-update arm's; ``hidden_frac`` = 1 − exposed / snapshot_ms.  The
+    reference blocks the trainer for the whole update instead (finetune_loop.py:174-215)."""
     from .weight_update import FlatLayout, HipFlatPacker, WeightUpdateManager, parameters_info
 
     rank = dist.get_rank() if dist.is_initialized() else 0
-    wum = WeightUpdateManager([], ts.model, None, _snapshot_only_group(), transport="bucketed", overlap=True,
-                              is_main=rank == 0, write_message=lambda s, m: None)
-    named = wum.named_parameters()
+    mk = lambda mode: WeightUpdateManager([], ts.model, None, _snapshot_only_group(), transport="bucketed",  # noqa: E731
+                                          overlap=True, is_main=rank == 0, write_message=lambda s, m: None,
+                                          snapshot=mode)
+    named = list(ts.model.named_parameters())
     layout = FlatLayout.from_infos(parameters_info(named))
-    flat = wum._ensure_staging(layout.total, ts.device)
+    flat = torch.empty(layout.total, dtype=torch.bfloat16, device=ts.device)
     params = [p.detach() for _, p in named]
     side = torch.cuda.Stream(device=ts.device)
     side.wait_stream(torch.cuda.current_stream(ts.device))
@@ -347,23 +349,34 @@ def snapshot_overlap(ts: "TrainerStep", t_ref: float, steps: int, warmup: int, f
             evs.append((e0, e1))
     _sync(ts.device)
     snap_ms = sum(a.elapsed_time(b) for a, b in evs[1:]) / flatten_iters
-    nbytes = sum(p.numel() * p.element_size() for p in params) + 2 * sum(p.numel() for p in params)
-    plain, snap = [t_ref], []
+    del flat, params
+    nbytes = sum(p.numel() * p.element_size() for _, p in named) + 2 * sum(p.numel() for _, p in named)
+    arms = {"no_update": [t_ref], "copy": [], "zero_copy": []}
+    managers = {"copy": mk("copy"), "zero_copy": mk("zero_copy")}
     for r in range(rounds):
-        snap.append(ts.timed(steps, warmup if r == 0 else 0, wum=wum))
+        for mode in ("copy", "zero_copy"):
+            arms[mode].append(ts.timed(steps, warmup if r == 0 else 0, wum=managers[mode]))
+            managers[mode].wait()
         if r < rounds - 1:
-            plain.append(ts.timed(steps, 0))
-    wum.close()
-    wum._staging = None
-    t_plain, t_snap = sum(plain) / len(plain), sum(snap) / len(snap)
-    delta_ms = (t_snap - t_plain) * 1e3
-    exposed = max(0.0, delta_ms)
-    return {"params": len(params), "snapshot_bytes": 2 * layout.total, "snapshot_ms": round(snap_ms, 3),
+            arms["no_update"].append(ts.timed(steps, 0))
+    in_place = managers["zero_copy"]._flat_params is not None
+    for m in managers.values():
+        m.close()
+        m._staging = None
+    mean = {k: sum(v) / len(v) for k, v in arms.items()}
+
+    def arm(mode: str, cost_ms: float) -> dict:
+        delta = (mean[mode] - mean["no_update"]) * 1e3
+        exposed = max(0.0, delta)
+        return {"ms_per_step": round(mean[mode] * 1e3, 2), "step_delta_ms": round(delta, 3),
+                "exposed_ms": round(exposed, 3),
+                "hidden_frac": round(1.0 - min(1.0, exposed / cost_ms), 4) if cost_ms > 0 else None}
+
+    return {"params": len(named), "snapshot_bytes": 2 * layout.total, "snapshot_ms": round(snap_ms, 3),
             "snapshot_GBps": round(nbytes / (snap_ms * 1e-3) / 1e9, 1),
-            "ms_per_step_no_snapshot": round(t_plain * 1e3, 2), "ms_per_step_with_snapshot": round(t_snap * 1e3, 2),
-            "arms_ms": {"no_snapshot": [round(x * 1e3, 2) for x in plain], "with_snapshot": [round(x * 1e3, 2) for x in snap]},
-            "step_delta_ms": round(delta_ms, 3), "exposed_ms": round(exposed, 3),
-            "hidden_frac": round(1.0 - min(1.0, exposed / snap_ms), 4) if snap_ms > 0 else None,
+            "ms_per_step_no_update": round(mean["no_update"] * 1e3, 2),
+            "copy": arm("copy", snap_ms), "zero_copy": dict(arm("zero_copy", snap_ms), in_place=in_place),
+            "arms_ms": {k: [round(x * 1e3, 2) for x in v] for k, v in arms.items()},
             "steps_per_arm": steps, "rounds": rounds}
 
 

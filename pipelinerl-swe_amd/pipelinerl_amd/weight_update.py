@@ -11,11 +11,17 @@ Protocol (unchanged, so unmodified reference actors keep working):
 ``version`` is the cumulative number of samples trained (finetune_loop.py:795-801).
 
 What changes:
-  * snapshot: all parameters are packed into ONE bf16 staging buffer by the HIP flatten
-    kernel (prl_flatten_bf16) on a side stream, ordered after the optimizer step by an
-    event; the broadcast then reads the snapshot, so the trainer's next passes (and the next
-    optimizer step) run concurrently on the main stream — the broadcast is overlapped,
-    not blocking (the reference idles the trainer for the whole transfer);
+  * snapshot (``snapshot="zero_copy"``, the default for a bf16 model on one HIP device): at the
+    first update every parameter is re-homed into ONE flat bf16 buffer in the broadcast layout
+    (``p.data`` becomes a view; a one-time copy), so the broadcast reads the parameters in place:
+    no per-update copy at all.  The next optimizer step waits (device-side) until the broadcast has
+    read them — one step later, long after it finished.  ``snapshot="copy"`` (and any non-bf16 or
+    multi-device model): every parameter is packed into a bf16 staging buffer by the HIP flatten
+    kernel (prl_flatten_bf16) on a side stream after the optimizer step; measured on MI355X, that
+    5.6 ms copy of 7B's 15.23 GB costs the next step about its own duration (it competes for the
+    CUs: ``snapshot_overlap`` in the bench line).  Either way the broadcast runs on a side stream
+    while the trainer's next passes run on the main stream — overlapped, not blocking (the
+    reference idles the trainer for the whole transfer);
   * transport "per_tensor" (compat: one broadcast per parameter, views into the snapshot)
     or "bucketed" (our actors only: ~256 MiB broadcasts of the flat snapshot, 1 call per
     bucket instead of 339 for 7B).  Layout: parameter i starts at an 8-element (16 B)
@@ -185,12 +191,18 @@ class WeightUpdateManager:
                  transport: str = "per_tensor", bucket_bytes: int = 256 << 20, overlap: bool = True,
                  packer=None, post: Callable[[str, BaseModel], None] | None = None, is_main: bool = True,
                  write_message: Callable[[Any, BaseModel], None] | None = None, timeout_s: float | None = 900.0,
-                 http_timeout_s: float | None = 600.0):
+                 http_timeout_s: float | None = 600.0, snapshot: str = "zero_copy"):
         """``timeout_s``: an update (every actor's HTTP answer and the whole broadcast) that has not
         completed this long after its request raises WeightUpdateError from the next ``wait()`` /
         ``send_weight_update()``; so does any actor's HTTP error, as soon as it arrives.  A failed
         update aborts an RcclComm actor group (in-flight broadcasts return) — the trainer exits
         instead of hanging in the collective (failure handling)."""
+        if snapshot not in ("zero_copy", "copy"):
+            raise ValueError(f"snapshot must be 'zero_copy' or 'copy', got {snapshot!r}")
+        self.snapshot = snapshot
+        self._flat_params: torch.Tensor | None = None
+        self._read_done = None  # zero-copy: event after the last broadcast read of the parameters
+        self._works: list = []
         self.llm_urls = list(llm_urls)
         self.model = accelerated_model
         self.update_stream = update_stream
@@ -223,6 +235,37 @@ class WeightUpdateManager:
 
         with write_to_streams(self.update_stream) as w:
             w.write(msg)
+
+    def _zero_copy_flat(self, named, layout: FlatLayout) -> torch.Tensor | None:
+        """The flat buffer the parameters live in (re-homed on first use), or None when the model
+        cannot be broadcast in place (snapshot="copy", a non-bf16 or non-HIP parameter, or several
+        devices): then the staging copy is used."""
+        if self.snapshot != "zero_copy" or not named:
+            return None
+        params = [p for _, p in named]
+        dev = params[0].device
+        if any(p.dtype != torch.bfloat16 or p.device != dev or p.device.type != "cuda" or not p.is_contiguous()
+               for p in params):
+            return None
+        flat = self._flat_params
+        if flat is not None and flat.numel() == layout.total and all(
+                p.data_ptr() == flat.data_ptr() + 2 * off for p, off in zip(params, layout.offsets)):
+            return flat
+        from .finetune.model_ops import weights_written
+
+        flat = torch.zeros(layout.total, dtype=torch.bfloat16, device=dev)  # padding gaps stay 0
+        with torch.no_grad():
+            for p, off in zip(params, layout.offsets):
+                view = flat[off:off + p.numel()].view(p.shape)
+                view.copy_(p.data)
+                p.data = view  # the same Parameter (optimizer state, hooks, ties), storage in the buffer
+        weights_written()
+        torch.cuda.current_stream(dev).synchronize()  # the old storages are released after the copies
+        self._flat_params = flat
+        unwrap_model(self.model)._prl_flat_params = True  # checkpoints save copies (shared storage)
+        logger.info(f"weight updates broadcast the parameters in place: {len(params)} tensors re-homed into one "
+                    f"{2 * layout.total / 1e9:.2f} GB buffer")
+        return flat
 
     def _ensure_staging(self, total: int, device: torch.device) -> torch.Tensor:
         if self._staging is None or self._staging.numel() < total or self._staging.device != device:
@@ -263,7 +306,10 @@ class WeightUpdateManager:
         futures = [self.pool.submit(self.post, url, request) for url in self.llm_urls]
         logger.info(f"Published weight update request for version {version}")
         params = [p.detach() for _, p in named]
-        if not sharded:
+        in_place = None if sharded else self._zero_copy_flat(named, layout)
+        if in_place is not None:
+            flat = in_place
+        elif not sharded:
             flat = self._ensure_staging(layout.total, dev)
         on_gpu = dev.type == "cuda"
         if on_gpu:
@@ -278,9 +324,9 @@ class WeightUpdateManager:
         with ctx:
             if on_gpu:
                 self._stream.wait_event(ready)  # snapshot after the optimizer step
-            if not sharded:
+            if not sharded and in_place is None:
                 self.packer.flatten(params, layout.offsets, flat)
-            if on_gpu:
+            if on_gpu and in_place is None:
                 self._snapshot_done = torch.cuda.Event()
                 self._snapshot_done.record(self._stream)
             if self.transport == "bucketed":
@@ -297,6 +343,9 @@ class WeightUpdateManager:
                     w.wait()
                 done = torch.cuda.Event()
                 done.record(self._stream)
+            if in_place is not None:  # the parameters are read until the broadcast ends
+                self._snapshot_done = done
+                self._works = works
 
         def finish():
             try:
@@ -341,11 +390,17 @@ class WeightUpdateManager:
             self._raise()
 
     def before_optimizer_step(self) -> None:
-        """Order the next in-place parameter update after the snapshot copy (device-side wait)."""
+        """Order the next in-place parameter update after the snapshot: after the staging copy, or
+        (zero-copy) after the broadcast's last read of the parameters — a device-side wait on an
+        RCCL / stream-ordered group; a host wait for a gloo group's works (tests, rehearsals)."""
         ev = getattr(self, "_snapshot_done", None)
         if ev is not None:
             torch.cuda.current_stream().wait_event(ev)
             self._snapshot_done = None
+        works, self._works = self._works, []
+        if works and not isinstance(self.group, comm.RcclComm) and "nccl" not in str(_backend_of(self.group)):
+            for w in works:
+                w.wait()
 
     def wait(self) -> None:
         """Block until the in-flight update (if any) has been received by every actor."""
@@ -369,6 +424,13 @@ class WeightUpdateManager:
     def close(self) -> None:
         self.wait()
         self.pool.shutdown(wait=True)
+
+
+def _backend_of(group) -> str:
+    try:
+        return dist.get_backend(group)
+    except Exception:  # noqa: BLE001 - not a torch process group
+        return ""
 
 
 def _is_sharded(named) -> bool:

@@ -65,3 +65,65 @@ def _offsets(model):
 
     infos = [ParameterInfo(name=n, shape=list(p.shape), dtype=str(torch.bfloat16)) for n, p in model.named_parameters()]
     return FlatLayout.from_infos(infos).offsets
+
+
+def test_zero_copy_snapshot_broadcasts_the_parameters_in_place(tmp_path):
+    """snapshot="zero_copy" (the default): a bf16 model's parameters are re-homed once into one
+    buffer in the broadcast layout (the same Parameter objects, values bit-identical, a tied weight
+    kept tied), every later update reads them in place (no re-home, no staging buffer), the next
+    optimizer step is ordered after the broadcast's reads, and a checkpoint of the re-homed model
+    saves and loads back exactly (safetensors refuses shared storage: host copies are saved)."""
+    from transformers import AutoConfig, AutoModelForCausalLM
+
+    from loop_helpers import tiny_model_dir
+    from pipelinerl_amd.finetune.checkpoints import save_model_and_tokenizer
+    from pipelinerl_amd.finetune.optim import PrlAdamW
+    from pipelinerl_amd.weight_update import WeightUpdateManager
+
+    c = _comm()
+    try:
+        cfg = AutoConfig.from_pretrained(tiny_model_dir(tmp_path))
+        torch.manual_seed(0)
+        model = AutoModelForCausalLM.from_config(cfg, dtype=torch.bfloat16).cuda()
+        tied = model.get_input_embeddings().weight is model.get_output_embeddings().weight
+        before = {n: p.detach().clone() for n, p in model.named_parameters()}
+        ids = {n: id(p) for n, p in model.named_parameters()}
+        mgr = WeightUpdateManager([], model, None, c, transport="bucketed", bucket_bytes=4096, overlap=True,
+                                  write_message=lambda s, m: None)
+        mgr.send_weight_update(1)
+        mgr.wait()
+        flat = mgr._flat_params
+        assert flat is not None and mgr._staging is None
+        offs = _offsets(model)
+        for (n, p), o in zip(model.named_parameters(), offs):
+            assert id(p) == ids[n] and p.data_ptr() == flat.data_ptr() + 2 * o, n
+            assert torch.equal(p.detach(), before[n]), n
+        assert (model.get_input_embeddings().weight is model.get_output_embeddings().weight) == tied
+        # an optimizer step after the update: ordered after the broadcast, parameters stay in place
+        opt = PrlAdamW(model.parameters(), lr=1e-2)
+        for p in model.parameters():
+            p.grad = torch.randn_like(p)
+        mgr.before_optimizer_step()
+        opt.step()
+        mgr.send_weight_update(2)
+        mgr.close()
+        assert mgr._flat_params is flat and mgr.completed_versions == [1, 2]
+        for (n, p), o in zip(model.named_parameters(), offs):
+            assert p.data_ptr() == flat.data_ptr() + 2 * o and not torch.equal(p.detach(), before[n]), n
+        # checkpoint of the re-homed model: saves, and loads back bit for bit
+        out = tmp_path / "current"
+        save_model_and_tokenizer(out, model, object(), safe_serialization=True)
+        back = AutoModelForCausalLM.from_pretrained(out, dtype=torch.bfloat16).cuda()
+        for n, p in back.named_parameters():
+            assert torch.equal(p.detach(), dict(model.named_parameters())[n].detach()), n
+        # snapshot="copy" keeps the parameters where they are
+        m2 = AutoModelForCausalLM.from_config(cfg, dtype=torch.bfloat16).cuda()
+        ptrs = [p.data_ptr() for p in m2.parameters()]
+        mgr2 = WeightUpdateManager([], m2, None, c, transport="bucketed", bucket_bytes=4096, overlap=True,
+                                   write_message=lambda s, m: None, snapshot="copy")
+        mgr2.send_weight_update(1)
+        mgr2.close()
+        assert mgr2._flat_params is None and mgr2._staging is not None
+        assert [p.data_ptr() for p in m2.parameters()] == ptrs
+    finally:
+        c.close()
