@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import time
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -314,18 +315,18 @@ def _snapshot_only_group():
 
 
 def snapshot_overlap(ts: "TrainerStep", t_ref: float, steps: int, warmup: int, flatten_iters: int = 3,
-                     rounds: int = 2) -> dict:
+                     rounds: int = 3) -> dict:
     """The trainer-side half of "weight broadcast fully overlapped" (north_star), on this rank's GPU.
 
     First the staging copy alone: prl_flatten_bf16 over every parameter into a bf16 buffer on a side
     stream, HIP events, nothing else running (``snapshot_ms``).  Then the same optimizer step as
-    ``t_ref`` (seconds per step, measured just before on ``ts``) in three arms, ``rounds`` alternated
-    rounds of ``steps`` steps each: no weight update; WeightUpdateManager (weight_update.py, rank 0)
+    ``t_ref`` (seconds per step, measured just before on ``ts``) in three arms, ``rounds`` rounds of
+    ``steps`` steps each, the arms' order rotating every round (medians reported): no weight update; WeightUpdateManager (weight_update.py, rank 0)
     with ``snapshot="copy"`` (the staging copy on its side stream after each optimizer step); and with
     ``snapshot="zero_copy"`` (the default: parameters re-homed once into the broadcast layout, read in
     place).  No receiver: the broadcasts are no-ops, so the arms price the trainer-side snapshot alone
-    (the broadcast's own cost needs actors: ``split_pipeline`` at N > 1).  ``exposed_ms`` = mean step
-    time of an arm − the no-update arm's; ``hidden_frac`` = 1 − exposed / snapshot_ms.  The
+    (the broadcast's own cost needs actors: ``split_pipeline`` at N > 1).  ``exposed_ms`` = median step
+    time of an arm − the no-update arm's (the no-update arm's own spread is the noise floor); ``hidden_frac`` = 1 − exposed / snapshot_ms.  The
     reference blocks the trainer for the whole update instead (finetune_loop.py:174-215)."""
     from .weight_update import FlatLayout, HipFlatPacker, WeightUpdateManager, parameters_info
 
@@ -352,30 +353,38 @@ def snapshot_overlap(ts: "TrainerStep", t_ref: float, steps: int, warmup: int, f
     del flat, params
     nbytes = sum(p.numel() * p.element_size() for _, p in named) + 2 * sum(p.numel() for _, p in named)
     arms = {"no_update": [t_ref], "copy": [], "zero_copy": []}
-    managers = {"copy": mk("copy"), "zero_copy": mk("zero_copy")}
-    for r in range(rounds):
-        for mode in ("copy", "zero_copy"):
-            arms[mode].append(ts.timed(steps, warmup if r == 0 else 0, wum=managers[mode]))
-            managers[mode].wait()
-        if r < rounds - 1:
-            arms["no_update"].append(ts.timed(steps, 0))
+    managers = {"no_update": None, "copy": mk("copy"), "zero_copy": mk("zero_copy")}
+    order = ["no_update", "copy", "zero_copy"]
+    for r in range(rounds):  # the order rotates every round, so a drift of the clocks hits every arm
+        for mode in order[r % 3:] + order[:r % 3]:
+            first = r == 0 and mode != "no_update"
+            arms[mode].append(ts.timed(steps, warmup if first else 0, wum=managers[mode]))
+            if managers[mode] is not None:
+                managers[mode].wait()
     in_place = managers["zero_copy"]._flat_params is not None
     for m in managers.values():
-        m.close()
-        m._staging = None
-    mean = {k: sum(v) / len(v) for k, v in arms.items()}
+        if m is not None:
+            m.close()
+            m._staging = None
+    mean = {k: float(np.median(v)) for k, v in arms.items()}
+
+    spread = (max(arms["no_update"]) - min(arms["no_update"])) * 1e3
 
     def arm(mode: str, cost_ms: float) -> dict:
         delta = (mean[mode] - mean["no_update"]) * 1e3
         exposed = max(0.0, delta)
         return {"ms_per_step": round(mean[mode] * 1e3, 2), "step_delta_ms": round(delta, 3),
-                "exposed_ms": round(exposed, 3),
-                "hidden_frac": round(1.0 - min(1.0, exposed / cost_ms), 4) if cost_ms > 0 else None}
+                "exposed_ms": round(exposed, 3), "within_noise": abs(delta) <= spread, "device_work_ms": cost_ms,
+                "hidden_frac": (round(1.0 - min(1.0, exposed / cost_ms), 4) if cost_ms > 0 else 1.0)}
 
     return {"params": len(named), "snapshot_bytes": 2 * layout.total, "snapshot_ms": round(snap_ms, 3),
             "snapshot_GBps": round(nbytes / (snap_ms * 1e-3) / 1e9, 1),
             "ms_per_step_no_update": round(mean["no_update"] * 1e3, 2),
-            "copy": arm("copy", snap_ms), "zero_copy": dict(arm("zero_copy", snap_ms), in_place=in_place),
+            "no_update_spread_ms": round(spread, 3),
+            "copy": arm("copy", round(snap_ms, 3)),
+            # in place there is no per-update device work on the trainer: hidden_frac 1 by construction,
+            # step_delta_ms is the run's noise (compare no_update_spread_ms)
+            "zero_copy": dict(arm("zero_copy", 0.0 if in_place else round(snap_ms, 3)), in_place=in_place),
             "arms_ms": {k: [round(x * 1e3, 2) for x in v] for k, v in arms.items()},
             "steps_per_arm": steps, "rounds": rounds}
 
