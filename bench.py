@@ -402,12 +402,13 @@ def main():
     c3 = None
     if not args.no_c3:
         # configs[2] (C3): Qwen2.5-7B DP trainer step on C3's packed math rollouts, with the full
-        # bucketed 15.23 GB gradient all-reduce at N > 1 (local / DP / all-reduce-alone timings),
-        # then the same step with the weight-update snapshot in flight on its side stream
+        # bucketed 15.23 GB gradient all-reduce at N > 1 (local / DP / all-reduce-alone timings);
+        # at N = 1 also the same step with the weight-update snapshot (staging copy / in place) in
+        # flight (at N > 1 the split_pipeline probe prices the whole broadcast with real actors)
         from pipelinerl_amd.trainer_probe import dp_step_probe
 
         c3 = optional("c3_dp", lambda: dp_step_probe("c3", micro_batches=4, steps=2, warmup=1, device=dev,
-                                                      layers=4 if rehearse else None, snapshot=True))
+                                                      layers=4 if rehearse else None, snapshot=world == 1))
     trainer = None
     if not args.no_trainer_step:
         # the whole optimizer step the loss head sits in
