@@ -37,6 +37,14 @@ trainers run the next step.  The trainers' step time with and without the broadc
 gives hidden_frac (1.0 = the broadcast latency is fully overlapped).  At N >= 4, "fsdp_32b":
 BASELINE.json configs[4] (C5), Qwen2.5-32B shapes sharded with FSDP2 over all ranks, KL on.
 
+At N = 1, "snapshot_overlap" prices the trainer-side half of "weight broadcast fully overlapped":
+C3's 7B step with no weight update, with WeightUpdateManager's staging copy in flight after each
+optimizer step, and with the in-place (zero-copy, default) snapshot, in rotating rounds, beside the
+copy's own duration.  At N > 1, "communicators" first checks that every communicator reports (and
+carries, by an all-reduce of ones) the intended rank count: the DP group, the CPU control group and a
+prl_comm RCCL communicator (ncclCommCount); the split pipeline's DP and actor groups are checked in
+its own probe ("split_pipeline.groups").
+
 Prints ONE JSON line (rank 0).  roofline.achieved = algorithmic bytes per launch
 (T*V*2 read + T*V*2 dlogits write + 37*T side data) / the average duration
 of the prl_grpo_forward launch measured with HIP events on its stream.
