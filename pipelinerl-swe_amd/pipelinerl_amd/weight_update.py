@@ -192,7 +192,10 @@ class WeightUpdateManager:
                  packer=None, post: Callable[[str, BaseModel], None] | None = None, is_main: bool = True,
                  write_message: Callable[[Any, BaseModel], None] | None = None, timeout_s: float | None = 900.0,
                  http_timeout_s: float | None = 600.0, snapshot: str = "zero_copy"):
-        """``timeout_s``: an update (every actor's HTTP answer and the whole broadcast) that has not
+        """``snapshot``: "zero_copy" (the parameters are broadcast in place: call
+        ``before_optimizer_step()`` before writing them — the trainer loop does, before every
+        optimizer step) or "copy" (a staging copy per update; the parameters may be written at once).
+        ``timeout_s``: an update (every actor's HTTP answer and the whole broadcast) that has not
         completed this long after its request raises WeightUpdateError from the next ``wait()`` /
         ``send_weight_update()``; so does any actor's HTTP error, as soon as it arrives.  A failed
         update aborts an RcclComm actor group (in-flight broadcasts return) — the trainer exits
@@ -238,14 +241,13 @@ class WeightUpdateManager:
 
     def _zero_copy_flat(self, named, layout: FlatLayout) -> torch.Tensor | None:
         """The flat buffer the parameters live in (re-homed on first use), or None when the model
-        cannot be broadcast in place (snapshot="copy", a non-bf16 or non-HIP parameter, or several
-        devices): then the staging copy is used."""
+        cannot be broadcast in place (snapshot="copy", a non-bf16 or non-contiguous parameter, or
+        several devices): then the staging copy is used."""
         if self.snapshot != "zero_copy" or not named:
             return None
         params = [p for _, p in named]
         dev = params[0].device
-        if any(p.dtype != torch.bfloat16 or p.device != dev or p.device.type != "cuda" or not p.is_contiguous()
-               for p in params):
+        if any(p.dtype != torch.bfloat16 or p.device != dev or not p.is_contiguous() for p in params):
             return None
         flat = self._flat_params
         if flat is not None and flat.numel() == layout.total and all(
@@ -260,7 +262,8 @@ class WeightUpdateManager:
                 view.copy_(p.data)
                 p.data = view  # the same Parameter (optimizer state, hooks, ties), storage in the buffer
         weights_written()
-        torch.cuda.current_stream(dev).synchronize()  # the old storages are released after the copies
+        if dev.type == "cuda":
+            torch.cuda.current_stream(dev).synchronize()  # the old storages are released after the copies
         self._flat_params = flat
         unwrap_model(self.model)._prl_flat_params = True  # checkpoints save copies (shared storage)
         logger.info(f"weight updates broadcast the parameters in place: {len(params)} tensors re-homed into one "

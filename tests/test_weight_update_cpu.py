@@ -68,11 +68,16 @@ def _trainer(port, world, transport, exp, versions, use_reference_pg, qwen=False
     mgr = WeightUpdateManager([], model, stream, pg, transport=transport, bucket_bytes=1000, overlap=True,
                               packer=TorchFlatPacker())
     for v in versions:
+        mgr.before_optimizer_step()  # the parameters are written below: after the previous broadcast read them
         with torch.no_grad():
             for p in model.parameters():
                 p.add_(0.125 * (v + 1))
         mgr.send_weight_update(v)  # returns immediately (overlapped)
     mgr.close()
+    # the bf16 model is broadcast in place (snapshot="zero_copy"): its parameters live in one buffer
+    flat = mgr._flat_params
+    assert flat is not None and mgr._staging is None
+    assert all(flat.data_ptr() <= p.data_ptr() < flat.data_ptr() + 2 * flat.numel() for p in model.parameters())
     torch.save({n: p.detach().clone() for n, p in model.named_parameters()}, Path(exp) / "trainer_params.pt")
 
 
