@@ -15,7 +15,8 @@ What the components' own tests do not cover, checked here in one run:
     both transports.  (The staging-copy snapshot runs the HIP flatten kernel: on the GPU in
     tests/test_split_pipeline_gpu.py and tests/test_comm_gpu.py, with a torch packer in
     tests/test_weight_update_cpu.py.)
-The loss is the CPU torch restatement of rl_step (tests/cpu_rl_step.py): the HIP loss head needs a GPU.
+The loss is the CPU torch restatement of rl_step (tests/cpu_rl_step.py) here; tests/test_pipeline_e2e_gpu.py
+runs the same pipeline with the product's rl_step and the actor on the GPU.
 """
 
 from __future__ import annotations
@@ -36,13 +37,14 @@ ROOT = Path(__file__).resolve().parents[1]
 PKG = ROOT / "pipelinerl-swe_amd"
 
 
-def _trainer(rank, exp, actor_url, group_port, transport, snapshot):
+def _trainer(rank, exp, actor_url, group_port, transport, snapshot, device="cpu"):
     sys.path[:0] = [str(ROOT), str(ROOT / "tests"), str(PKG)]
     os.environ.update(OMP_NUM_THREADS="1")
     for k in ("RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
         os.environ.pop(k, None)
     from cpu_rl_step import cpu_rl_step
     from loop_helpers import loop_cfg
+    from pipelinerl_amd.finetune.rl import rl_step
     from pipelinerl_amd.finetune_loop import run_finetuning_loop
     from pipelinerl_amd.streams import reset_streams_backend
 
@@ -57,17 +59,32 @@ def _trainer(rank, exp, actor_url, group_port, transport, snapshot):
     cfg.me.llm_urls = actor_url
     captured = {}
 
-    def step(model, batch, cur, mx, config):
+    def step(model, batch, cur, mx, config):  # CPU: the torch restatement
         captured["model"] = model
         return cpu_rl_step(model, batch, cur, mx, config)
 
-    m = run_finetuning_loop(cfg, step_fn=step)
+    m = run_finetuning_loop(cfg, step_fn=step if device == "cpu" else _Capture(rl_step, captured))
     sums = {n: float(p.detach().to(torch.bfloat16).double().sum()) for n, p in captured["model"].named_parameters()}
     (exp / "trainer.json").write_text(json.dumps({"steps": m.completed_steps, "samples": m.samples, "sums": sums}))
 
 
+class _Capture:
+    """rl_step itself (so the loop takes its native path: deferred statistics, loss scale), noting the model."""
+
+    def __init__(self, fn, captured):
+        self.fn, self.captured = fn, captured
+
+    def __call__(self, model, *a, **kw):
+        self.captured["model"] = model
+        return self.fn(model, *a, **kw)
+
+
 @pytest.mark.parametrize("transport,snapshot", [("bucketed", "zero_copy"), ("per_tensor", "zero_copy")])
 def test_loop_updates_a_standalone_actor_process(tmp_path, transport, snapshot):
+    run_pipeline(tmp_path, transport, snapshot, "cpu")
+
+
+def run_pipeline(tmp_path, transport, snapshot, device):
     import requests
 
     exp = tmp_path
@@ -76,15 +93,17 @@ def test_loop_updates_a_standalone_actor_process(tmp_path, transport, snapshot):
     actor_port, group_port = free_port(), free_port()
     url = f"http://127.0.0.1:{actor_port}"
     env = dict(os.environ, PYTHONPATH=os.pathsep.join([str(PKG), os.environ.get("PYTHONPATH", "")]),
-               OMP_NUM_THREADS="1", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+               OMP_NUM_THREADS="1")
+    if device == "cpu":
+        env.update(CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
     log = open(exp / "actor.log", "w")
     actor = subprocess.Popen([sys.executable, "-m", "pipelinerl_amd.actor", "--port", str(actor_port),
                               "--actor-llm-idx", "0", "--weight-update-group-init-method",
                               f"tcp://127.0.0.1:{group_port}", "--weight-update-group-world-size", "2",
-                              "--backend", "gloo", "--device", "cpu", "--model-config", str(exp / "tiny_qwen2")],
+                              "--backend", "gloo", "--device", device, "--model-config", str(exp / "tiny_qwen2")],
                              env=env, stdout=log, stderr=subprocess.STDOUT)
     try:
-        mp.spawn(_trainer, args=(str(exp), url, group_port, transport, snapshot), nprocs=1, join=True)
+        mp.spawn(_trainer, args=(str(exp), url, group_port, transport, snapshot, device), nprocs=1, join=True)
         got = requests.get(url + "/checksum", timeout=30).json()
     finally:
         actor.terminate()
@@ -112,3 +131,9 @@ def test_loop_updates_a_standalone_actor_process(tmp_path, transport, snapshot):
         assert i_done < i_succ, (v, i_done, i_succ)
     actor_log = (exp / "actor.log").read_text()
     assert actor_log.count("Weight update received") == 3, actor_log[-2000:]
+    # the final checkpoint of the (re-homed) trainer loads back with the weights the actor holds
+    from transformers import AutoModelForCausalLM
+
+    back = AutoModelForCausalLM.from_pretrained(exp / "finetune" / "current", dtype=torch.bfloat16)
+    for n, p in back.named_parameters():
+        assert float(p.detach().double().sum()) == t["sums"][n], n
