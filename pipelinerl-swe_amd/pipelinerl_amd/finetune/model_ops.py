@@ -250,9 +250,35 @@ def weights_written() -> None:
     _WEIGHT_EPOCH[0] += 1
 
 
+def _adjacent_view(ws) -> torch.Tensor | None:
+    """``ws`` as ONE tensor, without a copy, when they lie back to back in one storage with matching
+    trailing shapes — the case for gate_proj / up_proj once the parameters are re-homed into the
+    weight broadcast's flat layout (weight_update.py, snapshot="zero_copy": consecutive
+    named_parameters, 16-B aligned, and I x H is a multiple of 8) — else None."""
+    w0 = ws[0]
+    try:
+        base = w0.untyped_storage().data_ptr()
+    except Exception:  # noqa: BLE001
+        return None
+    off = w0.storage_offset()
+    for w in ws:
+        if (not w.is_contiguous() or w.dtype != w0.dtype or w.device != w0.device or w.shape[1:] != w0.shape[1:]
+                or w.untyped_storage().data_ptr() != base or w.storage_offset() != off):
+            return None
+        off += w.numel()
+    rows = sum(int(w.shape[0]) for w in ws)
+    return w0.detach().as_strided((rows,) + tuple(w0.shape[1:]), w0.stride(), w0.storage_offset())
+
+
 def _fused_weight(holder, ws, slot: str = "_prl_fused_w") -> torch.Tensor:
-    """cat(ws) cached on the module ``holder`` (so it lives and dies with the model), rebuilt when
-    a member's version counter or storage changes, or when weights_written() was called."""
+    """cat(ws): a view when the members are adjacent in memory (nothing cached: it always reads the
+    current weights), else a copy cached on the module ``holder`` (so it lives and dies with the
+    model), rebuilt when a member's version counter or storage changes, or when weights_written()
+    was called."""
+    view = _adjacent_view(ws)
+    if view is not None:
+        holder.__dict__.pop(slot, None)  # a copy made before the parameters were re-homed
+        return view
     ver = (_WEIGHT_EPOCH[0],) + tuple(w._version for w in ws) + tuple(w.data_ptr() for w in ws)
     hit = holder.__dict__.get(slot)
     if hit is not None and hit[0] == ver:

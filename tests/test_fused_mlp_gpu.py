@@ -215,3 +215,53 @@ def test_fused_gate_up_training_matches_separate(monkeypatch):
     print("fused vs separate MLP update rel:", {k: round(v, 4) for k, v in rels.items()})
     for n, rel in rels.items():
         assert rel < 0.08, (n, rel)
+
+
+def test_fused_gate_up_is_a_view_of_rehomed_weights():
+    """Parameters re-homed into the weight broadcast's flat layout (weight_update.py zero-copy: gate
+    then up, back to back): the fused [2 I, H] weight is a view of them — no concatenation copy, no
+    cache, always the current weights — and a patched Qwen2 MLP's outputs and gradients are
+    bit-identical to the same model before re-homing, also after an in-place weight change."""
+    from transformers import Qwen2Config, Qwen2ForCausalLM
+
+    from pipelinerl_amd.finetune import model_ops
+    from pipelinerl_amd.weight_update import FlatLayout, ParameterInfo
+
+    cfg = Qwen2Config(vocab_size=256, hidden_size=512, intermediate_size=1408, num_hidden_layers=1,
+                      num_attention_heads=4, num_key_value_heads=2, tie_word_embeddings=True)
+    torch.manual_seed(0)
+    a = Qwen2ForCausalLM(cfg).to(DEV, torch.bfloat16)
+    b = Qwen2ForCausalLM(cfg).to(DEV, torch.bfloat16)
+    b.load_state_dict(a.state_dict())
+    model_ops.patch_model(a)
+    model_ops.patch_model(b)
+    named = list(b.named_parameters())
+    layout = FlatLayout.from_infos([ParameterInfo(name=n, shape=list(p.shape), dtype="torch.bfloat16")
+                                    for n, p in named])
+    flat = torch.zeros(layout.total, dtype=torch.bfloat16, device=DEV)
+    with torch.no_grad():  # what WeightUpdateManager's zero-copy snapshot does
+        for (_, p), off in zip(named, layout.offsets):
+            v = flat[off:off + p.numel()].view(p.shape)
+            v.copy_(p.data)
+            p.data = v
+    model_ops.weights_written()
+    mlp_a, mlp_b = a.model.layers[0].mlp, b.model.layers[0].mlp
+    view = model_ops._fused_weight(mlp_b, (mlp_b.gate_proj.weight, mlp_b.up_proj.weight))
+    assert view.data_ptr() == mlp_b.gate_proj.weight.data_ptr() and view.shape == (2 * 1408, 512)
+    assert "_prl_fused_w" not in mlp_b.__dict__
+    g = torch.Generator(device=DEV).manual_seed(1)
+    x = (torch.randn((1, 700, 512), generator=g, device=DEV)).to(torch.bfloat16)
+    for step in range(2):
+        outs = []
+        for m in (mlp_a, mlp_b):
+            xi = x.clone().requires_grad_(True)
+            y = m(xi)
+            y.float().pow(2).mean().backward()
+            outs.append((y.detach(), xi.grad, m.gate_proj.weight.grad.clone(), m.up_proj.weight.grad.clone()))
+            m.zero_grad(set_to_none=True)
+        for u, v in zip(*outs):
+            assert torch.equal(_bits(u), _bits(v)), step
+        with torch.no_grad():  # an in-place update (as the optimizer's): the view sees it, the cache rebuilds
+            for m in (mlp_a, mlp_b):
+                m.gate_proj.weight.mul_(0.5)
+                m.up_proj.weight.add_(0.01)
