@@ -207,6 +207,12 @@ def run_finetuning_loop(cfg, step_fn: Callable = rl_step, model=None, tokenizer=
         tokenizer = load_tokenizer(args.config_name, getattr(getattr(model, "config", None), "eos_token_id", None))
     if sharded:  # before the optimizer: it must see the sharded parameters
         model = shard_model(model, cfg.get("fsdp"), grad_reduce=args.get("grad_reduce", "mean"))
+    elif args.get("flat_parameters", True):
+        # every bf16 parameter into one buffer in the weight broadcast's layout (weight_update.py):
+        # in-place broadcasts, the gate / up projections one tensor without a concatenation copy
+        from .weight_update import rehome_parameters
+
+        rehome_parameters(model)
     data_stream = SingleStreamSpec(exp_path=exp_root, topic=args.input, instance=0, partition=ctx.rank)
     optimizer = get_optimizer(args.optim, model, args.learning_rate, args.weight_decay)
     from transformers import get_scheduler

@@ -106,7 +106,7 @@ class TrainerStep:
                  micro_batches: int = 4, device=None, fused_head: bool = True, grad_ckpt: bool = False,
                  fused_ops: bool = True, group=None, model=None, step_fn=None, vocab: int | None = None,
                  fsdp: bool = False, kl_coef: float = 0.0, layers: int | None = None, batches: list | None = None,
-                 samples_per_step: int | None = None, local: bool = False):
+                 samples_per_step: int | None = None, local: bool = False, flat_params: bool = True):
         """``batches``: the packed micro-batches to train on (host PipelineBatchEncodings, e.g. from
         workloads.micro_batches), ``samples_per_step`` their global sample count (RLConfig.batch_size);
         default: ``micro_batches`` synthetic batches of ``tokens`` tokens.  ``local``: no gradient
@@ -126,6 +126,10 @@ class TrainerStep:
             if group is not None:
                 raise ValueError("fsdp shards over the default process group")
             self.model = shard_model(self.model)
+        elif flat_params:  # as the loop does at load (finetune.flat_parameters, weight_update.py)
+            from .weight_update import rehome_parameters
+
+            rehome_parameters(self.model)
         from .finetune.rl import rl_step
 
         self.native_step = step_fn is None or step_fn is rl_step
@@ -324,7 +328,7 @@ def snapshot_overlap(ts: "TrainerStep", t_ref: float, steps: int, warmup: int, f
     ``steps`` steps each, the arms' order rotating every round (medians reported): no weight update; WeightUpdateManager (weight_update.py, rank 0)
     with ``snapshot="copy"`` (the staging copy on its side stream after each optimizer step); and with
     ``snapshot="zero_copy"`` (the default: parameters re-homed once into the broadcast layout, read in
-    place; re-homed before the first arm, so every arm runs the same step).  No receiver: the broadcasts are no-ops, so the arms price the trainer-side snapshot alone
+    place; re-homed at load by TrainerStep, as the loop does, so every arm runs the same step).  No receiver: the broadcasts are no-ops, so the arms price the trainer-side snapshot alone
     (the broadcast's own cost needs actors: ``split_pipeline`` at N > 1).  ``exposed_ms`` = median step
     time of an arm − the no-update arm's (the no-update arm's own spread is the noise floor); ``hidden_frac`` = 1 − exposed / snapshot_ms.  The
     reference blocks the trainer for the whole update instead (finetune_loop.py:174-215)."""
@@ -353,11 +357,10 @@ def snapshot_overlap(ts: "TrainerStep", t_ref: float, steps: int, warmup: int, f
     del flat, params
     nbytes = sum(p.numel() * p.element_size() for _, p in named) + 2 * sum(p.numel() for _, p in named)
     managers = {"no_update": None, "copy": mk("copy"), "zero_copy": mk("zero_copy")}
-    # re-home the parameters before any arm runs (rank 0, as the first zero-copy update would): the
-    # fused gate/up weight becomes a view of them (model_ops._fused_weight), so every arm runs the
-    # same step; t_ref (measured before, with the per-step concatenation) is reported separately
+    # the parameters are re-homed at load (TrainerStep, as the loop does; or here, before any arm
+    # runs): every arm runs the same step, the fused gate/up weight a view of them
     in_place = managers["zero_copy"]._zero_copy_flat(named, layout) is not None if rank == 0 else False
-    arms = {"no_update": [], "copy": [], "zero_copy": []}
+    arms = {"no_update": [t_ref], "copy": [], "zero_copy": []}
     order = ["no_update", "copy", "zero_copy"]
     for r in range(rounds):  # the order rotates every round, so a drift of the clocks hits every arm
         for mode in order[r % 3:] + order[:r % 3]:
@@ -383,7 +386,6 @@ def snapshot_overlap(ts: "TrainerStep", t_ref: float, steps: int, warmup: int, f
     return {"params": len(named), "snapshot_bytes": 2 * layout.total, "snapshot_ms": round(snap_ms, 3),
             "snapshot_GBps": round(nbytes / (snap_ms * 1e-3) / 1e9, 1),
             "ms_per_step_no_update": round(mean["no_update"] * 1e3, 2),
-            "ms_per_step_before_rehoming": round(t_ref * 1e3, 2),
             "no_update_spread_ms": round(spread, 3),
             "copy": arm("copy", round(snap_ms, 3)),
             # in place there is no per-update device work on the trainer: hidden_frac 1 by construction,

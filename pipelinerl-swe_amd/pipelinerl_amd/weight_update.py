@@ -240,34 +240,19 @@ class WeightUpdateManager:
             w.write(msg)
 
     def _zero_copy_flat(self, named, layout: FlatLayout) -> torch.Tensor | None:
-        """The flat buffer the parameters live in (re-homed on first use), or None when the model
-        cannot be broadcast in place (snapshot="copy", a non-bf16 or non-contiguous parameter, or
-        several devices): then the staging copy is used."""
+        """The flat buffer the parameters live in (re-homed on first use unless the loop already did
+        it at load: ``rehome_parameters``), or None when the model cannot be broadcast in place
+        (snapshot="copy", a non-bf16 or non-contiguous parameter, or several devices): then the
+        staging copy is used."""
         if self.snapshot != "zero_copy" or not named:
             return None
-        params = [p for _, p in named]
-        dev = params[0].device
-        if any(p.dtype != torch.bfloat16 or p.device != dev or not p.is_contiguous() for p in params):
-            return None
         flat = self._flat_params
-        if flat is not None and flat.numel() == layout.total and all(
-                p.data_ptr() == flat.data_ptr() + 2 * off for p, off in zip(params, layout.offsets)):
-            return flat
-        from .finetune.model_ops import weights_written
-
-        flat = torch.zeros(layout.total, dtype=torch.bfloat16, device=dev)  # padding gaps stay 0
-        with torch.no_grad():
-            for p, off in zip(params, layout.offsets):
-                view = flat[off:off + p.numel()].view(p.shape)
-                view.copy_(p.data)
-                p.data = view  # the same Parameter (optimizer state, hooks, ties), storage in the buffer
-        weights_written()
-        if dev.type == "cuda":
-            torch.cuda.current_stream(dev).synchronize()  # the old storages are released after the copies
+        if flat is None or flat_home(named, layout) is None:
+            flat = rehome_parameters(self.model)
+            if flat is not None:
+                logger.info(f"weight updates broadcast the parameters in place ({len(named)} tensors, "
+                            f"{2 * layout.total / 1e9:.2f} GB)")
         self._flat_params = flat
-        unwrap_model(self.model)._prl_flat_params = True  # checkpoints save copies (shared storage)
-        logger.info(f"weight updates broadcast the parameters in place: {len(params)} tensors re-homed into one "
-                    f"{2 * layout.total / 1e9:.2f} GB buffer")
         return flat
 
     def _ensure_staging(self, total: int, device: torch.device) -> torch.Tensor:
@@ -427,6 +412,62 @@ class WeightUpdateManager:
     def close(self) -> None:
         self.wait()
         self.pool.shutdown(wait=True)
+
+
+def flat_home(named, layout: FlatLayout) -> torch.Tensor | None:
+    """The 1-D bf16 buffer the parameters already live in, laid out as ``layout`` (parameter i at
+    element ``layout.offsets[i]``), as a view from parameter 0 on; None when they do not."""
+    params = [p for _, p in named]
+    if not params or any(p.dtype != torch.bfloat16 or not p.is_contiguous() for p in params):
+        return None
+    p0 = params[0]
+    try:
+        st = p0.untyped_storage()
+        base = p0.storage_offset()
+        if any(p.untyped_storage().data_ptr() != st.data_ptr() or p.storage_offset() - base != off
+               for p, off in zip(params, layout.offsets)):
+            return None
+        if st.nbytes() < (base + layout.total) * 2:
+            return None
+    except Exception:  # noqa: BLE001 - a tensor without an ordinary storage
+        return None
+    return p0.detach().as_strided((layout.total,), (1,), base)
+
+
+def rehome_parameters(model) -> torch.Tensor | None:
+    """Put every parameter of (the language model of) ``model`` into ONE bf16 buffer laid out as the
+    weight broadcast's flat layout (``FlatLayout`` of ``parameters_info``: named_parameters order,
+    16-B aligned slots): ``p.data`` becomes a view of it — the same Parameter objects, optimizer
+    state, hooks and ties.  The broadcast then reads the parameters in place (no per-update copy),
+    and adjacent projections (gate_proj / up_proj) are one tensor without a concatenation copy
+    (finetune/model_ops.py ``_fused_weight``).  Returns the buffer, or None when the model does not
+    qualify (FSDP DTensors, a non-bf16 or non-contiguous parameter, several devices).  A one-time
+    copy; idempotent (an already re-homed model is returned as it is)."""
+    m = unwrap_model(model)
+    named = list(m.named_parameters())
+    if not named or _is_sharded(named):
+        return None
+    params = [p for _, p in named]
+    dev = params[0].device
+    if any(p.dtype != torch.bfloat16 or p.device != dev or not p.is_contiguous() for p in params):
+        return None
+    layout = FlatLayout.from_infos(parameters_info(named))
+    existing = flat_home(named, layout)
+    if existing is not None:
+        return existing
+    from .finetune.model_ops import weights_written
+
+    flat = torch.zeros(layout.total, dtype=torch.bfloat16, device=dev)  # padding gaps stay 0
+    with torch.no_grad():
+        for p, off in zip(params, layout.offsets):
+            view = flat[off:off + p.numel()].view(p.shape)
+            view.copy_(p.data)
+            p.data = view
+    weights_written()
+    if dev.type == "cuda":
+        torch.cuda.current_stream(dev).synchronize()  # the old storages are released after the copies
+    m._prl_flat_params = True  # checkpoints save host copies (safetensors refuses shared storage)
+    return flat
 
 
 def _backend_of(group) -> str:

@@ -116,8 +116,10 @@ def _product_run(tmp_path, init, stale_cache=False):
         os.symlink(tmp_path / f, exp / f)
     for k in ("RANK", "WORLD_SIZE", "MASTER_ADDR"):
         os.environ.pop(k, None)
+    # the stale-cache control needs the concatenation cache: with the parameters re-homed at load
+    # (flat_parameters, the default) the fused gate/up weight is a view and nothing is cached
     cfg = loop_cfg(exp, exp / "unused", 1, PER_STEP, ROLLOUTS // PER_STEP, dist_backend=None, learning_rate=LR,
-                   save_final_training_state=False, log_each_n_steps=1,
+                   save_final_training_state=False, log_each_n_steps=1, flat_parameters=not stale_cache,
                    rl=dict(policy_loss="ppo", epsilon=4, kl_coef=0.0, final_kl_coef=0.0,
                            clamp_log_ratio_ref_new_value=5, temperature=1.0, divide_advantage_by_std=False))
     finetune_loop.get_optimizer = get_optimizer
