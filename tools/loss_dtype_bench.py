@@ -3,10 +3,15 @@
 re-reads the row) at the same packed micro-batch; algorithmic bytes = logits read once + dlogits
 written once (measurement tool).
 
-    python tools/loss_dtype_bench.py [--tokens 65536] [--vocab 151936]
+With ``--inplace``: the bf16 loss head writing dlogits to its own buffer (the bench's form) vs over
+the logits it has just read (dlogits aliasing batch->logits, allowed by include/prl_hip.h): same
+bytes, same kernel, alternating arms, HIP events on the launch stream.
+
+    python tools/loss_dtype_bench.py [--tokens 65536] [--vocab 151936] [--inplace]
 """
 
 import argparse
+import ctypes
 import json
 import sys
 from pathlib import Path
@@ -14,6 +19,7 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 sys.path[:0] = [str(ROOT), str(ROOT / "pipelinerl-swe_amd")]
 
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import bench  # noqa: E402
@@ -23,7 +29,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tokens", type=int, default=65536)
     ap.add_argument("--vocab", type=int, default=151936)
+    ap.add_argument("--inplace", action="store_true", help="separate vs aliased dlogits A/B (bf16)")
     a = ap.parse_args()
+    if a.inplace:
+        return inplace_ab(a)
     from pipelinerl_amd.finetune.rl.fused import GrpoParams, grpo_loss
 
     dev = torch.device("cuda", 0)
@@ -52,6 +61,59 @@ def main():
               flush=True)
         del logits, fields, loss
         torch.cuda.empty_cache()
+
+
+def inplace_ab(a, rounds: int = 5, iters: int = 10):
+    from pipelinerl_amd import _native
+    from pipelinerl_amd.finetune.rl.fused import GrpoParams, _c_batch, _workspace
+
+    dev = torch.device("cuda", 0)
+    lib = _native.load()
+    params = GrpoParams(policy_loss="ppo", epsilon=4.0, kl_coef=0.0, entropy_coef=0.0, clamp_log_ratio=5.0,
+                        temperature=1.0, batch_size=4096.0)
+    logits, fields = bench.make_workload(a.tokens, a.vocab, 2048, 256, 1234, dev)
+    x = logits.detach()
+    master = x.clone()  # the in-place arm restores its logits from here before every launch
+    sep = torch.empty_like(x)
+    B, L, V = x.shape
+    rows = torch.empty((8, B * (L - 1)), dtype=torch.float32, device=dev)
+    stats = torch.empty(_native.NSTAT, dtype=torch.float64, device=dev)
+    ws = _workspace(dev)
+    cp = params.to_c(True)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def launch(out: torch.Tensor) -> float:
+        cb = _c_batch(x, fields, None)
+        co = _native.PrlGrpoOutputs(*[rows[i].data_ptr() for i in range(8)], None, out.data_ptr(), stats.data_ptr())
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        _native.check(lib.prl_grpo_forward(ctypes.byref(cb), ctypes.byref(cp), ctypes.byref(co), ws.data_ptr(),
+                                           ws.numel(), stream), "prl_grpo_forward")
+        e1.record()
+        e1.synchronize()
+        return e0.elapsed_time(e1)
+
+    # correctness first: the aliased launch writes exactly the separate launch's dlogits
+    launch(sep)
+    ref_rows = rows.clone()
+    launch(x)
+    same = bool(torch.equal(sep, x)) and bool(torch.equal(rows, ref_rows))
+    times = {"separate": [], "in_place": []}
+    for r in range(rounds):
+        for arm in (("separate", "in_place") if r % 2 == 0 else ("in_place", "separate")):
+            t = []
+            for _ in range(iters):
+                x.copy_(master)
+                torch.cuda.synchronize()
+                t.append(launch(sep if arm == "separate" else x))
+            times[arm].append(float(np.median(t)))
+    gb = 2.0 * x.numel() * x.element_size() + 37.0 * a.tokens
+    out = {"tool": "loss_inplace_ab", "tokens": a.tokens, "vocab": a.vocab, "bit_identical": same}
+    for arm, v in times.items():
+        ms = float(np.median(v))
+        out[arm] = {"ms": round(ms, 4), "rounds_ms": [round(t, 4) for t in v], "frac": round(gb / ms / 1e6 / 8000.0, 4)}
+    print(json.dumps(out), flush=True)
+
 
 
 if __name__ == "__main__":
