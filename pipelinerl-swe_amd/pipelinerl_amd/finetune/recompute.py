@@ -24,7 +24,9 @@ model is not FSDP-sharded; the lm_head weight gradient's staging, [V, H] bf16 fr
 GEMM or an fp32 accumulator over several chunks, finetune/rl/fused_linear.py); under FSDP, the
 larger of its two unsharded working sets (fsdp_transient_bytes: the start of the backward with the
 logits' gradient, the root unit gathered, the lm_head's unsharded gradient and two decoder layers;
-the root's reduce-scatter with 3 x the root); 5 % of the device plus 4 GiB of headroom.
+the root's reduce-scatter with 3 x the root); all of it times the device allocator's rounding
+allowance (devalloc.py: up to 1/d per block under d-division size rounding, 1.25 with the trainer
+loop's default); 5 % of the device plus 4 GiB of headroom.
 Checked against the measured steady-state peak of a 32B-shaped FSDP model (tests/test_fsdp_32b_gpu.py:
 estimate without the headroom between 1x and 1.3x the measured peak).
 """
@@ -158,7 +160,9 @@ def plan_gradient_checkpointing(args, model, device: torch.device, shard_world: 
     head = 0 if getattr(config, "tie_word_embeddings", False) else vocab * int(config.hidden_size) * pbytes
     buffers = build_buffer_bytes(config, int(seq), chunk, int(shard_world), pbytes) + \
         fsdp_transient_bytes(model, int(shard_world), act, logits, head)
-    need = state + act + logits + buffers + int(HEADROOM_FRAC * total) + HEADROOM_BYTES
+    from ..devalloc import rounding_allowance
+
+    need = int((state + act + logits + buffers) * rounding_allowance()) + int(HEADROOM_FRAC * total) + HEADROOM_BYTES
     keep = need <= total
     plan = RecomputePlan(not keep, ("activations fit: no recompute" if keep else "activations do not fit: recompute"),
                          state, act, logits, buffers, total)

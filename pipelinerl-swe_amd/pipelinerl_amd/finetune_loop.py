@@ -48,6 +48,7 @@ from .finetune.rl.utils import aggregate_rl_stats
 from .finetune.sharding import fsdp_requested, set_gradient_sync, shard_model
 from .finetune.trace import PhaseTrace
 from . import native_data
+from .devalloc import DEFAULT_SETTINGS, configure_device_allocator
 from .hostgc import freeze_setup_heap
 from .finetune.types import PipelineBatchEncoding, TrainingMetrics
 from .streams import SingleStreamSpec, read_stream, set_streams_backend, write_to_streams
@@ -189,6 +190,8 @@ def run_finetuning_loop(cfg, step_fn: Callable = rl_step, model=None, tokenizer=
         raise ValueError("gradient_accumulation_passes must be divisible by num_processes")
     torch.manual_seed(args.seed)
     np.random.seed(args.seed)
+    # variable-length micro-batches: cached blocks reusable across nearby sizes (devalloc.py)
+    configure_device_allocator(args.get("allocator_settings", DEFAULT_SETTINGS))
 
     exp_root = Path(cfg.output_dir)
     output_dir = Path(args.output_dir)

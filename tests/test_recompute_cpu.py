@@ -122,3 +122,24 @@ def test_build_buffers_are_counted(m7b, monkeypatch):
     head = 152064 * 5120 * 2
     start = p32.logits_bytes + root + head + 2 * layer  # beyond the activations
     assert p32.buffer_bytes == max(start, 3 * root - p32.activation_bytes) and not p32.checkpoint, p32.as_dict()
+
+
+def test_plan_counts_the_allocator_rounding(m7b, monkeypatch):
+    """Under size rounding (devalloc.py) every block may be up to 1/d larger than its request: the
+    plan multiplies its estimate by that allowance, so a micro-batch that fits unrounded can
+    recompute once the trainer loop's rounding is in force."""
+    from pipelinerl_amd import devalloc
+    from pipelinerl_amd.finetune.recompute import HEADROOM_BYTES, HEADROOM_FRAC, plan_gradient_checkpointing
+
+    for k in devalloc.ENV_KEYS:
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setattr(devalloc, "_applied", None)
+    p = plan_gradient_checkpointing(_args(), m7b, torch.device("cuda"), device_bytes=288 * GB)
+    est = p.state_bytes + p.activation_bytes + p.logits_bytes + p.buffer_bytes
+    # a device that holds the estimate plus its headroom, but not 1.25 x the estimate
+    dev = int((est * 1.1 + HEADROOM_BYTES) / (1 - HEADROOM_FRAC))
+    assert not plan_gradient_checkpointing(_args(), m7b, torch.device("cuda"), device_bytes=dev).checkpoint
+    monkeypatch.setattr(devalloc, "_applied", devalloc.DEFAULT_SETTINGS)
+    assert plan_gradient_checkpointing(_args(), m7b, torch.device("cuda"), device_bytes=dev).checkpoint
+    # the MI355X still keeps C3's activations with the rounding allowance
+    assert not plan_gradient_checkpointing(_args(), m7b, torch.device("cuda"), device_bytes=288 * GB).checkpoint

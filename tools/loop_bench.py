@@ -76,6 +76,8 @@ def main():
                     help="gradient_checkpointing: true, as the reference config sets it (conf/finetune/base.yaml:45)")
     ap.add_argument("--ckpt-policy", choices=["auto", "always"], default="auto",
                     help="gradient_checkpointing_policy (finetune/recompute.py)")
+    ap.add_argument("--alloc", default=None,
+                    help="finetune.allocator_settings (devalloc.py; default: the product's; 'none': torch's own)")
     ap.add_argument("--workdir", default=None)
     a = ap.parse_args()
 
@@ -121,6 +123,8 @@ def main():
         rl=dict(policy_loss="ppo", epsilon=4, kl_coef=0.0, final_kl_coef=0.0, clamp_log_ratio_ref_new_value=5,
                 temperature=1.0, divide_advantage_by_std=False, aggregate_loss="sum",
                 fused_lm_head=not a.full_logits))
+    if a.alloc is not None:
+        ft["allocator_settings"] = None if a.alloc == "none" else a.alloc
     cfg = Cfg.wrap({"output_dir": str(exp), "streams": {"backend": "files"}, "finetune": ft,
                     "me": {"weight_update_group_init_method": None, "weight_update_group_world_size": 0,
                            "llm_urls": ""}})
@@ -140,6 +144,7 @@ def main():
     t1 = time.time()
     m = run_finetuning_loop(cfg)
     loop_s = time.time() - t1
+    ms = torch.cuda.memory_stats()
     lines = [json.loads(x) for x in (exp / "finetune" / "logs" / "metrics.jsonl").read_text().splitlines()]
     steady = lines[1:] or lines
     tok = sum(x["throughput/tokens_per_step"] for x in steady)
@@ -148,13 +153,16 @@ def main():
     out = {"tool": "loop_bench", "model": f"Qwen2.5-{a.model} shapes (random init, bf16)",
            "seq_length": a.seq_length, "samples_per_step": a.samples_per_step, "mean_rollout_len": a.mean_len, "length_dist": a.dist,
            "fused_lm_head": not a.full_logits, "fused_model_ops": not a.eager_ops, "steps": m.completed_steps,
-           "gradient_checkpointing": a.grad_ckpt, "checkpointing_policy": a.ckpt_policy,
+           "gradient_checkpointing": a.grad_ckpt, "checkpointing_policy": a.ckpt_policy, "allocator_settings": ft.get("allocator_settings", "default"),
            "micro_batches_per_step": [x["throughput/micro_batches_per_step"] for x in lines],
            "tokens_per_step": [x["throughput/tokens_per_step"] for x in lines],
            "step_wall_s": [round(b - a_, 3) for a_, b in zip(stamps, stamps[1:])],
            "steady_tokens_per_s": round(tok / sec, 1),
            "compute_tokens_per_s": round(sum(x["throughput/tokens_per_sec"] for x in steady) / len(steady), 1),
-           "loss": [x.get("rl/loss") for x in lines], "prep_s": round(prep_s, 1), "loop_s": round(loop_s, 1)}
+           "loss": [x.get("rl/loss") for x in lines], "prep_s": round(prep_s, 1), "loop_s": round(loop_s, 1),
+           "allocator": {k: ms.get(k) for k in ("num_alloc_retries", "num_device_alloc", "num_device_free",
+                                                  "num_ooms")} | {"peak_reserved_gb": round(ms.get("reserved_bytes.all.peak", 0) / 1e9, 2),
+                                                                       "peak_allocated_gb": round(ms.get("allocated_bytes.all.peak", 0) / 1e9, 2)}}
     print(json.dumps(out), flush=True)
 
 
