@@ -211,12 +211,20 @@ class ProbeRunner:
     ranks' RCCL collectives without partners: those ranks then skip their device synchronise,
     abort the default RCCL group (so its queued collectives return instead of hanging), and every
     later probe is skipped with the reason.  An agreement that times out counts as such a failure.
-    A device that no longer synchronises ends the probing (SystemExit)."""
+    A device that no longer synchronises ends the probing (SystemExit).
 
-    def __init__(self, rank: int, device, ctrl=None):
+    ``deadline_s`` (N > 1): a probe still running after that long is taken to be stuck in a
+    collective that will never complete; a timer thread aborts this rank's RCCL communicators (the
+    torch groups and prl_comm's), so the stuck collective returns with an error, the probe fails,
+    and every later probe is skipped — the line with `value` (measured before the probes) is still
+    printed, well before torch's own RCCL watchdog (10 min) would abort the process."""
+
+    def __init__(self, rank: int, device, ctrl=None, deadline_s: float | None = None):
         self.rank, self.device, self.ctrl = rank, torch.device(device), ctrl
         self.wall: dict[str, float] = {}
         self.poisoned: str | None = None
+        self.deadline_s = deadline_s
+        self.expired: str | None = None
 
     def _agree(self, failed: int) -> tuple[int, int]:
         """(ranks that failed, ranks in ctrl); (-1, n) when the agreement itself failed."""
@@ -237,13 +245,26 @@ class ProbeRunner:
                 dist.distributed_c10d._abort_process_group()
         except Exception as e:  # noqa: BLE001
             print(f"[rank {self.rank}] aborting the RCCL group failed: {e}", file=sys.stderr, flush=True)
+        try:
+            from pipelinerl_amd import comm
+
+            comm.abort_all()
+        except Exception as e:  # noqa: BLE001
+            print(f"[rank {self.rank}] aborting the prl_comm communicators failed: {e}", file=sys.stderr, flush=True)
+
+    def _expire(self, name: str) -> None:
+        self.expired = name
+        print(f"[rank {self.rank}] probe {name} still running after its {self.deadline_s:.0f} s deadline: "
+              "aborting the RCCL communicators", file=sys.stderr, flush=True)
+        self._abort_rccl()
 
     def run(self, name: str, fn):
         t0 = time.perf_counter()
         if self.poisoned is not None:
             self.wall[name] = 0.0
-            return {"skipped": f"probe {self.poisoned} failed on some ranks only: its collectives may be unmatched",
-                    "wall_s": 0.0}
+            why = ("passed its deadline: the RCCL communicators were aborted" if self.expired
+                   else "failed on some ranks only: its collectives may be unmatched")
+            return {"skipped": f"probe {self.poisoned} {why}", "wall_s": 0.0}
         res, failed = None, 0
         done = threading.Event()
         if self.rank == 0:  # progress on stderr (a silent multi-minute probe looks hung to a watchdog)
@@ -254,6 +275,11 @@ class ProbeRunner:
                     print(f"[bench] probe {name} running {time.perf_counter() - t0:.0f} s", file=sys.stderr, flush=True)
 
             threading.Thread(target=beat, daemon=True).start()
+        timer = None
+        if self.deadline_s and self.ctrl is not None:
+            timer = threading.Timer(self.deadline_s, self._expire, args=(name,))
+            timer.daemon = True
+            timer.start()
         try:
             res = fn()
         except Exception as e:  # noqa: BLE001
@@ -262,8 +288,14 @@ class ProbeRunner:
             failed = 1
             print(f"[rank {self.rank}] probe {name} failed:\n{traceback.format_exc()}", file=sys.stderr, flush=True)
             res = {"error": f"{type(e).__name__}: {e}"[:400]}
+        finally:
+            if timer is not None:
+                timer.cancel()
+        if self.expired == name:  # the communicators are gone: nothing after this may use them
+            failed = 1
+            res = dict(res or {}, deadline_s=self.deadline_s)
         nfail, n = self._agree(failed)  # before any device synchronise
-        partial = nfail < 0 or 0 < nfail < n
+        partial = nfail < 0 or 0 < nfail < n or self.expired is not None
         if nfail != 0 and not failed:
             res = dict(res or {}, error_on_another_rank=True)
         if partial:
@@ -397,7 +429,9 @@ def main():
     import datetime
 
     ctrl = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=300)) if world > 1 else None
-    runner = ProbeRunner(rank, dev, ctrl)
+    # a probe stuck in a collective is cut off after this long (N > 1; torch's RCCL watchdog: 10 min)
+    deadline = float(os.environ.get("PRL_BENCH_PROBE_DEADLINE_S", "480")) if world > 1 else None
+    runner = ProbeRunner(rank, dev, ctrl, deadline_s=deadline)
     optional, probe_wall = runner.run, runner.wall
 
     logits = fields = None

@@ -13,6 +13,7 @@ Collectives are enqueued on the caller's current HIP stream and return immediate
 from __future__ import annotations
 
 import ctypes
+import weakref
 import os
 from datetime import timedelta
 from pathlib import Path
@@ -82,11 +83,29 @@ def _stream(t: torch.Tensor) -> int:
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
+_LIVE: "weakref.WeakSet[RcclComm]" = weakref.WeakSet()  # this process's open communicators
+
+
+def abort_all() -> int:
+    """Abort every open prl_comm communicator of this process, so a collective that will never
+    complete returns (bench.py's probe deadline); returns how many were aborted."""
+    n = 0
+    for c in list(_LIVE):
+        if c._h:
+            try:
+                c.abort()
+                n += 1
+            except CommError:
+                pass
+    return n
+
+
 class RcclComm:
     def __init__(self, handle: ctypes.c_void_p, rank: int, world: int, device: torch.device, store=None):
         self._h = handle
         self.rank, self.world, self.device = rank, world, device
         self._store = store  # keeps the rendezvous alive while the communicator exists
+        _LIVE.add(self)
 
     @classmethod
     def create(cls, init_method: str, rank: int, world: int, device: torch.device | str | int,

@@ -1,7 +1,8 @@
 """bench.py's side-probe orchestration on a world-2 gloo group (CPU): a probe that fails on every
 rank is reported and the next probe still runs; a probe that fails on one rank only is reported on
 every rank and every later probe is skipped with the reason (its collectives may be unmatched);
-wall times are recorded; the top-level DP scaling quantity is formed from the C3 probe's own local /
+a probe stuck past its deadline has its communicators aborted (the stuck collective returns), is
+reported, and every later probe is skipped; wall times are recorded; the top-level DP scaling quantity is formed from the C3 probe's own local /
 DP timings."""
 
 import json
@@ -77,3 +78,46 @@ def test_dp_scaling_from_the_c3_probe():
     assert s["c3_extrapolated_efficiency"] == 0.998 and s["c3_extrapolated_tokens_per_s"] == 56800.0
     assert s["trainer_step_1.5b_efficiency"] == 0.97
     assert bench.dp_scaling(8, {"error": "x"}, None) is None
+
+
+def _stuck(rank, world, port, out):
+    sys.path[:0] = [str(ROOT), str(ROOT / "pipelinerl-swe_amd")]
+    os.environ.update(OMP_NUM_THREADS="1")
+    import threading
+
+    import torch.distributed as dist
+
+    import bench
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    ctrl = dist.new_group(backend="gloo")
+    r = bench.ProbeRunner(rank, "cpu", ctrl, deadline_s=2.0)
+    released = threading.Event()
+    aborted = []
+
+    def abort():  # stands in for RCCL's abort: the stuck collective returns with an error
+        aborted.append(True)
+        released.set()
+
+    r._abort_rccl = abort
+
+    def hung():
+        if not released.wait(60):
+            return {"value": "never released"}
+        raise RuntimeError("collective aborted")
+
+    res = {"quick": r.run("quick", lambda: {"value": 1}), "hung": r.run("hung", hung),
+           "after": r.run("after", lambda: {"value": 2}), "aborted": len(aborted), "wall": r.wall}
+    Path(out, f"r{rank}.json").write_text(json.dumps(res))
+    dist.destroy_process_group()
+
+
+def test_probe_past_its_deadline_aborts_and_skips_the_rest(tmp_path):
+    mp.spawn(_stuck, args=(2, free_port(), str(tmp_path)), nprocs=2, join=True)
+    for rank in range(2):
+        r = json.loads((tmp_path / f"r{rank}.json").read_text())
+        assert r["quick"]["value"] == 1  # the timer of a probe that finished in time never fires
+        assert "collective aborted" in r["hung"]["error"] and r["hung"]["deadline_s"] == 2.0
+        assert 2.0 <= r["wall"]["hung"] < 30
+        assert r["aborted"] >= 1
+        assert "passed its deadline" in r["after"]["skipped"]

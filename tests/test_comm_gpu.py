@@ -39,6 +39,22 @@ def test_world1_collectives():
         c.close()
 
 
+def test_abort_all_tears_down_every_open_communicator():
+    """bench.py's probe deadline: comm.abort_all() aborts the process's open communicators (closed
+    ones are skipped) and leaves them unusable."""
+    from pipelinerl_amd import comm
+
+    a, b = _comm(), _comm()
+    b.close()
+    try:
+        assert comm.abort_all() == 1
+        assert a._h is None and comm.abort_all() == 0
+        with pytest.raises(Exception):
+            a.all_reduce(torch.ones(4, device="cuda"))
+    finally:
+        a.close()
+
+
 def test_weight_update_sender_on_prl_comm():
     from pipelinerl_amd.weight_update import WeightUpdateManager
 
