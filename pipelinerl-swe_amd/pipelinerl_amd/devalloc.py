@@ -62,6 +62,11 @@ def rounding_allowance() -> float:
     return 1.0 + 1.0 / min(ds) if ds else 1.0
 
 
+def _set_allocator_settings(settings: str) -> None:
+    fn = getattr(torch._C, "_accelerator_setAllocatorSettings", None)  # torch >= 2.9's name
+    (fn or torch.cuda.memory._set_allocator_settings)(settings)
+
+
 def configure_device_allocator(settings: str | None = DEFAULT_SETTINGS) -> str | None:
     """Apply ``settings`` to the device caching allocator (future allocations only; safe after
     device initialisation).  Returns what was applied, or None when nothing was (no settings, no
@@ -73,7 +78,7 @@ def configure_device_allocator(settings: str | None = DEFAULT_SETTINGS) -> str |
         logger.info("device allocator: keeping %s=%s", user[0], os.environ[user[0]])
         return None
     global _applied
-    torch.cuda.memory._set_allocator_settings(str(settings))
+    _set_allocator_settings(str(settings))
     _applied = str(settings)
     logger.info("device allocator: %s", settings)
     return str(settings)

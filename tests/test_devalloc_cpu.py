@@ -8,7 +8,7 @@ from pipelinerl_amd import devalloc
 def _fake_device(monkeypatch):
     applied = []
     monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
-    monkeypatch.setattr(torch.cuda.memory, "_set_allocator_settings", applied.append)
+    monkeypatch.setattr(devalloc, "_set_allocator_settings", applied.append)
     for k in devalloc.ENV_KEYS:
         monkeypatch.delenv(k, raising=False)
     return applied
