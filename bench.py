@@ -289,8 +289,9 @@ class ProbeRunner:
             print(f"[rank {self.rank}] probe {name} failed:\n{traceback.format_exc()}", file=sys.stderr, flush=True)
             res = {"error": f"{type(e).__name__}: {e}"[:400]}
         finally:
-            if timer is not None:
+            if timer is not None:  # after join() the abort either ran to completion or never will
                 timer.cancel()
+                timer.join()
         if self.expired == name:  # the communicators are gone: nothing after this may use them
             failed = 1
             res = dict(res or {}, deadline_s=self.deadline_s)
