@@ -159,6 +159,10 @@ def main():
            "step_wall_s": [round(b - a_, 3) for a_, b in zip(stamps, stamps[1:])],
            "steady_tokens_per_s": round(tok / sec, 1),
            "compute_tokens_per_s": round(sum(x["throughput/tokens_per_sec"] for x in steady) / len(steady), 1),
+           "passes_s": [round(x["throughput/sec_per_pass"] * x["throughput/micro_batches_per_step"], 3) for x in lines],
+           "waiting_for_data_s": [round(b - a_, 3) for a_, b in zip([0.0] + [x["stats/time_waiting_for_data"] for x in lines],
+                                                                    [x["stats/time_waiting_for_data"] for x in lines])],
+           "trace_ms": {k: [x.get(k) for x in lines] for k in sorted({k for x in lines for k in x if k.startswith("trace/")})},
            "loss": [x.get("rl/loss") for x in lines], "prep_s": round(prep_s, 1), "loop_s": round(loop_s, 1),
            "allocator": {k: ms.get(k) for k in ("num_alloc_retries", "num_device_alloc", "num_device_free",
                                                   "num_ooms")} | {"peak_reserved_gb": round(ms.get("reserved_bytes.all.peak", 0) / 1e9, 2),
