@@ -123,9 +123,10 @@ def test_f2_full_vocab_bf16_resident_path():
 
 
 @pytest.mark.parametrize("V,dtype", [(1000, "bf16"), (1001, "bf16"), (1001, "fp32"), (8 * 1024 * 3 + 8, "bf16"),
-                                     (152064, "bf16")])
+                                     (152064, "bf16"), (151936, "fp32"), (152064, "fp32")])
 def test_kernel_paths_vs_oracle(V, dtype):
-    """Resident (bf16, V % 8 == 0), streaming vector and scalar paths, ragged last vector."""
+    """Resident (bf16, V % 8 == 0), streaming vector and scalar paths, ragged last vector; fp32 logits
+    (Accelerate's upcast regime: the streaming kernel) at the Qwen2.5 vocabularies."""
     T = 29
     b = synth.packed_rl_batch(3, [10, 12, 7], [3, 4, 2], id_range=V, eos=5)
     rng = np.random.default_rng(V)
@@ -370,6 +371,62 @@ def test_c2_full_size_vs_oracle():
                                     grad_rows=np.array([0]), rows=o)
     assert not _c2_mismatches(float(lb), stats_b, rb.cpu().numpy(), mask, ob, hb, cfg_bad)
     print(f"C2 full size: oracle {t_oracle:.1f} s over {T} x {V}; negative control caught: {bad_ctl[:3]}")
+
+
+@pytest.mark.timeout(1200)
+def test_c2_fp32_logits_full_size_vs_oracle():
+    """C2's micro-batch in the fp32-logits regime (Accelerate mixed precision upcasts the logits,
+    finetune_loop.py:381-385; 65 536 x 151 936 fp32, 39.8 GB: the streaming kernel, which re-reads
+    each row for the gradient) against the oracle over every row, as the bf16 test above: loss and
+    statistics at 1e-4, every row's outputs, sampled dlogits vs the oracle's gradient at the fp32
+    bar (1e-4 relative).  The logits carry fp32 noise below bf16's resolution, so a kernel that
+    rounded them to bf16 anywhere would fail."""
+    from pipelinerl_amd.finetune.rl import build_stats
+    from pipelinerl_amd.finetune.rl.fused import grpo_loss, prepare_fields
+
+    T, V, seq = 65536, 151936, 2048
+    lb, f, pos = _c2_inputs(T, V, seq)
+    g = torch.Generator(device=DEV).manual_seed(1)
+    logits = torch.empty((1, T, V), device=DEV, dtype=torch.float32)
+    for a in range(0, T, 8192):
+        b = min(a + 8192, T)
+        logits[0, a:b] = lb[0, a:b].float() + 1e-3 * torch.randn((b - a, V), generator=g, device=DEV)
+    del lb
+    torch.cuda.empty_cache()
+    logits.requires_grad_(True)
+    p = _c2_params(C2_CFG)
+    fields = prepare_fields(f, logits.device)
+    loss1, stats1, rows1 = grpo_loss(logits, fields, p)
+    loss1.backward()
+    d1 = logits.grad
+    logits.grad = None
+    assert d1.dtype == torch.float32 and torch.all(d1[0, T - 1] == 0)
+    nseq = T // seq
+    hb = {k: v.cpu().numpy() for k, v in f.items()} | {"position_ids": pos[None].cpu().numpy(), "is_packed": True}
+    meta = _types_ns(is_packed=True, input_ids=f["input_ids"])
+    stats = build_stats(stats1.cpu().numpy(), meta, p, p.kl_coef, p.entropy_coef, nseq, False)
+    lg = np.empty((1, T, V), dtype=np.float32)
+    with torch.no_grad():
+        for a in range(0, T, 4096):
+            lg[0, a:a + 4096] = logits[0, a:a + 4096].cpu().numpy()
+    mask = hb["labels"][0, 1:] != -100
+    o = grpo_oracle.rl_step_oracle(lg, hb, C2_CFG, 0, 10, compute_grad=True, dtype=np.float32, threads=16,
+                                   row_chunk=64, grad_rows=np.array([0]))
+    bad = _c2_mismatches(float(loss1.detach()), stats, rows1.cpu().numpy(), mask, o, hb, C2_CFG)
+    assert not bad, bad
+    sample = np.array([0, 1, 255, 256, 257, 4095, 30000, 65534])
+    o_rows = grpo_oracle.rl_step_oracle(lg, hb, C2_CFG, 0, 10, compute_grad=True, dtype=np.float32,
+                                        grad_rows=sample, rows=o)
+    got = d1[0, torch.tensor(sample, device=DEV)].cpu().numpy()
+    want = o_rows["dlogits_rows"]
+    ok, err = rel_close(got, want, 1e-4, 1e-6 * float(np.abs(want).max()))
+    assert ok, ("sampled fp32 dlogits vs oracle", err)
+
+
+def _types_ns(**kw):
+    import types as _types
+
+    return _types.SimpleNamespace(**kw)
 
 
 def test_flatten_unflatten_and_sqnorm():
