@@ -570,6 +570,163 @@ __global__ __launch_bounds__(BLOCK) void grpo_fwd_stream(KArgs a) {
   }
 }
 
+// fp32 rows (Accelerate's mixed precision upcasts the logits, finetune_loop.py:381-385): a row
+// (594 KiB at V = 151 936) does not fit one CU's registers, and grpo_fwd_stream's gradient pass
+// re-reads it — from HBM, mostly: 74.0 GB fetched per C2 launch for 39.8 GB of logits
+// (profiles/r04_fp32_pmc.json).  This kernel keeps NR vectors per lane in registers and NL in LDS
+// (NL x 16 KiB of the CU's 160 KiB; 75 % of a Qwen2.5 row at NR = 19, NL = 9) and re-reads only the
+// tail.  Each lane writes and reads only its own LDS slots, so the slab needs no barrier; one
+// workgroup per CU (the slab), rows strided over the grid as grpo_fwd_stream.
+#ifndef PRL_HYB_NR
+#define PRL_HYB_NR 19
+#endif
+#ifndef PRL_HYB_NL
+#define PRL_HYB_NL 9
+#endif
+#ifndef PRL_HYB_U1
+#define PRL_HYB_U1 2
+#endif
+constexpr int kHybNR = PRL_HYB_NR, kHybNL = PRL_HYB_NL;
+typedef __attribute__((address_space(3))) void lds_void_t;
+// d = p (alpha + beta t) (+ gadd at the target column) of one fp32 vector, stored at voff + soff of
+// the dlogits row.  ``rel`` = target column - the vector's first column (in [0, 4) for the one lane
+// that owns it).  The offsets come as one per-lane VGPR plus a wave-uniform SGPR and the target as
+// a uniform difference: per-vector lane addresses would be hoisted out of the row loop as
+// loop invariants (3 VGPRs per resident vector: what spilled the first version).  The store is
+// store_row_b128 (fenced: SGPR soffset, see its comment).
+__device__ __forceinline__ void hyb_store(__amdgpu_buffer_rsrc_t ws, int voff, int soff, int rel, f32x4 x,
+                                         bool zero_row, float c, float M, float l2s, float alpha, float beta,
+                                         float gadd) {
+  f32x4 d = {0.f, 0.f, 0.f, 0.f};
+  if (!zero_row) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float t = __builtin_fmaf(x[j] - M, c, -l2s);
+      d[j] = fexp2(t) * __builtin_fmaf(beta, t, alpha);
+      if (j == rel) d[j] += gadd;
+    }
+  }
+  store_row_b128(__builtin_bit_cast(u32x4, d), ws, voff, soff);
+}
+template <int NR, int NL>
+__global__ __launch_bounds__(1024) void grpo_fwd_hybrid_f32(KArgs a) {
+  constexpr int BLOCK = 1024, NW = BLOCK / 64, U = 4;
+  constexpr int U1 = PRL_HYB_U1;  // the tail's vectors in flight in pass 1, beside the NR resident ones
+  constexpr int VSTRIDE = BLOCK * 16;  // bytes between a lane's consecutive vectors
+  __shared__ f32x4 slab[NL > 0 ? NL : 1][BLOCK];
+  __shared__ float red[2][NW][3];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int64_t nrows = fwd_rows(a);
+  const int nvec = (int)(a.V >> 2);  // the host guarantees nvec >= (NR + NL) * BLOCK
+  const float c = kLog2e / a.temperature;
+  const float inv_t = 1.0f / a.temperature;
+  const float* lg = static_cast<const float*>(a.logits);
+  float* dl = static_cast<float*>(a.dlogits);
+  const int voff = tid * 16;
+  const int wu = __builtin_amdgcn_readfirstlane(wid);
+  int par = 0;
+  for (int64_t i = blockIdx.x; i < nrows; i += gridDim.x, par ^= 1) {
+    int64_t lrow, tok, q;
+    map_row<RowLd>(a, i, lrow, tok, q);
+    const float* row = lg + lrow * a.ld;
+    const auto rs = row_rsrc(row, a.V * 4);
+    // the LDS share first, by LDS-DMA (no registers): wave w's 64 lanes fill slab[k][64 w ..] (1 KiB)
+#pragma unroll
+    for (int k = 0; k < NL; ++k)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(&slab[k][wu * 64]), 16, voff, (NR + k) * VSTRIDE, 0,
+                                               kLoadAux);
+    f32x4 buf[NR];
+#pragma unroll
+    for (int k = 0; k < NR; ++k)
+      buf[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, k * VSTRIDE, kLoadAux));
+    const int64_t tid_raw = RowLd::ld(a.input_ids, tok);
+    const TokIn tin = tok_in<RowLd>(a, tok);
+    const bool bad_id = (uint64_t)tid_raw >= (uint64_t)a.V;
+    const int tgt = bad_id ? -1 : (int)tid_raw;
+    const float xr = row_logit(row, bad_id ? 0 : tid_raw);
+    const float xt = bad_id ? __builtin_nanf("") : xr;
+    Lse st = lse_empty();
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      const float x[4] = {buf[k][0], buf[k][1], buf[k][2], buf[k][3]};
+      lse_add<4>(st, x, c);
+    }
+    // this lane's DMA pieces landed (issued before the register loads, which have all returned by
+    // now; the explicit wait also orders the LDS reads after the DMA for the compiler)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int k = 0; k < NL; ++k) {
+      const f32x4 v = slab[k][tid];
+      const float x[4] = {v[0], v[1], v[2], v[3]};
+      lse_add<4>(st, x, c);
+    }
+    constexpr int kTail0 = (NR + NL) * BLOCK;
+    int gv = kTail0 + tid;
+    for (; gv + (U1 - 1) * BLOCK < nvec; gv += U1 * BLOCK) {
+      float x[U1][4];
+#pragma unroll
+      for (int u = 0; u < U1; ++u) RowIO<float, 4>::load(row, gv + u * BLOCK, x[u]);
+#pragma unroll
+      for (int u = 0; u < U1; ++u) lse_add<4>(st, x[u], c);
+    }
+    for (; gv < nvec; gv += BLOCK) {
+      float x[4];
+      RowIO<float, 4>::load(row, gv, x);
+      lse_add<4>(st, x, c);
+    }
+    st = wave_reduce_lse(st, c);
+    if (lane == 0) {
+      red[par][wid][0] = st.m;
+      red[par][wid][1] = st.s;
+      red[par][wid][2] = st.w;
+    }
+    __syncthreads();
+    const Lse tot = block_combine<NW>(red[par], c);
+    const float l2s = log2f(tot.s);
+    const float M = tot.m;
+    const float lse = M * inv_t + kLn2 * l2s;
+    const float H = kLn2 * (l2s - tot.w / tot.s);
+    const float lp = (xt - M) * inv_t - kLn2 * l2s;
+    const TokGrad core = row_epilogue(a, q, tin, lp, H, lse, M, l2s, tid == 0);
+    // opaque here, so nothing pass 1 derived from the row stays live into pass 2
+#pragma unroll
+    for (int k = 0; k < NR; ++k) asm volatile("" : "+v"(buf[k]));
+    if (a.write_grad) {
+      const auto ws = row_rsrc(dl + lrow * a.ld, a.V * 4);
+      const float alpha = -(core.g_lp + core.g_h * H) * inv_t;
+      const float beta = -core.g_h * kLn2 * inv_t;
+      const float gadd = core.g_lp * inv_t;
+      const bool zero_row = (core.g_lp == 0.f && core.g_h == 0.f);
+      const int lcol = tid * 4;
+#pragma unroll
+      for (int k = 0; k < NR; ++k)
+        hyb_store(ws, voff, k * VSTRIDE, (tgt - k * BLOCK * 4) - lcol, buf[k], zero_row, c, M, l2s, alpha, beta, gadd);
+#pragma unroll
+      for (int k = 0; k < NL; ++k)
+        hyb_store(ws, voff, (NR + k) * VSTRIDE, (tgt - (NR + k) * BLOCK * 4) - lcol, slab[k][tid], zero_row, c, M, l2s,
+                  alpha, beta, gadd);
+      int g2 = kTail0 + tid;
+      for (; g2 + (U - 1) * BLOCK < nvec; g2 += U * BLOCK) {
+        f32x4 x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          x[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, g2 * 16, u * VSTRIDE, kLoadAux));
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          hyb_store(ws, g2 * 16, u * VSTRIDE, (tgt - u * BLOCK * 4) - g2 * 4, x[u], zero_row, c, M, l2s, alpha, beta,
+                    gadd);
+      }
+      for (; g2 < nvec; g2 += BLOCK) {
+        const f32x4 x = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, g2 * 16, 0, kLoadAux));
+        hyb_store(ws, g2 * 16, 0, tgt - g2 * 4, x, zero_row, c, M, l2s, alpha, beta, gadd);
+      }
+    }
+    // the next row's DMA overwrites this lane's slab slots only after its own reads above (same
+    // lane, program order: the LDS reads retire before the next row's DMA is issued)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+}
+
 // gradient pass from saved per-row coefficients for the upstream gradient *up (device);
 // skip_if_one: dlogits already holds the gradient for *up == grad_scale (fused forward)
 template <typename T, int VEC>
@@ -870,6 +1027,11 @@ static hipError_t launch_rows(const KArgs& a, const PrlGrpoBatch* b, const PrlGr
     hipLaunchKernelGGL((grpo_fwd_stream<uint16_t, 1>), dim3(grid), dim3(256), 0, s, a);
   } else if (b->V % 4 == 0 && b->ld % 4 == 0 && aligned16(b->logits) &&
              (!p->write_grad || aligned16(out->dlogits))) {
+    if (PRL_HYB_NL >= 0 && b->V / 4 >= (int64_t)(kHybNR + kHybNL) * 1024) {  // a tail to stream: the row part-resident
+      const int g1 = (int)(nrows < cus ? nrows : cus);  // one workgroup per CU (the LDS slab)
+      hipLaunchKernelGGL((grpo_fwd_hybrid_f32<kHybNR, kHybNL>), dim3(g1), dim3(1024), 0, s, a);
+      return hipGetLastError();
+    }
     const int64_t want1 = (int64_t)cus * PRL_STREAM_F32_WG_PER_CU;  // 1024-thread workgroups
     const int g1 = (int)(nrows < want1 ? nrows : want1);
     hipLaunchKernelGGL((grpo_fwd_stream<float, 4, 1024, PRL_STREAM_F32_U>), dim3(g1), dim3(1024), 0, s, a);
