@@ -586,6 +586,9 @@ __global__ __launch_bounds__(BLOCK) void grpo_fwd_stream(KArgs a) {
 #ifndef PRL_HYB_U1
 #define PRL_HYB_U1 2
 #endif
+#ifndef PRL_HYB_PREFETCH
+#define PRL_HYB_PREFETCH 0  // 1: the next row's resident loads are issued before this row's tail pass
+#endif
 constexpr int kHybNR = PRL_HYB_NR, kHybNL = PRL_HYB_NL;
 typedef __attribute__((address_space(3))) void lds_void_t;
 // d = p (alpha + beta t) (+ gadd at the target column) of one fp32 vector, stored at voff + soff of
@@ -610,7 +613,7 @@ __device__ __forceinline__ void hyb_store(__amdgpu_buffer_rsrc_t ws, int voff, i
 }
 template <int NR, int NL>
 __global__ __launch_bounds__(1024) void grpo_fwd_hybrid_f32(KArgs a) {
-  constexpr int BLOCK = 1024, NW = BLOCK / 64, U = 4;
+  constexpr int BLOCK = 1024, NW = BLOCK / 64, U = PRL_HYB_PREFETCH ? 2 : 4;  // pass 2's tail vectors in flight
   constexpr int U1 = PRL_HYB_U1;  // the tail's vectors in flight in pass 1, beside the NR resident ones
   constexpr int VSTRIDE = BLOCK * 16;  // bytes between a lane's consecutive vectors
   __shared__ f32x4 slab[NL > 0 ? NL : 1][BLOCK];
@@ -624,21 +627,32 @@ __global__ __launch_bounds__(1024) void grpo_fwd_hybrid_f32(KArgs a) {
   float* dl = static_cast<float*>(a.dlogits);
   const int voff = tid * 16;
   const int wu = __builtin_amdgcn_readfirstlane(wid);
+  f32x4 buf[NR];
+  // a row's resident part: the LDS share by LDS-DMA (no registers: wave w's 64 lanes fill
+  // slab[k][64 w ..], 1 KiB per instruction), then the register share
+  auto load_resident = [&](const __amdgpu_buffer_rsrc_t& r) {
+#pragma unroll
+    for (int k = 0; k < NL; ++k)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)(&slab[k][wu * 64]), 16, voff, (NR + k) * VSTRIDE, 0,
+                                               kLoadAux);
+#pragma unroll
+    for (int k = 0; k < NR; ++k)
+      buf[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, k * VSTRIDE, kLoadAux));
+  };
+  auto row_of_iter = [&](int64_t it) {
+    int64_t lr, tk, qq;
+    map_row<RowLd>(a, it, lr, tk, qq);
+    return row_rsrc(lg + lr * a.ld, a.V * 4);
+  };
+  if (blockIdx.x < nrows) load_resident(row_of_iter(blockIdx.x));
   int par = 0;
   for (int64_t i = blockIdx.x; i < nrows; i += gridDim.x, par ^= 1) {
     int64_t lrow, tok, q;
     map_row<RowLd>(a, i, lrow, tok, q);
     const float* row = lg + lrow * a.ld;
     const auto rs = row_rsrc(row, a.V * 4);
-    // the LDS share first, by LDS-DMA (no registers): wave w's 64 lanes fill slab[k][64 w ..] (1 KiB)
-#pragma unroll
-    for (int k = 0; k < NL; ++k)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(&slab[k][wu * 64]), 16, voff, (NR + k) * VSTRIDE, 0,
-                                               kLoadAux);
-    f32x4 buf[NR];
-#pragma unroll
-    for (int k = 0; k < NR; ++k)
-      buf[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, k * VSTRIDE, kLoadAux));
+    const bool has_next = i + gridDim.x < nrows;
+    bool loaded_next = false;
     const int64_t tid_raw = RowLd::ld(a.input_ids, tok);
     const TokIn tin = tok_in<RowLd>(a, tok);
     const bool bad_id = (uint64_t)tid_raw >= (uint64_t)a.V;
@@ -705,6 +719,15 @@ __global__ __launch_bounds__(1024) void grpo_fwd_hybrid_f32(KArgs a) {
       for (int k = 0; k < NL; ++k)
         hyb_store(ws, voff, (NR + k) * VSTRIDE, (tgt - (NR + k) * BLOCK * 4) - lcol, slab[k][tid], zero_row, c, M, l2s,
                   alpha, beta, gadd);
+      if constexpr (PRL_HYB_PREFETCH != 0) {
+        // the next row's resident part streams in behind this row's tail (its slab slots were just
+        // read by this lane: the reads retire first)
+        if (has_next) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          load_resident(row_of_iter(i + gridDim.x));
+          loaded_next = true;
+        }
+      }
       int g2 = kTail0 + tid;
       for (; g2 + (U - 1) * BLOCK < nvec; g2 += U * BLOCK) {
         f32x4 x[U];
@@ -724,6 +747,7 @@ __global__ __launch_bounds__(1024) void grpo_fwd_hybrid_f32(KArgs a) {
     // the next row's DMA overwrites this lane's slab slots only after its own reads above (same
     // lane, program order: the LDS reads retire before the next row's DMA is issued)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (has_next && !loaded_next) load_resident(row_of_iter(i + gridDim.x));
   }
 }
 
