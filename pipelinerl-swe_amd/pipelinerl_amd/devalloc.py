@@ -17,9 +17,11 @@ torch build: it warns and ignores it.)
 
 Rounding costs memory: a block is up to 1/d larger than its request (d divisions).  The default
 rounds requests under 512 MB (parameters, their gradients and AdamW moments, most activations) to
-16 divisions and larger ones (the logits chunk, long activations, the flat parameter buffer) to 4,
-and the gradient-checkpointing plan multiplies its estimate by ``rounding_allowance()``
-(finetune/recompute.py).
+16 divisions and larger ones (the logits chunk, long activations, the flat parameter buffer) to 4.
+The gradient-checkpointing plan (finetune/recompute.py) sizes each of its terms with the
+allocator's own rounding (``round_size``) at the micro-batch's largest shapes — rounding is
+monotonic, so shorter micro-batches never round above them; a flat 1 + 1/d allowance
+(``rounding_allowance``) flipped the 32B FSDP plan at 8 ranks to recomputing every layer.
 
 ``finetune.allocator_settings`` (build-only key; default ``DEFAULT_SETTINGS``; empty or null keeps
 torch's defaults).  Settings the user exports in ``PYTORCH_HIP_ALLOC_CONF`` /
@@ -53,12 +55,72 @@ def divisions(settings: str | None) -> list[int]:
     return [int(v)]
 
 
+_MB = 1 << 20
+_INTERVALS = 16  # PyTorch's per-power-of-two division table: [< 2 MiB, < 4 MiB, ..., >= 32 GiB]
+
+
+def division_table(settings: str | None) -> list[int]:
+    """The caching allocator's divisions per power-of-two size interval under ``settings`` (index i:
+    sizes in [2^(20+i), 2^(21+i)), index 0 also below, the last also above), following PyTorch's
+    parser: ``N`` fills every interval; ``[<MB>:N, ..., >:N]`` fills up to log2(MB) with each
+    count and the rest with the ``>`` count.  All zeros: no rounding."""
+    table = [0] * _INTERVALS
+    m = re.search(r"roundup_power2_divisions:(\[[^\]]*\]|\d+)", settings or "")
+    if not m:
+        return table
+    v = m.group(1)
+    if not v.startswith("["):
+        return [int(v)] * _INTERVALS
+    last = 0
+    for item in v[1:-1].split(","):
+        if ":" not in item:
+            continue
+        key, n = item.rsplit(":", 1)
+        n = int(n)
+        if key.strip() == ">":
+            table[last:] = [n] * (_INTERVALS - last)
+        else:
+            idx = min(max(int(key).bit_length() - 1, 0), _INTERVALS - 1)
+            table[last:idx] = [n] * (idx - last)
+            last = idx
+    return table
+
+
+def _in_force() -> str | None:
+    return _applied or next((os.environ[k] for k in ENV_KEYS if os.environ.get(k)), None)
+
+
+def round_size(nbytes: int, settings: str | None = None) -> int:
+    """The block the caching allocator serves an ``nbytes`` request with (PyTorch's round_size:
+    512-B granules, or the next of ``d`` equal steps between two powers of two when the request's
+    interval has d > 1 divisions and exceeds 512·d bytes).  ``settings``: the settings in force by default."""
+    n = int(nbytes)
+    if n < 512:
+        return 512
+    table = division_table(settings if settings is not None else _in_force())
+    d = table[min(max(n.bit_length() - 1 - 20, 0), _INTERVALS - 1)]
+    if d > 1 and n > 512 * d:
+        if n & (n - 1) == 0:
+            return n
+        floor = 1 << (n.bit_length() - 1)
+        step = floor >> (d.bit_length() - 1)
+        if step == 0:
+            return floor << 1
+        base = n & ~(step - 1)
+        return n if base == n else base + step
+    return -(-n // 512) * 512
+
+
+def rounded_factor(nbytes: int, settings: str | None = None) -> float:
+    """round_size(nbytes) / nbytes (1.0 for an empty request)."""
+    return round_size(nbytes, settings) / nbytes if nbytes > 0 else 1.0
+
+
 def rounding_allowance() -> float:
     """Upper bound of a block's size over its request under the settings in force (ours, else the
     user's environment): 1 + 1/d for the smallest division count d > 1 (1.0: no rounding; a count
     of 1 or 0 leaves sizes unrounded)."""
-    src = _applied or next((os.environ[k] for k in ENV_KEYS if os.environ.get(k)), None)
-    ds = [d for d in divisions(src) if d > 1]
+    ds = [d for d in divisions(_in_force()) if d > 1]
     return 1.0 + 1.0 / min(ds) if ds else 1.0
 
 

@@ -24,9 +24,10 @@ model is not FSDP-sharded; the lm_head weight gradient's staging, [V, H] bf16 fr
 GEMM or an fp32 accumulator over several chunks, finetune/rl/fused_linear.py); under FSDP, the
 larger of its two unsharded working sets (fsdp_transient_bytes: the start of the backward with the
 logits' gradient, the root unit gathered, the lm_head's unsharded gradient and two decoder layers;
-the root's reduce-scatter with 3 x the root); all of it times the device allocator's rounding
-allowance (devalloc.py: up to 1/d per block under d-division size rounding, 1.25 with the trainer
-loop's default); 5 % of the device plus 4 GiB of headroom.
+the root's reduce-scatter with 3 x the root); each term sized with the device allocator's own
+rounding at the micro-batch's largest shapes (devalloc.round_size: the parameters' per-tensor
+blocks, the [T, H] / [T, I] / [T, 2I] / [T, kv] activations, the logits chunk); 5 % of the device
+plus 4 GiB of headroom.
 Checked against the measured steady-state peak of a 32B-shaped FSDP model (tests/test_fsdp_32b_gpu.py:
 estimate without the headroom between 1x and 1.3x the measured peak).
 """
@@ -54,11 +55,13 @@ class RecomputePlan:
     logits_bytes: int = 0
     buffer_bytes: int = 0
     device_bytes: int = 0
+    need_bytes: int = 0  # the terms after the allocator's rounding, plus the headroom
 
     def as_dict(self) -> dict:
         return {"checkpoint": self.checkpoint, "reason": self.reason, "state_gb": round(self.state_bytes / 1e9, 2),
                 "activation_gb": round(self.activation_bytes / 1e9, 2), "logits_gb": round(self.logits_bytes / 1e9, 2),
-                "buffer_gb": round(self.buffer_bytes / 1e9, 2), "device_gb": round(self.device_bytes / 1e9, 2)}
+                "buffer_gb": round(self.buffer_bytes / 1e9, 2), "device_gb": round(self.device_bytes / 1e9, 2),
+                "need_gb": round(self.need_bytes / 1e9, 2)}
 
 
 def activation_bytes_per_token(config, dtype_bytes: int = 2) -> int:
@@ -150,8 +153,9 @@ def plan_gradient_checkpointing(args, model, device: torch.device, shard_world: 
     params = list(model.parameters())
     n = sum(p.numel() for p in params)
     pbytes = params[0].element_size() if params else 2
+    sw = max(1, int(shard_world))
     # weight + gradient + exp_avg + exp_avg_sq, all in the parameter dtype (torch / PrlAdamW)
-    state = 4 * n * pbytes // max(1, int(shard_world))
+    state = 4 * n * pbytes // sw
     act = int(ACT_ALLOWANCE * int(seq) * activation_bytes_per_token(config, pbytes))
     vocab = int(getattr(config, "vocab_size", 0))
     rl = args.get("rl", None) or {}
@@ -160,10 +164,21 @@ def plan_gradient_checkpointing(args, model, device: torch.device, shard_world: 
     head = 0 if getattr(config, "tie_word_embeddings", False) else vocab * int(config.hidden_size) * pbytes
     buffers = build_buffer_bytes(config, int(seq), chunk, int(shard_world), pbytes) + \
         fsdp_transient_bytes(model, int(shard_world), act, logits, head)
-    from ..devalloc import rounding_allowance
+    # the device allocator's size rounding (devalloc.py) at the largest shapes of the micro-batch
+    # (rounding is monotonic: shorter micro-batches round to no more)
+    from ..devalloc import round_size, rounded_factor
 
-    need = int((state + act + logits + buffers) * rounding_allowance()) + int(HEADROOM_FRAC * total) + HEADROOM_BYTES
+    H = int(config.hidden_size)
+    inter = int(getattr(config, "intermediate_size", 4 * H))
+    heads = int(getattr(config, "num_attention_heads", 1))
+    kvw = int(getattr(config, "num_key_value_heads", None) or heads) * int(getattr(config, "head_dim", None) or H // heads)
+    f_act = max(rounded_factor(int(seq) * w * pbytes) for w in (H, inter, 2 * inter, kvw))
+    f_logits = rounded_factor(logits) if logits else 1.0
+    sizes = [p.numel() * pbytes // sw for p in params]
+    f_state = (sum(round_size(b) for b in sizes if b) / max(1, sum(sizes))) if sizes else 1.0
+    need = int(state * f_state + act * f_act + logits * f_logits + buffers * max(f_state, f_act, f_logits)) + \
+        int(HEADROOM_FRAC * total) + HEADROOM_BYTES
     keep = need <= total
     plan = RecomputePlan(not keep, ("activations fit: no recompute" if keep else "activations do not fit: recompute"),
-                         state, act, logits, buffers, total)
+                         state, act, logits, buffers, total, need)
     return plan

@@ -125,21 +125,45 @@ def test_build_buffers_are_counted(m7b, monkeypatch):
 
 
 def test_plan_counts_the_allocator_rounding(m7b, monkeypatch):
-    """Under size rounding (devalloc.py) every block may be up to 1/d larger than its request: the
-    plan multiplies its estimate by that allowance, so a micro-batch that fits unrounded can
-    recompute once the trainer loop's rounding is in force."""
+    """Under the trainer loop's size rounding (devalloc.py) each term of the plan is sized with the
+    allocator's own rounding at the micro-batch's largest shapes: a device between the unrounded
+    and the rounded need recomputes only when the rounding is in force; the 32B FSDP plan at 8
+    ranks (C5) still keeps its activations (a flat 1.25 allowance flipped it to recomputing)."""
     from pipelinerl_amd import devalloc
-    from pipelinerl_amd.finetune.recompute import HEADROOM_BYTES, HEADROOM_FRAC, plan_gradient_checkpointing
+    from pipelinerl_amd.finetune.recompute import plan_gradient_checkpointing
 
     for k in devalloc.ENV_KEYS:
         monkeypatch.delenv(k, raising=False)
+    cuda = torch.device("cuda")
     monkeypatch.setattr(devalloc, "_applied", None)
-    p = plan_gradient_checkpointing(_args(), m7b, torch.device("cuda"), device_bytes=288 * GB)
-    est = p.state_bytes + p.activation_bytes + p.logits_bytes + p.buffer_bytes
-    # a device that holds the estimate plus its headroom, but not 1.25 x the estimate
-    dev = int((est * 1.1 + HEADROOM_BYTES) / (1 - HEADROOM_FRAC))
-    assert not plan_gradient_checkpointing(_args(), m7b, torch.device("cuda"), device_bytes=dev).checkpoint
+    raw = plan_gradient_checkpointing(_args(), m7b, cuda, device_bytes=288 * GB).need_bytes
     monkeypatch.setattr(devalloc, "_applied", devalloc.DEFAULT_SETTINGS)
-    assert plan_gradient_checkpointing(_args(), m7b, torch.device("cuda"), device_bytes=dev).checkpoint
-    # the MI355X still keeps C3's activations with the rounding allowance
-    assert not plan_gradient_checkpointing(_args(), m7b, torch.device("cuda"), device_bytes=288 * GB).checkpoint
+    rounded = plan_gradient_checkpointing(_args(), m7b, cuda, device_bytes=288 * GB).need_bytes
+    assert raw < rounded < raw * 1.1, (raw, rounded)
+    from pipelinerl_amd.finetune.recompute import HEADROOM_BYTES, HEADROOM_FRAC
+
+    # the terms without the headroom (5 % of the device + 4 GiB), then a device between the two
+    core = [n - int(HEADROOM_FRAC * 288 * GB) - HEADROOM_BYTES for n in (raw, rounded)]
+    dev = int((sum(core) / 2 + HEADROOM_BYTES) / (1 - HEADROOM_FRAC))
+    assert plan_gradient_checkpointing(_args(), m7b, cuda, device_bytes=dev).checkpoint
+    monkeypatch.setattr(devalloc, "_applied", None)
+    assert not plan_gradient_checkpointing(_args(), m7b, cuda, device_bytes=dev).checkpoint
+    monkeypatch.setattr(devalloc, "_applied", devalloc.DEFAULT_SETTINGS)
+    m32 = _meta_model("32b")
+    p = plan_gradient_checkpointing(_args(), m32, cuda, shard_world=8, device_bytes=288 * 2 ** 30)
+    assert not p.checkpoint, p.as_dict()
+
+
+def test_round_size_follows_the_allocator():
+    """devalloc.round_size against PyTorch's rule (the GPU test checks two of these on the device)."""
+    from pipelinerl_amd import devalloc
+
+    S = devalloc.DEFAULT_SETTINGS
+    assert devalloc.division_table(S) == [16] * 9 + [4] * 7
+    assert devalloc.division_table("roundup_power2_divisions:8") == [8] * 16
+    assert devalloc.division_table("max_split_size_mb:64") == [0] * 16
+    assert devalloc.round_size(int(1.1 * 2 ** 30), S) == 5 * 2 ** 28  # 4 divisions above 512 MiB
+    assert devalloc.round_size(300 * 10 ** 6, S) == 288 << 20  # 16 below
+    assert devalloc.round_size(2 ** 27, S) == 2 ** 27  # powers of two are kept
+    assert devalloc.round_size(1000, S) == 1024 and devalloc.round_size(100, S) == 512
+    assert devalloc.round_size(300 * 10 ** 6, "") == -(-300 * 10 ** 6 // 512) * 512  # no rounding configured
