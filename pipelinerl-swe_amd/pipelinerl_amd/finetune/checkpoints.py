@@ -85,11 +85,30 @@ def load_model(args, model_class: str, current_dir: Path, device: torch.device, 
     if plan.checkpoint:
         model.gradient_checkpointing_enable(
             gradient_checkpointing_kwargs={"use_reentrant": bool(args.get("reentrant_checkpointing", False))})
+        keep_activations(model, plan.keep_layers)
     if model_class == "causal-language-modeling-with-value-head":
         from .value_model import AutoModelForCausalLMWithValueHead
 
         model = AutoModelForCausalLMWithValueHead(model)
     return model.to(device)
+
+
+def keep_activations(model, keep: int) -> int:
+    """After ``gradient_checkpointing_enable``: the last ``keep`` decoder layers keep their
+    activations (their ``gradient_checkpointing`` flag, which transformers' GradientCheckpointingLayer
+    reads per call, goes back off); the others recompute.  The kept layers are the last ones, so
+    only checkpointed layers precede the boundary: the decoder's cross-layer residual hand-over
+    (model_ops._decoder_forward) already stays off out of a checkpointed layer.  Returns how many
+    layers keep their activations."""
+    if keep <= 0:
+        return 0
+    from .sharding import decoder_layers
+
+    layers = [m for m in decoder_layers(model) if hasattr(m, "gradient_checkpointing")]
+    kept = layers[len(layers) - min(keep, len(layers)):]
+    for m in kept:
+        m.gradient_checkpointing = False
+    return len(kept)
 
 
 @contextlib.contextmanager

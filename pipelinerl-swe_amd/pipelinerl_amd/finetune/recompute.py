@@ -9,8 +9,14 @@ recomputing them only costs time.  The results are the same either way (the reco
 forward is the same deterministic kernels on the same inputs).
 
 ``finetune.gradient_checkpointing_policy`` (build-only key):
-  ``auto`` (default)  checkpoint only when the estimate below does not fit the device
+  ``auto`` (default)  keep every layer's activations when the estimate below fits the device;
+                      else recompute only as many decoder layers as needed: the last K layers keep
+                      their activations (K the largest that fits, from the same estimate with a
+                      recomputed layer holding only its input hidden state, plus one layer's
+                      activations while it is recomputed), the others recompute — every layer
+                      when K = 0.  The results are the same for every K.
   ``always``          the reference's behaviour: checkpoint whenever gradient_checkpointing is set
+``finetune.gradient_checkpointing_keep_layers`` (build-only, optional int): K itself (A/B runs).
 
 The estimate is deliberately conservative (upper bounds, measured against the trainer probes'
 peak memory in DESIGN.md): model state = parameters x (weight + gradient + two AdamW moments),
@@ -56,12 +62,13 @@ class RecomputePlan:
     buffer_bytes: int = 0
     device_bytes: int = 0
     need_bytes: int = 0  # the terms after the allocator's rounding, plus the headroom
+    keep_layers: int = -1  # checkpoint: the last keep_layers decoder layers keep their activations
 
     def as_dict(self) -> dict:
         return {"checkpoint": self.checkpoint, "reason": self.reason, "state_gb": round(self.state_bytes / 1e9, 2),
                 "activation_gb": round(self.activation_bytes / 1e9, 2), "logits_gb": round(self.logits_bytes / 1e9, 2),
                 "buffer_gb": round(self.buffer_bytes / 1e9, 2), "device_gb": round(self.device_bytes / 1e9, 2),
-                "need_gb": round(self.need_bytes / 1e9, 2)}
+                "need_gb": round(self.need_bytes / 1e9, 2), "keep_layers": self.keep_layers}
 
 
 def activation_bytes_per_token(config, dtype_bytes: int = 2) -> int:
@@ -141,19 +148,22 @@ def plan_gradient_checkpointing(args, model, device: torch.device, shard_world: 
     policy = str(args.get("gradient_checkpointing_policy", "auto"))
     if policy not in ("auto", "always"):
         raise ValueError(f"gradient_checkpointing_policy must be 'auto' or 'always', got {policy!r}")
-    if policy == "always":
-        return RecomputePlan(True, "policy always (the reference's behaviour)")
+    forced = args.get("gradient_checkpointing_keep_layers", None)
+    if policy == "always" and forced is None:
+        return RecomputePlan(True, "policy always (the reference's behaviour)", keep_layers=0)
     if device_bytes is None and device.type != "cuda":
-        return RecomputePlan(True, "not a HIP device: the reference's behaviour")
+        return RecomputePlan(True, "not a HIP device: the reference's behaviour", keep_layers=0)
     seq = args.get("seq_length")
     config = getattr(model, "config", None)
     if not seq or config is None or not hasattr(config, "hidden_size") or not hasattr(config, "num_hidden_layers"):
-        return RecomputePlan(True, "no seq_length / decoder shape to size the activations: the reference's behaviour")
+        return RecomputePlan(True, "no seq_length / decoder shape to size the activations: the reference's behaviour",
+                             keep_layers=0)
     total = int(device_bytes) if device_bytes is not None else int(torch.cuda.get_device_properties(device).total_memory)
     params = list(model.parameters())
     n = sum(p.numel() for p in params)
     pbytes = params[0].element_size() if params else 2
     sw = max(1, int(shard_world))
+    L = int(config.num_hidden_layers)
     # weight + gradient + exp_avg + exp_avg_sq, all in the parameter dtype (torch / PrlAdamW)
     state = 4 * n * pbytes // sw
     act = int(ACT_ALLOWANCE * int(seq) * activation_bytes_per_token(config, pbytes))
@@ -162,8 +172,6 @@ def plan_gradient_checkpointing(args, model, device: torch.device, shard_world: 
     chunk = min(int(seq), int(rl.get("lm_head_chunk_rows", 65536) or 65536))  # RLConfig default
     logits = chunk * vocab * pbytes
     head = 0 if getattr(config, "tie_word_embeddings", False) else vocab * int(config.hidden_size) * pbytes
-    buffers = build_buffer_bytes(config, int(seq), chunk, int(shard_world), pbytes) + \
-        fsdp_transient_bytes(model, int(shard_world), act, logits, head)
     # the device allocator's size rounding (devalloc.py) at the largest shapes of the micro-batch
     # (rounding is monotonic: shorter micro-batches round to no more)
     from ..devalloc import round_size, rounded_factor
@@ -176,9 +184,32 @@ def plan_gradient_checkpointing(args, model, device: torch.device, shard_world: 
     f_logits = rounded_factor(logits) if logits else 1.0
     sizes = [p.numel() * pbytes // sw for p in params]
     f_state = (sum(round_size(b) for b in sizes if b) / max(1, sum(sizes))) if sizes else 1.0
-    need = int(state * f_state + act * f_act + logits * f_logits + buffers * max(f_state, f_act, f_logits)) + \
-        int(HEADROOM_FRAC * total) + HEADROOM_BYTES
-    keep = need <= total
-    plan = RecomputePlan(not keep, ("activations fit: no recompute" if keep else "activations do not fit: recompute"),
-                         state, act, logits, buffers, total, need)
-    return plan
+    act_layer = act // max(1, L)
+    saved_input = round_size(int(seq) * H * pbytes)  # what a recomputed layer keeps: its input
+
+    def need_for(keep: int) -> tuple[int, int, int]:
+        """(bytes compared with the device, activation bytes, buffer bytes) when the last ``keep``
+        layers keep their activations and the others recompute."""
+        a = act if keep >= L else keep * act_layer + act_layer  # + the layer being recomputed
+        a_bytes = int(a * f_act) + (0 if keep >= L else (L - keep) * saved_input)
+        buffers = build_buffer_bytes(config, int(seq), chunk, int(shard_world), pbytes) + \
+            fsdp_transient_bytes(model, int(shard_world), a, logits, head)
+        need = int(state * f_state) + a_bytes + int(logits * f_logits) + \
+            int(buffers * max(f_state, f_act, f_logits)) + int(HEADROOM_FRAC * total) + HEADROOM_BYTES
+        return need, a_bytes, buffers
+
+    if forced is not None:
+        keep = max(0, min(int(forced), L))
+        need, _, buffers = need_for(keep)
+        return RecomputePlan(keep < L, f"keep_layers {keep} of {L} (finetune.gradient_checkpointing_keep_layers)",
+                             state, act, logits, buffers, total, need, keep if keep < L else -1)
+    need, _, buffers = need_for(L)
+    if need <= total:
+        return RecomputePlan(False, "activations fit: no recompute", state, act, logits, buffers, total, need)
+    keep = L - 1
+    while keep > 0 and need_for(keep)[0] > total:
+        keep -= 1
+    need_k, _, buffers_k = need_for(keep)
+    reason = (f"activations of the last {keep} of {L} layers fit: {L - keep} recompute" if keep > 0
+              else "activations do not fit: recompute")
+    return RecomputePlan(True, reason, state, act, logits, buffers_k, total, need_k, keep)

@@ -33,7 +33,9 @@ QWEN = {  # published Qwen2.5 shapes (config.json of each checkpoint)
 
 
 def qwen2_model(name: str, device: torch.device, grad_ckpt: bool = False, fused_ops: bool = True,
-                layers: int | None = None):
+                layers: int | None = None, keep_layers: int = 0):
+    """``grad_ckpt``: HF gradient checkpointing, except the last ``keep_layers`` decoder layers
+    (finetune/checkpoints.keep_activations, the plan's partial recompute)."""
     from transformers import AutoModelForCausalLM, Qwen2Config
 
     from .finetune.attention import register
@@ -48,7 +50,10 @@ def qwen2_model(name: str, device: torch.device, grad_ckpt: bool = False, fused_
 
         patch_model(model)
     if grad_ckpt:
+        from .finetune.checkpoints import keep_activations
+
         model.gradient_checkpointing_enable(gradient_checkpointing_kwargs={"use_reentrant": False})
+        keep_activations(model, keep_layers)
     model.train()
     return model
 
@@ -106,7 +111,8 @@ class TrainerStep:
                  micro_batches: int = 4, device=None, fused_head: bool = True, grad_ckpt: bool = False,
                  fused_ops: bool = True, group=None, model=None, step_fn=None, vocab: int | None = None,
                  fsdp: bool = False, kl_coef: float = 0.0, layers: int | None = None, batches: list | None = None,
-                 samples_per_step: int | None = None, local: bool = False, flat_params: bool = True):
+                 samples_per_step: int | None = None, local: bool = False, flat_params: bool = True,
+                 keep_layers: int = 0):
         """``batches``: the packed micro-batches to train on (host PipelineBatchEncodings, e.g. from
         workloads.micro_batches), ``samples_per_step`` their global sample count (RLConfig.batch_size);
         default: ``micro_batches`` synthetic batches of ``tokens`` tokens.  ``local``: no gradient
@@ -120,7 +126,8 @@ class TrainerStep:
         world = dist.get_world_size(group) if dist.is_initialized() else 1
         rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.world, self.tokens, self.micro_batches = world, tokens, micro_batches
-        self.model = model if model is not None else qwen2_model(name, self.device, grad_ckpt, fused_ops, layers)
+        self.model = model if model is not None else qwen2_model(name, self.device, grad_ckpt, fused_ops, layers,
+                                                                 keep_layers)
         self.fsdp = fsdp
         if fsdp:  # FSDP2 over the default group (finetune/sharding.py): it reduce-scatters the grads
             if group is not None:
@@ -397,7 +404,8 @@ def snapshot_overlap(ts: "TrainerStep", t_ref: float, steps: int, warmup: int, f
 
 def dp_step_probe(config: str = "c3", micro_batches: int = 4, steps: int = 2, warmup: int = 1, device=None,
                   samples_per_step: int = 4096, layers: int | None = None, batches: list | None = None,
-                  model=None, step_fn=None, snapshot: bool = False) -> dict:
+                  model=None, step_fn=None, snapshot: bool = False, grad_ckpt: bool = False,
+                  keep_layers: int = 0) -> dict:
     """BASELINE.json configs[2] (C3) data-parallel trainer step on this rank's GPU: the config's
     model shapes (Qwen2.5-7B), ``micro_batches`` packed micro-batches per rank from the config's
     rollout distribution (workloads.py: prompt U{64..512} + completion U{256..8192}, packing cap
@@ -430,7 +438,8 @@ def dp_step_probe(config: str = "c3", micro_batches: int = 4, steps: int = 2, wa
     if on_gpu:
         torch.cuda.reset_peak_memory_stats(device)
     ts = TrainerStep(spec.model, device=device, fused_head=True, kl_coef=spec.kl_coef, layers=layers,
-                     batches=batches, samples_per_step=samples_per_step, local=True, model=model, step_fn=step_fn)
+                     batches=batches, samples_per_step=samples_per_step, local=True, model=model, step_fn=step_fn,
+                     grad_ckpt=grad_ckpt, keep_layers=keep_layers)
     t_local = ts.timed(steps, warmup)
     t_tail = ts.optimizer_tail()
     t_dp, t_ar = t_local, 0.0

@@ -167,3 +167,61 @@ def test_round_size_follows_the_allocator():
     assert devalloc.round_size(2 ** 27, S) == 2 ** 27  # powers of two are kept
     assert devalloc.round_size(1000, S) == 1024 and devalloc.round_size(100, S) == 512
     assert devalloc.round_size(300 * 10 ** 6, "") == -(-300 * 10 ** 6 // 512) * 512  # no rounding configured
+
+
+def test_partial_recompute_keeps_the_layers_that_fit(monkeypatch):
+    """C5 on 4 trainer ranks (32B, 12 000 tokens) does not fit whole: instead of recomputing all 64
+    layers the plan keeps the activations of the largest K that fits — need(K) <= device <
+    need(K + 1) — and finetune.gradient_checkpointing_keep_layers sets K directly."""
+    from pipelinerl_amd import devalloc
+    from pipelinerl_amd.finetune.recompute import plan_gradient_checkpointing
+
+    for k in devalloc.ENV_KEYS:
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setattr(devalloc, "_applied", devalloc.DEFAULT_SETTINGS)
+    m32 = _meta_model("32b")
+    cuda, dev = torch.device("cuda"), 288 * 2 ** 30
+    p = plan_gradient_checkpointing(_args(), m32, cuda, shard_world=4, device_bytes=dev)
+    assert p.checkpoint and 0 < p.keep_layers < 64, p.as_dict()
+    assert p.need_bytes <= dev
+    nxt = plan_gradient_checkpointing(_args(gradient_checkpointing_keep_layers=p.keep_layers + 1), m32, cuda,
+                                      shard_world=4, device_bytes=dev)
+    assert nxt.need_bytes > dev and nxt.keep_layers == p.keep_layers + 1
+    # fewer kept layers need less; keeping all 64 is the no-recompute plan
+    lo = plan_gradient_checkpointing(_args(gradient_checkpointing_keep_layers=0), m32, cuda, shard_world=4,
+                                     device_bytes=dev)
+    assert lo.checkpoint and lo.keep_layers == 0 and lo.need_bytes < p.need_bytes
+    allk = plan_gradient_checkpointing(_args(gradient_checkpointing_keep_layers=64), m32, cuda, shard_world=4,
+                                       device_bytes=dev)
+    assert not allk.checkpoint
+    # "always" is the reference's behaviour: every layer recomputes
+    assert plan_gradient_checkpointing(_args(gradient_checkpointing_policy="always"), m32, cuda,
+                                       device_bytes=dev).keep_layers == 0
+
+
+def test_keep_activations_flags_the_last_layers_and_gradients_are_unchanged():
+    """checkpoints.keep_activations after HF's gradient_checkpointing_enable: the last K decoder
+    layers stop recomputing; the gradients of a tiny fp32 Qwen2 on CPU are bit-identical for
+    every K (the recomputed forward is the same computation)."""
+    from transformers import AutoModelForCausalLM, Qwen2Config
+
+    from pipelinerl_amd.finetune.checkpoints import keep_activations
+
+    cfg = Qwen2Config(vocab_size=64, hidden_size=32, intermediate_size=64, num_hidden_layers=4,
+                      num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=64)
+    ids = torch.randint(0, 64, (1, 24), generator=torch.Generator().manual_seed(0))
+    grads = {}
+    for keep in (None, 0, 2, 4):
+        torch.manual_seed(0)
+        m = AutoModelForCausalLM.from_config(cfg, dtype=torch.float32)
+        m.train()
+        if keep is not None:
+            m.gradient_checkpointing_enable(gradient_checkpointing_kwargs={"use_reentrant": False})
+            assert keep_activations(m, keep) == keep
+            flags = [layer.gradient_checkpointing for layer in m.model.layers]
+            assert flags == [True] * (4 - keep) + [False] * keep
+        m(input_ids=ids, labels=ids).loss.backward()
+        grads[keep] = {n: p.grad.clone() for n, p in m.named_parameters()}
+    for keep in (0, 2, 4):
+        for n, g in grads[None].items():
+            assert torch.equal(g, grads[keep][n]), (keep, n)

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--layers", type=int, default=None)
     ap.add_argument("--snapshot", action="store_true")
+    ap.add_argument("--grad-ckpt", action="store_true", help="gradient checkpointing (the reference config's)")
+    ap.add_argument("--keep-layers", type=int, default=0, help="with --grad-ckpt: the last K layers keep activations")
     a = ap.parse_args()
     import gc
     import time
@@ -65,7 +67,9 @@ def main():
     torch.cuda.set_device(0)
 
     r = dp_step_probe(a.config, micro_batches=a.micro_batches, steps=a.steps, warmup=a.warmup,
-                      device=torch.device("cuda", 0), layers=a.layers, snapshot=a.snapshot)
+                      device=torch.device("cuda", 0), layers=a.layers, snapshot=a.snapshot, grad_ckpt=a.grad_ckpt,
+                      keep_layers=a.keep_layers)
+    r["grad_ckpt"], r["keep_layers"] = a.grad_ckpt, a.keep_layers
     r["host_gc"] = {f"gen{g}": {"n": n, "ms": round(ms, 1)} for g, (n, ms) in gcs.items()}
     print(json.dumps(r), flush=True)
 
