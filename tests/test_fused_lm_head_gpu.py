@@ -155,3 +155,22 @@ def test_rl_step_fused_lm_head_matches_full_logits(tmp_path):
     for (n, p), (_, q) in zip(model.named_parameters(), twin.named_parameters()):
         err = float((p.grad - q.grad).abs().max())
         assert err <= 1e-6 + 1e-3 * float(q.grad.abs().max()), (n, err)
+
+
+def test_fp32_label_rows_at_qwen_vocab():
+    """An fp32 model's label-row chunks at V = 151 936 run the part-resident fp32 kernel through
+    the row map (prl_grpo_forward_rows): loss, dh and dW against the oracle composed with the
+    lm_head, at the fp32 bar."""
+    V, Hd = 151936, 64
+    lens, prompts = [13, 17], [4, 6]
+    b = _batch(lens, prompts, V, seed=5)
+    g = torch.Generator().manual_seed(5)
+    h = (torch.randn((1, sum(lens), Hd), generator=g) * 0.5).to(DEV)
+    w = (torch.randn((V, Hd), generator=g) * 0.5).to(DEV)
+    loss, stats, rows, dh, dw = _run_fused(h, w, b, CFG, 4096)
+    o, dh_o, dw_o = _oracle(h, w, b, CFG)
+    assert abs(loss - o["loss"]) <= 1e-4 * max(1.0, abs(o["loss"]))
+    ok, err = rel_close(dh.cpu().numpy()[0], dh_o, 1e-4, 1e-5 * float(np.abs(dh_o).max()))
+    assert ok, err
+    ok, err = rel_close(dw.cpu().numpy(), dw_o, 1e-4, 1e-5 * float(np.abs(dw_o).max()))
+    assert ok, err

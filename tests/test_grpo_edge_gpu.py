@@ -200,3 +200,76 @@ def test_target_columns_at_vector_edges(ent):
     for r in rows:
         got, want = d[0, r, cols[r]], o["dlogits"][0, r, cols[r]]
         assert abs(got - want) <= 1e-2 * abs(want) + 1e-8, (r, cols[r], got, want)
+
+
+# fp32 logits at a Qwen2.5 vocabulary take the part-resident kernel (grpo_fwd_hybrid_f32<19, 9>):
+# columns [0, 77 824) in registers, [77 824, 114 688) in LDS, the rest streamed and re-read
+HYB_EDGES = [0, 3, 4, 77823, 77824, 77827, 114687, 114688, 114691, 151935]
+
+
+@pytest.mark.parametrize("ent", [0.0, 0.01])
+def test_fp32_part_resident_targets_at_region_edges(ent):
+    """Targets on both sides of the register / LDS / streamed boundaries, fp32 at 1e-4."""
+    T, V = 12, 151936
+    b = _batch(T, V, seed=11, lens=[T], prompts=[1])
+    for r, col in enumerate(HYB_EDGES):
+        b["input_ids"][0, 1 + r] = col
+        if b["labels"][0, 1 + r] != -100:
+            b["labels"][0, 1 + r] = col
+    lg = np.random.default_rng(11).normal(0, 2, (1, T, V)).astype(np.float32)
+    cfg = dict(CFG, entropy_bonus=ent, final_entropy_bonus=ent)
+    _, d = _cmp(lg, b, cfg, dtype=torch.float32)
+    o = grpo_oracle.rl_step_oracle(lg, b, cfg, 0, 10)
+    for r, col in enumerate(HYB_EDGES):
+        if b["labels"][0, 1 + r] != -100:
+            assert rel_close(d[0, r, col], o["dlogits"][0, r, col], 1e-4, 1e-7)[0], col
+
+
+def test_fp32_part_resident_many_rows_per_workgroup_and_non_finite():
+    """~2.3 rows per workgroup (rows with and without a successor on the same CU, the LDS slab
+    reused row after row), a -inf in the streamed tail and one in the LDS share of two rows; two
+    runs bitwise identical."""
+    V = 151936
+    lens = [150, 200, 251]
+    T = sum(lens)
+    b = _batch(T, V, seed=12, lens=lens, prompts=[20, 30, 40])
+    lg = np.random.default_rng(12).normal(0, 2.5, (1, T, V)).astype(np.float32)
+    tgt = b["input_ids"][0, 1:]
+    for r, col in ((40, 140000), (41, 90000)):
+        lg[0, r, col if col != tgt[r] else col + 1] = -np.inf
+    loss, stats, d1 = _run(lg, b, dtype=torch.float32)
+    o = grpo_oracle.rl_step_oracle(lg, b, CFG, 0, 10)
+    assert stats["num_nans"] == o["stats"]["num_nans"] >= 2
+    assert abs(loss - o["loss"]) <= 1e-4 * max(1, abs(o["loss"]))
+    other = [r for r in range(T - 1) if r not in (40, 41)]
+    ok, err = rel_close(d1[0, other], o["dlogits"][0, other], 1e-4, 1e-7)
+    assert ok, err
+    assert np.all(d1[0, [40, 41]] == 0)
+    _, _, d2 = _run(lg, b, dtype=torch.float32)
+    assert np.array_equal(d1, d2)
+
+
+def test_fp32_part_resident_strided_rows():
+    """fp32 logits sliced out of a wider buffer (row stride V + 64) at a Qwen2.5 vocabulary."""
+    from pipelinerl_amd.finetune.rl import RLConfig, rl_step
+
+    T, V, W = 9, 151936, 151936 + 64
+    b = _batch(T, V, seed=13)
+    full = np.random.default_rng(13).normal(0, 2, (1, T, W)).astype(np.float32)
+    base = torch.tensor(full).to(DEV).requires_grad_(True)
+    view = base[:, :, :V]
+    assert view.stride(1) == W
+
+    class M(torch.nn.Module):
+        def forward(self, **kw):
+            import types
+            return types.SimpleNamespace(logits=view)
+
+    loss, stats = rl_step(M(), to_batch(b), 0, 10, RLConfig(**CFG))
+    loss.backward()
+    o = grpo_oracle.rl_step_oracle(full[:, :, :V], b, CFG, 0, 10)
+    for k, v in o["stats"].items():
+        assert abs(stats[k] - v) <= 1e-4 * max(1.0, abs(v)), k
+    g = base.grad.cpu().numpy()
+    assert rel_close(g[:, :, :V], o["dlogits"], 1e-4, 1e-7)[0]
+    assert np.all(g[:, :, V:] == 0)
