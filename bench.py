@@ -43,7 +43,9 @@ optimizer step, and with the in-place (zero-copy, default) snapshot, in rotating
 copy's own duration.  At N > 1, "communicators" first checks that every communicator reports (and
 carries, by an all-reduce of ones) the intended rank count: the DP group, the CPU control group and a
 prl_comm RCCL communicator (ncclCommCount); the split pipeline's DP and actor groups are checked in
-its own probe ("split_pipeline.groups").
+its own probe ("split_pipeline.groups").  At N = 1, "loss_head_fp32": the same C2 micro-batch with
+fp32 logits (Accelerate's upcast regime; the part-resident grpo_fwd_hybrid_f32), its kernel time
+and fraction of the HBM peak on 2 x 4 x T x V algorithmic bytes.
 
 Prints ONE JSON line (rank 0).  roofline.achieved = algorithmic bytes per launch
 (T*V*2 read + T*V*2 dlogits write + 37*T side data) / the average duration
@@ -71,6 +73,40 @@ import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md); measured float4 copy 6290 GB/s
 SIDE_BYTES_PER_TOKEN = 37  # ids 8 + old 4 + ref 4 + adv 4 + w 4 + mask 1 + lp/H/tok_loss 12
+
+
+def fp32_loss_head_probe(T: int, V: int, device, iters: int = 8, warmup: int = 2) -> dict:
+    """C2's micro-batch with fp32 logits (Accelerate's mixed precision upcasts them,
+    finetune_loop.py:381-385): the fused loss head's forward + gradient (the part-resident
+    grpo_fwd_hybrid_f32 at Qwen2.5 vocabularies), HIP events on its stream; algorithmic bytes =
+    logits read once + dlogits written once + side data."""
+    from pipelinerl_amd.finetune.rl.fused import GrpoParams, grpo_loss
+
+    lb, fields = make_workload(T, V, seq=2048, prompt=256, seed=4321, device=device)
+    logits = lb.detach().float().requires_grad_(True)
+    del lb
+    torch.cuda.empty_cache()
+    params = GrpoParams(policy_loss="ppo", epsilon=4.0, kl_coef=0.0, entropy_coef=0.0, clamp_log_ratio=5.0,
+                        temperature=1.0, batch_size=4096.0)
+    times = []
+    for i in range(warmup + iters):
+        logits.grad = None
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        loss, stats, _ = grpo_loss(logits, fields, params)
+        e1.record()
+        loss.backward()
+        stats.cpu()
+        if i >= warmup:
+            times.append(e0.elapsed_time(e1))
+    ms = float(np.median(times))
+    alg = 2.0 * T * V * 4 + SIDE_BYTES_PER_TOKEN * T
+    del logits, fields
+    torch.cuda.empty_cache()
+    return {"kernel": "grpo_fwd_hybrid_f32<19, 9> (+stats/finalize) per prl_grpo_forward", "tokens": T, "vocab": V,
+            "logits_dtype": "fp32", "kernel_ms": round(ms, 4), "algorithmic_bytes": alg,
+            "achieved_GBps": round(alg / ms / 1e6, 1), "frac": round(alg / ms / 1e6 / HBM_PEAK_GBS, 4),
+            "tokens_per_s": round(T / ms * 1e3, 1), "iters": iters}
 
 
 def make_workload(T: int, V: int, seq: int, prompt: int, seed: int, device):
@@ -352,6 +388,7 @@ def main():
     ap.add_argument("--no-trainer-step", action="store_true", help="skip the full trainer-step probe")
     ap.add_argument("--no-c3", action="store_true", help="skip the configs[2] 7B DP trainer-step probe")
     ap.add_argument("--no-fsdp", action="store_true", help="N >= 4: skip the configs[4] FSDP 32B probe")
+    ap.add_argument("--no-fp32", action="store_true", help="N = 1: skip the fp32-logits loss-head probe")
     ap.add_argument("--no-split-pipeline", action="store_true",
                     help="N > 1: skip the split trainer/actor probe (configs[3]: 7B, overlapped weight broadcast)")
     args = ap.parse_args()
@@ -460,6 +497,10 @@ def main():
         trainer = optional("trainer_step", lambda: trainer_step_probe("1.5b", tokens=T, micro_batches=2, steps=2,
                                                                       warmup=1, device=dev, fused_head=True,
                                                                       layers=4 if rehearse else None))
+    fp32 = None
+    if world == 1 and not args.no_fp32:
+        # the loss head in the fp32-logits regime (Accelerate's upcast): the part-resident kernel
+        fp32 = optional("loss_head_fp32", lambda: fp32_loss_head_probe(T, V, dev))
     fsdp = None
     if world >= 4 and not args.no_fsdp:
         # configs[4] (C5): Qwen2.5-32B shapes, FSDP2 over every rank, KL-to-reference on
@@ -552,7 +593,8 @@ def main():
             # the trainer-side half of "weight broadcast fully overlapped": C3's 7B step with and
             # without WeightUpdateManager's snapshot in flight on its side stream
             out["snapshot_overlap"] = dict(c3.pop("snapshot_overlap"), step="c3_dp (Qwen2.5-7B, 4 micro-batches)")
-        for key, res in (("communicators", census), ("c3_dp", c3), ("trainer_step", trainer), ("fsdp_32b", fsdp),
+        for key, res in (("communicators", census), ("c3_dp", c3), ("trainer_step", trainer),
+                         ("loss_head_fp32", fp32), ("fsdp_32b", fsdp),
                          ("split_pipeline", split), ("exchange", comm)):
             if res is not None:
                 out[key] = res
