@@ -103,9 +103,18 @@ def fp32_loss_head_probe(T: int, V: int, device, iters: int = 8, warmup: int = 2
     alg = 2.0 * T * V * 4 + SIDE_BYTES_PER_TOKEN * T
     del logits, fields
     torch.cuda.empty_cache()
+    traffic = None  # HBM bytes per launch from the committed PMC passes (tools/profile_bench.sh)
+    try:
+        pmc = json.loads((ROOT / "profiles" / "r04_fp32_pmc.json").read_text())["per_launch_median"]
+        hyb = next(v for k, v in pmc.items() if "hybrid" in k)
+        if T == 65536 and V == 151936:
+            traffic = hyb["fetch_size_bytes"] + hyb["write_size_bytes"]
+    except (OSError, KeyError, StopIteration, ValueError):
+        pass
     return {"kernel": "grpo_fwd_hybrid_f32<19, 9> (+stats/finalize) per prl_grpo_forward", "tokens": T, "vocab": V,
             "logits_dtype": "fp32", "kernel_ms": round(ms, 4), "algorithmic_bytes": alg,
             "achieved_GBps": round(alg / ms / 1e6, 1), "frac": round(alg / ms / 1e6 / HBM_PEAK_GBS, 4),
+            "traffic": traffic, "traffic_source": "r04_fp32_pmc.json" if traffic else None,
             "tokens_per_s": round(T / ms * 1e3, 1), "iters": iters}
 
 

@@ -1,6 +1,8 @@
 # The bench's rocprofv3 evidence: kernel stats of the loss-head bench, then FETCH_SIZE and
 # WRITE_SIZE in separate PMC passes (never combined with tracing; each pass under its own limit).
 # Outputs (small CSVs only) under gpurun_out/prof_bench, gpurun_out/pmc_fetch, gpurun_out/pmc_write.
+# The bench's N = 1 loss_head_fp32 probe runs in every pass: the part-resident fp32 kernel is
+# profiled and counted beside the bf16 one.
 set -u
 export TMPDIR=/tmp
 B="bench.py --steps 47 --warmup 3 --no-cpu-baseline --no-trainer-step --no-c3"
