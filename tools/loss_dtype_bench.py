@@ -30,9 +30,13 @@ def main():
     ap.add_argument("--tokens", type=int, default=65536)
     ap.add_argument("--vocab", type=int, default=151936)
     ap.add_argument("--inplace", action="store_true", help="separate vs aliased dlogits A/B (bf16)")
+    ap.add_argument("--dl-offsets", default=None,
+                    help="comma-separated byte offsets of the dlogits buffer's start (bf16 A/B of HBM placement)")
     a = ap.parse_args()
     if a.inplace:
         return inplace_ab(a)
+    if a.dl_offsets:
+        return offsets_ab(a, [int(x) for x in a.dl_offsets.split(",")])
     from pipelinerl_amd.finetune.rl.fused import GrpoParams, grpo_loss
 
     dev = torch.device("cuda", 0)
@@ -114,6 +118,60 @@ def inplace_ab(a, rounds: int = 5, iters: int = 10):
         out[arm] = {"ms": round(ms, 4), "rounds_ms": [round(t, 4) for t in v], "frac": round(gb / ms / 1e6 / 8000.0, 4)}
     print(json.dumps(out), flush=True)
 
+
+def offsets_ab(a, offsets: list[int], rounds: int = 3, iters: int = 10):
+    """The bf16 loss head writing dlogits into one spare buffer at several byte offsets of its start
+    (16-B aligned): does the placement of the write stream relative to the read stream (HBM
+    channels / banks) change the rate?  Alternating rounds; the outputs must be bit-identical."""
+    from pipelinerl_amd import _native
+    from pipelinerl_amd.finetune.rl.fused import GrpoParams, _c_batch, _workspace
+
+    dev = torch.device("cuda", 0)
+    lib = _native.load()
+    params = GrpoParams(policy_loss="ppo", epsilon=4.0, kl_coef=0.0, entropy_coef=0.0, clamp_log_ratio=5.0,
+                        temperature=1.0, batch_size=4096.0)
+    logits, fields = bench.make_workload(a.tokens, a.vocab, 2048, 256, 1234, dev)
+    x = logits.detach()
+    nbytes = x.numel() * x.element_size()
+    spare = torch.empty(nbytes + max(offsets) + 16, dtype=torch.uint8, device=dev)
+    B, L, V = x.shape
+    rows = torch.empty((8, B * (L - 1)), dtype=torch.float32, device=dev)
+    stats = torch.empty(_native.NSTAT, dtype=torch.float64, device=dev)
+    ws = _workspace(dev)
+    cp = params.to_c(True)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    assert all(o % 16 == 0 for o in offsets)
+
+    def launch(off: int) -> float:
+        cb = _c_batch(x, fields, None)
+        co = _native.PrlGrpoOutputs(*[rows[i].data_ptr() for i in range(8)], None, spare.data_ptr() + off,
+                                    stats.data_ptr())
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        _native.check(lib.prl_grpo_forward(ctypes.byref(cb), ctypes.byref(cp), ctypes.byref(co), ws.data_ptr(),
+                                           ws.numel(), stream), "prl_grpo_forward")
+        e1.record()
+        e1.synchronize()
+        return e0.elapsed_time(e1)
+
+    launch(offsets[0])
+    ref = spare[offsets[0]:offsets[0] + nbytes].clone()
+    same = True
+    for o in offsets[1:]:
+        launch(o)
+        same &= bool(torch.equal(spare[o:o + nbytes], ref))
+    del ref
+    times = {o: [] for o in offsets}
+    for r in range(rounds):
+        for o in (offsets if r % 2 == 0 else offsets[::-1]):
+            times[o].append(float(np.median([launch(o) for _ in range(iters)])))
+    gb = 2.0 * nbytes + 37.0 * a.tokens
+    out = {"tool": "loss_dl_offsets_ab", "tokens": a.tokens, "vocab": a.vocab, "bit_identical": same,
+           "base_mod_2MiB": spare.data_ptr() % (2 << 20), "logits_mod_2MiB": x.data_ptr() % (2 << 20)}
+    for o, v in times.items():
+        ms = float(np.median(v))
+        out[str(o)] = {"ms": round(ms, 4), "rounds_ms": [round(t, 4) for t in v], "frac": round(gb / ms / 1e6 / 8000.0, 4)}
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":
