@@ -26,7 +26,7 @@ v, the attention output, the residual stream, gate, up and the SwiGLU output), t
 ``seq_length`` tokens, times the layers, times a 1.25 allowance for backward temporaries; one
 label-row logits chunk; the build's own long-lived buffers (the fused gate/up weight cache,
 2 I x H per layer when finetune/model_ops.py fuses the projection at this micro-batch size and the
-model is not FSDP-sharded; the lm_head weight gradient's staging, [V, H] bf16 from the single-chunk
+model is neither FSDP-sharded nor flat-homed — with flat parameters the fused weight is a view; the lm_head weight gradient's staging, [V, H] bf16 from the single-chunk
 GEMM or an fp32 accumulator over several chunks, finetune/rl/fused_linear.py); under FSDP, the
 larger of its two unsharded working sets (fsdp_transient_bytes: the start of the backward with the
 logits' gradient, the root unit gathered, the lm_head's unsharded gradient and two decoder layers;
@@ -86,8 +86,11 @@ def activation_bytes_per_token(config, dtype_bytes: int = 2) -> int:
     return per_layer * layers * dtype_bytes
 
 
-def build_buffer_bytes(config, seq: int, chunk: int, shard_world: int, dtype_bytes: int = 2) -> int:
-    """Long-lived buffers of the build's fused paths at this micro-batch size (upper bound)."""
+def build_buffer_bytes(config, seq: int, chunk: int, shard_world: int, dtype_bytes: int = 2,
+                       flat_params: bool = False) -> int:
+    """Long-lived buffers of the build's fused paths at this micro-batch size (upper bound).
+    ``flat_params``: the parameters live in one flat buffer (finetune.flat_parameters), so the fused
+    gate / up weight is a view of it, not a cached concatenation."""
     from . import model_ops
 
     H = int(config.hidden_size)
@@ -95,7 +98,7 @@ def build_buffer_bytes(config, seq: int, chunk: int, shard_world: int, dtype_byt
     layers = int(config.num_hidden_layers)
     vocab = int(getattr(config, "vocab_size", 0))
     out = 0
-    if shard_world <= 1 and model_ops._FUSED_GATE_UP and seq <= model_ops._FUSED_GATE_UP_MAX_ROWS:
+    if shard_world <= 1 and model_ops._FUSED_GATE_UP and seq <= model_ops._FUSED_GATE_UP_MAX_ROWS and not flat_params:
         out += 2 * inter * H * layers * dtype_bytes  # cat(Wg, Wu) per layer (_fused_weight)
     if shard_world <= 1 and getattr(model_ops, "_FUSED_QKV", False):
         heads = int(getattr(config, "num_attention_heads", 1))
@@ -185,6 +188,8 @@ def plan_gradient_checkpointing(args, model, device: torch.device, shard_world: 
     sizes = [p.numel() * pbytes // sw for p in params]
     f_state = (sum(round_size(b) for b in sizes if b) / max(1, sum(sizes))) if sizes else 1.0
     act_layer = act // max(1, L)
+    # the loop re-homes a non-FSDP bf16 model into one flat buffer (finetune_loop.py, flat_parameters)
+    flat = sw <= 1 and pbytes == 2 and bool(args.get("flat_parameters", True))
     saved_input = round_size(int(seq) * H * pbytes)  # what a recomputed layer keeps: its input
 
     def need_for(keep: int) -> tuple[int, int, int]:
@@ -192,7 +197,7 @@ def plan_gradient_checkpointing(args, model, device: torch.device, shard_world: 
         layers keep their activations and the others recompute."""
         a = act if keep >= L else keep * act_layer + act_layer  # + the layer being recomputed
         a_bytes = int(a * f_act) + (0 if keep >= L else (L - keep) * saved_input)
-        buffers = build_buffer_bytes(config, int(seq), chunk, int(shard_world), pbytes) + \
+        buffers = build_buffer_bytes(config, int(seq), chunk, int(shard_world), pbytes, flat) + \
             fsdp_transient_bytes(model, int(shard_world), a, logits, head)
         need = int(state * f_state) + a_bytes + int(logits * f_logits) + \
             int(buffers * max(f_state, f_act, f_logits)) + int(HEADROOM_FRAC * total) + HEADROOM_BYTES

@@ -98,22 +98,26 @@ def test_build_buffers_are_counted(m7b, monkeypatch):
 
     cuda = torch.device("cuda")
     monkeypatch.setattr(model_ops, "_FUSED_GATE_UP", True)
-    p = plan_gradient_checkpointing(_args(), m7b, cuda, device_bytes=288 * GB)
+    nf = dict(flat_parameters=False)  # the cache exists only without flat parameter storage
+    p = plan_gradient_checkpointing(_args(**nf), m7b, cuda, device_bytes=288 * GB)
     cache = 2 * 18944 * 3584 * 28 * 2
     assert p.buffer_bytes == cache + 152064 * 3584 * 2, p.as_dict()
+    # flat parameters (the loop's default): the fused weight is a view, no cache
+    assert plan_gradient_checkpointing(_args(), m7b, cuda, device_bytes=288 * GB).buffer_bytes == 152064 * 3584 * 2
     # several lm_head chunks: an fp32 accumulator
-    p2 = plan_gradient_checkpointing(_args(rl={"lm_head_chunk_rows": 4096}), m7b, cuda, device_bytes=288 * GB)
+    p2 = plan_gradient_checkpointing(_args(rl={"lm_head_chunk_rows": 4096}, **nf), m7b, cuda, device_bytes=288 * GB)
     assert p2.buffer_bytes == cache + 152064 * 3584 * 4
     # above the fused size (12 288 tokens) the cache is not built
-    p3 = plan_gradient_checkpointing(_args(seq_length=16384), m7b, cuda, device_bytes=288 * GB)
+    p3 = plan_gradient_checkpointing(_args(seq_length=16384, **nf), m7b, cuda, device_bytes=288 * GB)
     assert p3.buffer_bytes == 152064 * 3584 * 2
     monkeypatch.setattr(model_ops, "_FUSED_GATE_UP", False)
-    assert plan_gradient_checkpointing(_args(), m7b, cuda, device_bytes=288 * GB).buffer_bytes == 152064 * 3584 * 2
+    assert plan_gradient_checkpointing(_args(**nf), m7b, cuda, device_bytes=288 * GB).buffer_bytes == \
+        152064 * 3584 * 2
     # a device the estimate barely fits without the buffers: with them, recompute
     monkeypatch.setattr(model_ops, "_FUSED_GATE_UP", True)
     base = p.state_bytes + p.activation_bytes + p.logits_bytes
     dev = int((base + (4 << 30) + cache // 2) / 0.95)
-    assert plan_gradient_checkpointing(_args(), m7b, cuda, device_bytes=dev).checkpoint
+    assert plan_gradient_checkpointing(_args(**nf), m7b, cuda, device_bytes=dev).checkpoint
     # 32B under FSDP 4: no fused cache (off under sharding), FSDP's transients
     m32 = _meta_model("32b")
     p32 = plan_gradient_checkpointing(_args(seq_length=4096), m32, cuda, shard_world=4, device_bytes=288 * GB)
