@@ -349,11 +349,14 @@ class ProbeRunner:
             self._abort_rccl()
         ok = 1
         # the probe's memory back before the next one: Python garbage first (reference cycles can
-        # hold a probe's model and optimizer state), then torch's cached device blocks and pinned host
-        # buffers (gloo stages CUDA tensors through pinned host memory in the one-GPU rehearsal,
-        # where every rank shares one card)
+        # hold a probe's model and optimizer state; the trainer probes freeze the heap they set up,
+        # as the loop does, so it is unfrozen first or those cycles would never be collected — the
+        # C3 probe's 15 GB parameter buffer stayed allocated through every later probe), then
+        # torch's cached device blocks and pinned host buffers (gloo stages CUDA tensors through
+        # pinned host memory in the one-GPU rehearsal, where every rank shares one card)
         import gc
 
+        gc.unfreeze()
         gc.collect()
         if self.device.type == "cuda" and not partial:
             try:

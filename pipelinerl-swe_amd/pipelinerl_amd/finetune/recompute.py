@@ -12,8 +12,9 @@ forward is the same deterministic kernels on the same inputs).
   ``auto`` (default)  keep every layer's activations when the estimate below fits the device;
                       else recompute only as many decoder layers as needed: the last K layers keep
                       their activations (K the largest that fits, from the same estimate with a
-                      recomputed layer holding only its input hidden state, plus one layer's
-                      activations while it is recomputed), the others recompute — every layer
+                      recomputed layer holding only its input hidden state, plus two layers'
+                      worth while one is recomputed: its activations and its backward's
+                      temporaries), the others recompute — every layer
                       when K = 0.  The results are the same for every K.
   ``always``          the reference's behaviour: checkpoint whenever gradient_checkpointing is set
 ``finetune.gradient_checkpointing_keep_layers`` (build-only, optional int): K itself (A/B runs).
@@ -195,7 +196,9 @@ def plan_gradient_checkpointing(args, model, device: torch.device, shard_world: 
     def need_for(keep: int) -> tuple[int, int, int]:
         """(bytes compared with the device, activation bytes, buffer bytes) when the last ``keep``
         layers keep their activations and the others recompute."""
-        a = act if keep >= L else keep * act_layer + act_layer  # + the layer being recomputed
+        # + the layer being recomputed and its backward's own temporaries (measured on an 8-layer
+        # 7B model at K = 4: one layer's worth was 5 % short, tests/test_recompute_gpu.py)
+        a = act if keep >= L else keep * act_layer + 2 * act_layer
         a_bytes = int(a * f_act) + (0 if keep >= L else (L - keep) * saved_input)
         buffers = build_buffer_bytes(config, int(seq), chunk, int(shard_world), pbytes, flat) + \
             fsdp_transient_bytes(model, int(shard_world), a, logits, head)

@@ -39,3 +39,38 @@ def test_partial_recompute_gradients_and_memory():
         assert worst <= 1e-2, (keep, worst)
     assert peaks[0] < peaks[2] < peaks[4], peaks
     print({"peak_mb": {k: round(v / 2**20, 1) for k, v in peaks.items()}, "no_ckpt_mb": round(peak_none / 2**20, 1)})
+
+
+def test_plan_bounds_the_measured_peak_per_kept_layers():
+    """The plan's estimate (finetune/recompute.py, without its fixed headroom) against the measured
+    peak of the C3 step on an 8-layer 7B-shaped model (2 of C3's packed micro-batches, AdamW) with
+    0, 4 and 8 layers keeping their activations: an upper bound within 1.3 x at every K."""
+    import gc
+
+    from transformers import AutoModelForCausalLM, Qwen2Config
+
+    from pipelinerl_amd import workloads
+    from pipelinerl_amd.finetune.recompute import HEADROOM_BYTES, HEADROOM_FRAC, plan_gradient_checkpointing
+    from pipelinerl_amd.trainer_probe import QWEN, dp_step_probe
+
+    batches = workloads.micro_batches("c3", 2, seed=1234)
+    T = max(int(b.attention_mask.sum()) for b in batches)
+    with torch.device("meta"):
+        meta = AutoModelForCausalLM.from_config(Qwen2Config(**dict(QWEN["7b"], num_hidden_layers=8)),
+                                                dtype=torch.bfloat16)
+    dev_bytes = torch.cuda.get_device_properties(DEV).total_memory
+    out = {}
+    for keep in (0, 4, 8):
+        gc.unfreeze()  # the probe freezes the heap it sets up (as the loop does): release the last one
+        gc.collect()
+        torch.cuda.empty_cache()
+        base = torch.cuda.memory_allocated(DEV)  # the probe's peak counts from here
+        r = dp_step_probe("c3", steps=1, warmup=1, device=DEV, layers=8, batches=batches, grad_ckpt=True,
+                          keep_layers=keep)
+        peak = r["peak_mem_gb"] * 1e9 - base
+        args = {"gradient_checkpointing": True, "seq_length": T, "gradient_checkpointing_keep_layers": keep}
+        p = plan_gradient_checkpointing(args, meta, DEV, device_bytes=dev_bytes)
+        est = p.need_bytes - int(HEADROOM_FRAC * dev_bytes) - HEADROOM_BYTES
+        out[keep] = (round(peak / 1e9, 2), round(est / 1e9, 2))
+        assert peak <= est <= 1.3 * peak, (keep, out)
+    print({"peak_vs_estimate_gb": out, "tokens": T})
