@@ -76,6 +76,8 @@ def main():
                     help="gradient_checkpointing: true, as the reference config sets it (conf/finetune/base.yaml:45)")
     ap.add_argument("--ckpt-policy", choices=["auto", "always"], default="auto",
                     help="gradient_checkpointing_policy (finetune/recompute.py)")
+    ap.add_argument("--keep-layers", type=int, default=None,
+                    help="finetune.gradient_checkpointing_keep_layers (with --grad-ckpt: the last K layers keep activations)")
     ap.add_argument("--alloc", default=None,
                     help="finetune.allocator_settings (devalloc.py; default: the product's; 'none': torch's own)")
     ap.add_argument("--workdir", default=None)
@@ -125,6 +127,8 @@ def main():
                 fused_lm_head=not a.full_logits))
     if a.alloc is not None:
         ft["allocator_settings"] = None if a.alloc == "none" else a.alloc
+    if a.keep_layers is not None:
+        ft["gradient_checkpointing_keep_layers"] = a.keep_layers
     cfg = Cfg.wrap({"output_dir": str(exp), "streams": {"backend": "files"}, "finetune": ft,
                     "me": {"weight_update_group_init_method": None, "weight_update_group_world_size": 0,
                            "llm_urls": ""}})
@@ -153,7 +157,7 @@ def main():
     out = {"tool": "loop_bench", "model": f"Qwen2.5-{a.model} shapes (random init, bf16)",
            "seq_length": a.seq_length, "samples_per_step": a.samples_per_step, "mean_rollout_len": a.mean_len, "length_dist": a.dist,
            "fused_lm_head": not a.full_logits, "fused_model_ops": not a.eager_ops, "steps": m.completed_steps,
-           "gradient_checkpointing": a.grad_ckpt, "checkpointing_policy": a.ckpt_policy, "allocator_settings": ft.get("allocator_settings", "default"),
+           "gradient_checkpointing": a.grad_ckpt, "checkpointing_policy": a.ckpt_policy, "keep_layers": a.keep_layers, "allocator_settings": ft.get("allocator_settings", "default"),
            "micro_batches_per_step": [x["throughput/micro_batches_per_step"] for x in lines],
            "tokens_per_step": [x["throughput/tokens_per_step"] for x in lines],
            "step_wall_s": [round(b - a_, 3) for a_, b in zip(stamps, stamps[1:])],
