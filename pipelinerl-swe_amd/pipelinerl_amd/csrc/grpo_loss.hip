@@ -586,9 +586,6 @@ __global__ __launch_bounds__(BLOCK) void grpo_fwd_stream(KArgs a) {
 #ifndef PRL_HYB_U1
 #define PRL_HYB_U1 2
 #endif
-#ifndef PRL_HYB_PREFETCH
-#define PRL_HYB_PREFETCH 0  // 1: the next row's resident loads are issued before this row's tail pass
-#endif
 constexpr int kHybNR = PRL_HYB_NR, kHybNL = PRL_HYB_NL;
 typedef __attribute__((address_space(3))) void lds_void_t;
 // d = p (alpha + beta t) (+ gadd at the target column) of one fp32 vector, stored at voff + soff of
@@ -613,7 +610,7 @@ __device__ __forceinline__ void hyb_store(__amdgpu_buffer_rsrc_t ws, int voff, i
 }
 template <int NR, int NL>
 __global__ __launch_bounds__(1024) void grpo_fwd_hybrid_f32(KArgs a) {
-  constexpr int BLOCK = 1024, NW = BLOCK / 64, U = PRL_HYB_PREFETCH ? 2 : 4;  // pass 2's tail vectors in flight
+  constexpr int BLOCK = 1024, NW = BLOCK / 64, U = 4;  // pass 2's tail vectors in flight
   constexpr int U1 = PRL_HYB_U1;  // the tail's vectors in flight in pass 1, beside the NR resident ones
   constexpr int VSTRIDE = BLOCK * 16;  // bytes between a lane's consecutive vectors
   __shared__ f32x4 slab[NL > 0 ? NL : 1][BLOCK];
@@ -652,7 +649,6 @@ __global__ __launch_bounds__(1024) void grpo_fwd_hybrid_f32(KArgs a) {
     const float* row = lg + lrow * a.ld;
     const auto rs = row_rsrc(row, a.V * 4);
     const bool has_next = i + gridDim.x < nrows;
-    bool loaded_next = false;
     const int64_t tid_raw = RowLd::ld(a.input_ids, tok);
     const TokIn tin = tok_in<RowLd>(a, tok);
     const bool bad_id = (uint64_t)tid_raw >= (uint64_t)a.V;
@@ -719,15 +715,6 @@ __global__ __launch_bounds__(1024) void grpo_fwd_hybrid_f32(KArgs a) {
       for (int k = 0; k < NL; ++k)
         hyb_store(ws, voff, (NR + k) * VSTRIDE, (tgt - (NR + k) * BLOCK * 4) - lcol, slab[k][tid], zero_row, c, M, l2s,
                   alpha, beta, gadd);
-      if constexpr (PRL_HYB_PREFETCH != 0) {
-        // the next row's resident part streams in behind this row's tail (its slab slots were just
-        // read by this lane: the reads retire first)
-        if (has_next) {
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          load_resident(row_of_iter(i + gridDim.x));
-          loaded_next = true;
-        }
-      }
       int g2 = kTail0 + tid;
       for (; g2 + (U - 1) * BLOCK < nvec; g2 += U * BLOCK) {
         f32x4 x[U];
@@ -747,7 +734,7 @@ __global__ __launch_bounds__(1024) void grpo_fwd_hybrid_f32(KArgs a) {
     // the next row's DMA overwrites this lane's slab slots only after its own reads above (same
     // lane, program order: the LDS reads retire before the next row's DMA is issued)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (has_next && !loaded_next) load_resident(row_of_iter(i + gridDim.x));
+    if (has_next) load_resident(row_of_iter(i + gridDim.x));
   }
 }
 
