@@ -156,6 +156,11 @@ def plan_gradient_checkpointing(args, model, device: torch.device, shard_world: 
     if policy == "always" and forced is None:
         return RecomputePlan(True, "policy always (the reference's behaviour)", keep_layers=0)
     if device_bytes is None and device.type != "cuda":
+        if forced is not None:  # K stated by the config: nothing to size
+            L = int(getattr(getattr(model, "config", None), "num_hidden_layers", 0) or 0)
+            keep = max(0, min(int(forced), L))
+            return RecomputePlan(keep < L, f"keep_layers {keep} of {L} (finetune.gradient_checkpointing_keep_layers)",
+                                 keep_layers=keep if keep < L else -1)
         return RecomputePlan(True, "not a HIP device: the reference's behaviour", keep_layers=0)
     seq = args.get("seq_length")
     config = getattr(model, "config", None)

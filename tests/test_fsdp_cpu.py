@@ -43,8 +43,11 @@ def _loop_rank(rank, world, port, exp, steps, passes, extra):
     full = {n: (p.full_tensor() if isinstance(p, DTensor) else p).detach().clone()
             for n, p in captured["model"].named_parameters()}
     torch.save(full, exp / f"params_w{world}_r{rank}.pt")
+    from pipelinerl_amd.finetune.sharding import decoder_layers
+
+    flags = [bool(getattr(layer, "gradient_checkpointing", False)) for layer in decoder_layers(captured["model"])]
     (exp / f"metrics_w{world}_r{rank}.json").write_text(json.dumps({"steps": m.completed_steps,
-                                                                    "samples": m.samples}))
+                                                                    "samples": m.samples, "ckpt_flags": flags}))
     if dist.is_initialized():
         dist.destroy_process_group()
 
@@ -147,3 +150,24 @@ def test_sharded_weight_snapshot_reaches_actor(tmp_path):
     assert set(got) == set(want)
     for n in want:
         assert torch.equal(got[n], want[n].to(torch.bfloat16)), n
+
+
+def test_fsdp_loop_with_partial_recompute_matches(tmp_path):
+    """gradient_checkpointing with the last 1 of 2 decoder layers keeping its activations
+    (finetune.gradient_checkpointing_keep_layers, checkpoints.keep_activations) under the FSDP2
+    loop: the same parameters as the FSDP loop without checkpointing."""
+    from test_finetune_loop_cpu import free_port
+
+    runs = {}
+    for name, extra in (("plain", {"sharding": "fsdp"}),
+                        ("ckpt", {"sharding": "fsdp", "gradient_checkpointing": True,
+                                  "gradient_checkpointing_keep_layers": 1})):
+        exp = tmp_path / name
+        exp.mkdir()
+        per_step, _ = _setup(exp, 2)
+        mp.spawn(_loop_rank, args=(2, free_port(), str(exp), 2, per_step, extra), nprocs=2, join=True)
+        runs[name] = torch.load(exp / "params_w2_r0.pt")
+        flags = json.loads((exp / "metrics_w2_r0.json").read_text())["ckpt_flags"]
+        assert flags == ([False, False] if name == "plain" else [True, False]), (name, flags)
+    worst = max(float((runs["plain"][n] - runs["ckpt"][n]).abs().max()) for n in runs["plain"])
+    assert worst < 2e-6, worst
