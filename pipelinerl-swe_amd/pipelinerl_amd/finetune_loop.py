@@ -412,7 +412,19 @@ def rl_finetuning_worker(args, ctx: Dist, model, optimizer, lr_scheduler, grads:
             local_samples += nseq
             tokens_processed.append(ntok)
 
-        total_over = ctx.sum_int(local_samples)  # lockstep count exchange (CPU control group)
+        if native_step:  # stats read back after the backward is queued; gradients at loss_scale
+            loss, stats = step_fn(model, batch, metrics.completed_steps, final_steps, rl_config,
+                                  grad_scale=loss_scale, defer_stats=defer_stats)
+        else:
+            loss, stats = step_fn(model, batch, metrics.completed_steps, final_steps, rl_config)
+        trace.mark("forward")
+        # The lockstep count exchange (CPU control group) after the forward is queued and before the
+        # backward, the first thing that needs its answer (the boundary pass arms the gradient
+        # all-reduce / FSDP's reduce-scatter): a host waiting here for a slower rank leaves its
+        # device this pass's forward to run instead of nothing (workloads.lockstep_cost's model at
+        # 8 ranks on C3 rollouts: 0.874 -> 0.889 of the balanced step).  The values
+        # exchanged and the messages written are the reference's (finetune_loop.py:577-617).
+        total_over = ctx.sum_int(local_samples)
         assert total_over % args.seq_parallel == 0
         total = total_over // args.seq_parallel
         do_step = total == target
@@ -420,12 +432,6 @@ def rl_finetuning_worker(args, ctx: Dist, model, optimizer, lr_scheduler, grads:
         if do_step and grads is not None:
             grads.arm()
         set_gradient_sync(model, do_step or sync_every)  # FSDP: reduce-scatter on the boundary only
-        if native_step:  # stats read back after the backward is queued; gradients at loss_scale
-            loss, stats = step_fn(model, batch, metrics.completed_steps, final_steps, rl_config,
-                                  grad_scale=loss_scale, defer_stats=defer_stats)
-        else:
-            loss, stats = step_fn(model, batch, metrics.completed_steps, final_steps, rl_config)
-        trace.mark("forward")
         if sentinel:
             loss = loss * 0.0
         elif loss_scale != 1.0:

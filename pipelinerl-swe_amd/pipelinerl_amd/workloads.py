@@ -118,3 +118,55 @@ def rl_config(config: str, samples_per_step: int):
     spec = SPECS[config]
     return RLConfig(policy_loss="ppo", epsilon=4.0, kl_coef=spec.kl_coef, final_kl_coef=spec.kl_coef,
                     clamp_log_ratio_ref_new_value=5, divide_advantage_by_std=False, batch_size=samples_per_step)
+
+
+def lockstep_cost(config: str, ranks: int, samples_per_rank: int, seed: int = 7, seq_length: int | None = None,
+                  ms_fixed: float = 30.0, ms_per_token: float = (350.0 - 30.0) / 11425,
+                  forward_share: float = 1 / 3) -> dict:
+    """A timing model of one optimizer step under the reference's lockstep protocol
+    (finetune_loop.py:577-617: every pass exchanges the sample counts on the host; ranks past their
+    quota run sentinel passes) on the preprocessor's own assignment of ``config``'s rollouts to
+    ``ranks`` trainers (preprocess.py:557-626, ``samples_per_rank`` each).  A micro-batch costs
+    ms_fixed + ms_per_token x tokens on the device (defaults: the C3 7B step in DESIGN.md, 350 ms at
+    11 425 tokens; a sentinel 30 ms), ``forward_share`` of it in the forward.  A host reaches pass
+    p's exchange once its forward(p-1) statistics are read back, so the exchange ends when the
+    slowest rank's forward(p-1) has.  Step times (ms): ``full_pass`` (every pass waits for every
+    rank's whole previous pass: the naive bound), ``exchange_then_forward`` (forward(p) enqueued
+    after the exchange: the reference's order and this build's through round 4),
+    ``forward_then_exchange`` (forward(p) enqueued before it, backward(p) after: the loop's order
+    now), ``free`` (no per-pass coupling; sentinels skipped) and ``balanced`` (the mean rank's
+    work); efficiencies = balanced / each."""
+    spec = SPECS[config]
+    data = rollouts(config, ranks * samples_per_rank, seed=seed)
+    writes = pack(data, seq_length or spec.seq_length, ranks * samples_per_rank, num_trainers=ranks)
+    tok: dict[int, list[int]] = {r: [] for r in range(ranks)}
+    for r, b in writes:
+        tok[r].append(0 if b.sentinel else int(b.attention_mask.sum()))
+    t = {r: [ms_fixed + ms_per_token * x for x in v] for r, v in tok.items()}
+    passes = max(len(v) for v in t.values())
+
+    def cost(r: int, p: int) -> float:
+        return t[r][p] if p < len(t[r]) else 0.0
+
+    def coupled(forward_first: bool) -> float:
+        end, fwd = [0.0] * ranks, [0.0] * ranks
+        for p in range(passes):
+            barrier = max(fwd)
+            for r in range(ranks):
+                f, b = cost(r, p) * forward_share, cost(r, p) * (1 - forward_share)
+                if forward_first:
+                    fwd[r] = end[r] + f
+                    end[r] = max(fwd[r], barrier) + b
+                else:
+                    fwd[r] = max(end[r], barrier) + f
+                    end[r] = fwd[r] + b
+        return max(end)
+
+    times = {"full_pass": sum(max(cost(r, p) for r in range(ranks)) for p in range(passes)),
+             "exchange_then_forward": coupled(False), "forward_then_exchange": coupled(True),
+             "free": max(sum(x for x, n in zip(t[r], tok[r]) if n) for r in range(ranks))}
+    balanced = sum(sum(x for x, n in zip(t[r], tok[r]) if n) for r in range(ranks)) / ranks
+    return {"config": config, "ranks": ranks, "samples_per_step": ranks * samples_per_rank, "passes": passes,
+            "sentinels_per_rank": [v.count(0) for v in tok.values()], "tokens_per_rank": [sum(v) for v in tok.values()],
+            "ms": {k: round(v, 1) for k, v in times.items()} | {"balanced": round(balanced, 1)},
+            "efficiency": {k: round(balanced / v, 4) for k, v in times.items()}}
