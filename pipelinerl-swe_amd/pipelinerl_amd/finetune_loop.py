@@ -45,7 +45,7 @@ from .finetune.grad_sync import GradBuckets
 from .finetune.optim import clip_grad_norm, get_optimizer
 from .finetune.rl import RLConfig, RLStats, rl_step
 from .finetune.rl.utils import aggregate_rl_stats
-from .finetune.sharding import fsdp_requested, set_gradient_sync, shard_model
+from .finetune.sharding import fsdp_requested, is_sharded, set_gradient_sync, shard_model
 from .finetune.trace import PhaseTrace
 from . import native_data
 from .devalloc import DEFAULT_SETTINGS, configure_device_allocator
@@ -375,6 +375,7 @@ def rl_finetuning_worker(args, ctx: Dist, model, optimizer, lr_scheduler, grads:
     loss_scale = micro_batch_loss_scale(args, ctx.world, grad_scale_mode)
     native_step = step_fn is rl_step
     defer_stats = os.environ.get("PRL_DEFER_STATS", "1") != "0"  # 0: read them before backward (A/B)
+    collective_backward = is_sharded(model)  # FSDP: every rank's backward joins all-gathers
     trace = PhaseTrace(ctx.device, bool(args.get("trace_gpu_phases", False)) or os.environ.get("PRL_TRACE_GPU") == "1")
     trace_md: dict[str, float] = {}
 
@@ -418,19 +419,29 @@ def rl_finetuning_worker(args, ctx: Dist, model, optimizer, lr_scheduler, grads:
         else:
             loss, stats = step_fn(model, batch, metrics.completed_steps, final_steps, rl_config)
         trace.mark("forward")
-        # The lockstep count exchange (CPU control group) after the forward is queued and before the
-        # backward, the first thing that needs its answer (the boundary pass arms the gradient
-        # all-reduce / FSDP's reduce-scatter): a host waiting here for a slower rank leaves its
-        # device this pass's forward to run instead of nothing (workloads.lockstep_cost's model at
-        # 8 ranks on C3 rollouts: 0.874 -> 0.889 of the balanced step).  The values
-        # exchanged and the messages written are the reference's (finetune_loop.py:577-617).
-        total_over = ctx.sum_int(local_samples)
-        assert total_over % args.seq_parallel == 0
-        total = total_over // args.seq_parallel
-        do_step = total == target
+        # The lockstep count exchange (CPU control group) after the forward is queued: a host waiting
+        # there for a slower rank leaves its device this pass's forward (and, below the quota, its
+        # backward) to run instead of nothing.  Only the boundary pass needs the answer before its
+        # backward (it arms the gradient all-reduce / FSDP's reduce-scatter); a rank still below
+        # its own quota cannot be on it — every rank's count is at most its quota, so the total is
+        # short of the target — and exchanges after queueing the backward, unless the backward
+        # itself is collective (FSDP re-gathers parameters there: a rank at its quota would wait in
+        # the exchange for one blocked in that all-gather).  Same values exchanged,
+        # same messages as the reference (finetune_loop.py:577-617); workloads.lockstep_cost prices
+        # the coupling.
+        def exchange() -> int:
+            total_over = ctx.sum_int(local_samples)
+            assert total_over % args.seq_parallel == 0
+            return total_over // args.seq_parallel
 
-        if do_step and grads is not None:
-            grads.arm()
+        early = args.seq_parallel == 1 and local_samples < target_per_lead and not collective_backward
+        if early:
+            do_step = False
+        else:
+            total = exchange()
+            do_step = total == target
+            if do_step and grads is not None:
+                grads.arm()
         set_gradient_sync(model, do_step or sync_every)  # FSDP: reduce-scatter on the boundary only
         if sentinel:
             loss = loss * 0.0
@@ -438,6 +449,12 @@ def rl_finetuning_worker(args, ctx: Dist, model, optimizer, lr_scheduler, grads:
             loss = loss * loss_scale  # DeepSpeed's engine.backward: loss / gradient_accumulation_steps
         loss.backward()
         trace.mark("backward")
+        if early:
+            total = exchange()
+            if total == target:
+                raise RuntimeError(f"the global sample count reached the step's target ({target}) while this rank "
+                                   f"was below its quota ({local_samples} < {target_per_lead}): the input streams "
+                                   "do not follow the per-rank quota protocol")
         if isinstance(stats, RLStats):
             stats = stats.resolve()  # also raises the reference's non-finite assertions
         if not sentinel:

@@ -133,8 +133,9 @@ def lockstep_cost(config: str, ranks: int, samples_per_rank: int, seed: int = 7,
     slowest rank's forward(p-1) has.  Step times (ms): ``full_pass`` (every pass waits for every
     rank's whole previous pass: the naive bound), ``exchange_then_forward`` (forward(p) enqueued
     after the exchange: the reference's order and this build's through round 4),
-    ``forward_then_exchange`` (forward(p) enqueued before it, backward(p) after: the loop's order
-    now), ``free`` (no per-pass coupling; sentinels skipped) and ``balanced`` (the mean rank's
+    ``forward_then_exchange`` (forward(p) enqueued before it, backward(p) after), ``loop`` (this
+    loop: in addition a rank below its quota queues backward(p) before the exchange too), ``free``
+    (no per-pass coupling; sentinels skipped) and ``balanced`` (the mean rank's
     work); efficiencies = balanced / each."""
     spec = SPECS[config]
     data = rollouts(config, ranks * samples_per_rank, seed=seed)
@@ -162,8 +163,24 @@ def lockstep_cost(config: str, ranks: int, samples_per_rank: int, seed: int = 7,
                     end[r] = fwd[r] + b
         return max(end)
 
+    last_real = {r: max((i for i, x in enumerate(tok[r]) if x), default=-1) for r in range(ranks)}
+
+    def loop_order() -> float:
+        # this loop: forward(p); below the rank's quota backward(p) then the exchange, at the quota
+        # the exchange then backward(p); the host moves on once the exchange is done and its
+        # forward(p) statistics are read back
+        end, host = [0.0] * ranks, [0.0] * ranks
+        for p in range(passes):
+            fwd = [max(end[r], host[r]) + cost(r, p) * forward_share for r in range(ranks)]
+            x = max(host)  # every host reaches the exchange right after queueing its pass
+            for r in range(ranks):
+                b = cost(r, p) * (1 - forward_share)
+                end[r] = (fwd[r] if p < last_real[r] else max(fwd[r], x)) + b
+                host[r] = max(x, fwd[r])
+        return max(end)
+
     times = {"full_pass": sum(max(cost(r, p) for r in range(ranks)) for p in range(passes)),
-             "exchange_then_forward": coupled(False), "forward_then_exchange": coupled(True),
+             "exchange_then_forward": coupled(False), "forward_then_exchange": coupled(True), "loop": loop_order(),
              "free": max(sum(x for x, n in zip(t[r], tok[r]) if n) for r in range(ranks))}
     balanced = sum(sum(x for x, n in zip(t[r], tok[r]) if n) for r in range(ranks)) / ranks
     return {"config": config, "ranks": ranks, "samples_per_step": ranks * samples_per_rank, "passes": passes,
