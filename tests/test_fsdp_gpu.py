@@ -3,7 +3,9 @@ gloo (RCCL needs one GPU per rank), so FSDP really frees each layer's unsharded 
 the forward and all-gathers them again for the backward — the case where PrlLinearFn / RMSNorm /
 SwiGLU / RoPE autograd functions must find their saved parameters re-gathered in place.  The
 sharded gradients (mean over the two ranks' batches) must equal one unsharded model's gradients
-of the mean loss."""
+of the mean loss — also with gradient checkpointing on the first layer and the second keeping its
+activations (checkpoints.keep_activations, the plan's partial recompute), where the recomputed
+layer's forward runs inside FSDP's backward."""
 
 import os
 import sys
@@ -46,7 +48,7 @@ def _batch(rank):
     return ids, pos, packed_kwargs(b, "cuda:0")
 
 
-def _run(rank, port, tmp):
+def _run(rank, port, tmp, keep):
     sys.path[:0] = [str(ROOT), str(ROOT / "pipelinerl-swe_amd"), str(ROOT / "tests")]
     os.environ["OMP_NUM_THREADS"] = "1"
     import torch.distributed as dist
@@ -57,7 +59,13 @@ def _run(rank, port, tmp):
     # gloo for CUDA tensors too: FSDP's device mesh would otherwise open an RCCL group, which
     # cannot span two ranks on one GPU
     dist.init_process_group("cpu:gloo,cuda:gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=2)
-    m = shard_model(_model(tmp))
+    m = _model(tmp)
+    if keep is not None:
+        from pipelinerl_amd.finetune.checkpoints import keep_activations
+
+        m.gradient_checkpointing_enable(gradient_checkpointing_kwargs={"use_reentrant": False})
+        assert keep_activations(m, keep) == keep
+    m = shard_model(m)
     ids, pos, kw = _batch(rank)
     _loss(m, ids, pos, kw).backward()
     grads = {n: p.grad.full_tensor().float().cpu() for n, p in m.named_parameters()}
@@ -70,10 +78,11 @@ def _run(rank, port, tmp):
     dist.destroy_process_group()
 
 
-def test_fsdp_resharding_with_patched_ops(tmp_path):
+@pytest.mark.parametrize("keep", [None, 1])
+def test_fsdp_resharding_with_patched_ops(tmp_path, keep):
     from test_weight_update_cpu import free_port
 
-    mp.spawn(_run, args=(free_port(), str(tmp_path)), nprocs=2, join=True)
+    mp.spawn(_run, args=(free_port(), str(tmp_path), keep), nprocs=2, join=True)
     d = torch.load(tmp_path / "grads.pt")
     for n, r in d["ref"].items():
         g = d["fsdp"][n]
