@@ -471,6 +471,23 @@ def main():
         dist.all_reduce(k_max, op=dist.ReduceOp.MAX)
     elapsed = float(t_max)
     kern_ms = float(k_max)
+    # the same bytes through a plain device copy on this box (torch's copy kernel, logits -> a second
+    # buffer: one read + one write of T x V bf16), after the timed region: HBM rates vary a few %
+    # from box to box, and this puts the loss head's rate beside a copy measured in the same run
+    copy_ms = None
+    if rank == 0:
+        dst = torch.empty_like(logits)
+        cts = []
+        for i in range(8):
+            c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            c0.record()
+            dst.copy_(logits.detach())
+            c1.record()
+            c1.synchronize()
+            if i >= 2:
+                cts.append(c0.elapsed_time(c1))
+        copy_ms = float(np.median(cts))
+        del dst
     # The probes below are reported beside `value`, never in it.  Each one is independent: a probe
     # that raises is reported as an error (every rank's traceback on stderr), the ranks agree on its
     # outcome over a CPU control group, and the next probe still runs; each reports its wall time.
@@ -595,7 +612,11 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "kernel": "grpo_fwd_resident<19> (+stats/finalize) per prl_grpo_forward",
                          "kernel_ms": round(kern_ms, 4), "algorithmic_bytes": alg_bytes,
-                         "traffic_source": tsrc},
+                         "traffic_source": tsrc,
+                         "box_copy": None if copy_ms is None else {
+                             "what": "torch copy_ of the T x V bf16 logits into a second buffer, same run",
+                             "ms": round(copy_ms, 4), "GBps": round(2.0 * T * V * 2 / copy_ms / 1e6, 1),
+                             "loss_head_vs_copy": round(copy_ms / kern_ms, 4)}},
             "cpu_baseline": cpu,
         }
         scaling = dp_scaling(world, c3, trainer)
