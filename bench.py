@@ -49,7 +49,8 @@ and fraction of the HBM peak on 2 x 4 x T x V algorithmic bytes.
 
 Prints ONE JSON line (rank 0).  roofline.achieved = algorithmic bytes per launch
 (T*V*2 read + T*V*2 dlogits write + 37*T side data) / the average duration
-of the prl_grpo_forward launch measured with HIP events on its stream.
+of the prl_grpo_forward launch measured with HIP events on its stream; roofline.box_copy = the
+same bytes through torch's device copy in the same run (box-to-box HBM rates differ by a few %).
 """
 
 from __future__ import annotations
