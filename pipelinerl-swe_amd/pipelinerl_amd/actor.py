@@ -1,8 +1,13 @@
-"""Actor-side receive of the trainer's weight broadcast (mirror of pipelinerl/vllm1.py:53-117).
+"""Actor-side receive of the trainer's weight broadcast (mirror of pipelinerl/vllm1.py:53-117 and
+pipelinerl/vllm0.py:51-104).
 
-``WorkerExtension`` is a mixin for an inference worker (vLLM's ``worker_extension_cls``) or any
+``WorkerExtension`` is a mixin for an inference worker (vLLM v1's ``worker_extension_cls``) or any
 object with: ``rank``, ``device``, ``model_runner.model.load_weights(weights=[(name, t)])`` and
-``model_config.dtype``.  Methods, arguments and errors are the reference's:
+``model_config.dtype``.  vLLM v0 — the reference's default actor (conf/base.yaml ``use_v1: false``,
+launch.py:130-131) — registers a Worker SUBCLASS instead (``parallel_config.worker_cls``,
+vllm0.py:204-206): ``make_worker_class(multi_step)`` builds it over vLLM's ``Worker`` /
+``MultiStepWorker`` with the same methods, and ``AsyncRLWorker`` / ``AsyncRLMultiStepWorker`` are
+the two classes the reference registers by name.  Methods, arguments and errors are the reference's:
 
   init_actor_update_group(actor_idx, actor_ngpus, weight_update_group_init_method,
                           weight_update_group_world_size)      -> joins the "actor" group as
@@ -98,12 +103,16 @@ class WorkerExtension:
         for name, shape, n, off in zip(layout.names, layout.shapes, layout.numels, layout.offsets):
             self._load_one(name, flat[off:off + n].view(shape))
 
+    def _inference_model(self):
+        """The model loads go to (vllm1.py:89-93: the runner's model)."""
+        return self.model_runner.model
+
     def _direct_targets(self, layout) -> list[torch.Tensor] | None:
         """The destination region of every broadcast name, from the model's direct_target(name,
         shape) (ParamDictModel: the parameter; StackedParamsModel: a row block of a fused
         parameter), when each is a contiguous, 16-B aligned bf16 tensor on this HIP device; None
         otherwise (models without direct_target keep the per-name load)."""
-        resolve = getattr(self.model_runner.model, "direct_target", None)
+        resolve = getattr(self._inference_model(), "direct_target", None)
         if resolve is None or self.device.type != "cuda":
             return None
         out = []
@@ -116,9 +125,73 @@ class WorkerExtension:
         return out
 
     def _load_one(self, name: str, tensor: torch.Tensor):
-        loaded = self.model_runner.model.load_weights(weights=[(name, tensor)])
+        loaded = self._inference_model().load_weights(weights=[(name, tensor)])
         if len(loaded) != 1:
             raise ValueError(f"model {name} not found in model state dict")
+
+
+# ------------------------------------------------------------------------------------------
+# vLLM v0 (vllm0.py:51-104): a Worker subclass registered through parallel_config.worker_cls
+
+def is_multi_step_runner(runner) -> bool:
+    """vllm0.py:90 ``isinstance(self.model_runner, MultiStepModelRunner)``; without vLLM importable
+    (tests, stand-ins) a class of that name anywhere in the runner's MRO."""
+    try:
+        from vllm.worker.multi_step_model_runner import MultiStepModelRunner
+    except ImportError:
+        return any(c.__name__ == "MultiStepModelRunner" for c in type(runner).__mro__)
+    return isinstance(runner, MultiStepModelRunner)
+
+
+class V0WorkerMixin(WorkerExtension):
+    """The receive side of vllm0.py's worker class: the v1 extension's methods (per_tensor /
+    bucketed transports, the HIP unflatten into direct targets), with the model taken where the v0
+    runner keeps it — a MultiStepModelRunner wraps the real runner and loads go to
+    ``model_runner._base_model_runner.model`` (vllm0.py:90-95)."""
+
+    actor_group_backend = "nccl"  # vllm0.py:75
+
+    def _inference_model(self):
+        runner = self.model_runner
+        if is_multi_step_runner(runner):
+            return runner._base_model_runner.model
+        return runner.model
+
+
+def _vllm_v0_worker_base(multi_step: bool) -> type:
+    """vllm0.py:26,32,52: vLLM v0's Worker or MultiStepWorker."""
+    try:
+        if multi_step:
+            from vllm.worker.multi_step_worker import MultiStepWorker as base
+        else:
+            from vllm.worker.worker import Worker as base
+    except ImportError as e:
+        raise ImportError("the vLLM v0 worker classes need vLLM (vllm.worker.worker / vllm.worker.multi_step_worker); "
+                          "pass base_class= to make_worker_class for another engine's worker") from e
+    return base
+
+
+def make_worker_class(multi_step: bool, base_class: type | None = None) -> type:
+    """vllm0.py:51-100: a class deriving from vLLM v0's ``MultiStepWorker`` (``multi_step``) or
+    ``Worker`` — or ``base_class`` — with ``init_actor_update_group`` / ``receive_weight_update``.
+    The mixin comes first in the MRO, so the base worker's own methods are untouched."""
+    base = base_class if base_class is not None else _vllm_v0_worker_base(multi_step)
+    name = "AsyncRLMultiStepWorker" if multi_step else "AsyncRLWorker"
+    return type(name, (V0WorkerMixin, base), {"__module__": __name__, "__qualname__": name})
+
+
+_V0_CLASSES: dict[str, type] = {}
+
+
+def __getattr__(name: str):
+    """``AsyncRLWorker`` / ``AsyncRLMultiStepWorker`` (vllm0.py:103-104), built on first access so
+    this module imports without vLLM; vLLM resolves ``worker_cls`` by qualified name, which lands
+    here.  One class per process, so the reference's isinstance checks (vllm0.py:127) hold."""
+    if name in ("AsyncRLWorker", "AsyncRLMultiStepWorker"):
+        if name not in _V0_CLASSES:
+            _V0_CLASSES[name] = make_worker_class(multi_step=name == "AsyncRLMultiStepWorker")
+        return _V0_CLASSES[name]
+    raise AttributeError(f"module {__name__!r} has no attribute {name!r}")
 
 
 class ParamDictModel:

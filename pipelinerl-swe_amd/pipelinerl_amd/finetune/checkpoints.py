@@ -90,6 +90,8 @@ def load_model(args, model_class: str, current_dir: Path, device: torch.device, 
         from .value_model import AutoModelForCausalLMWithValueHead
 
         model = AutoModelForCausalLMWithValueHead(model)
+        if src == str(current_dir):  # resume: the saved head too (value_model.py:189-192)
+            model.load_value_head(current_dir)
     return model.to(device)
 
 
@@ -139,11 +141,14 @@ def save_model_and_tokenizer(output_dir: Path, model, tokenizer, *, safe_seriali
             m = getattr(model, "module", model)
             if sd is None and getattr(getattr(m, "pretrained_model", m), "_prl_flat_params", False):
                 # parameters re-homed into one buffer for in-place weight broadcasts
-                # (weight_update.py): save host copies, which share no storage
+                # (weight_update.py): save host copies, which share no storage.  Keys in m's own
+                # namespace: a value-head wrapper splits them (value_model.save_pretrained)
                 sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
             if sd is not None:
                 if getattr(getattr(m, "config", None), "tie_word_embeddings", False):
-                    sd.pop("lm_head.weight", None)  # tied copy (finetune_loop.py:228-231)
+                    # tied copy (finetune_loop.py:228-231), under the wrapper's prefix too
+                    lm_prefix = "pretrained_model." if hasattr(m, "pretrained_model") else ""
+                    sd.pop(lm_prefix + "lm_head.weight", None)
                 m.save_pretrained(tmp, state_dict=sd, safe_serialization=safe_serialization)
             else:
                 m.save_pretrained(tmp, safe_serialization=safe_serialization)

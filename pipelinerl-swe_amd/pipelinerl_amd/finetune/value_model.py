@@ -42,6 +42,37 @@ class AutoModelForCausalLMWithValueHead(nn.Module):
     def gradient_checkpointing_enable(self, gradient_checkpointing_kwargs=None):
         self.pretrained_model.gradient_checkpointing_enable(gradient_checkpointing_kwargs)
 
-    def save_pretrained(self, save_directory, safe_serialization: bool = True, **kw):
-        self.pretrained_model.save_pretrained(save_directory, safe_serialization=safe_serialization, **kw)
-        torch.save(self.value_head.state_dict(), f"{save_directory}/value_head.pt")
+    def save_pretrained(self, save_directory, safe_serialization: bool = True, state_dict: dict | None = None, **kw):
+        """value_model.py:124-172: the LM (loadable by vLLM as is) and ``value_head.pt`` apart; a
+        given ``state_dict`` is in this wrapper's namespace (``pretrained_model.*`` / ``value_head.*``)
+        and split by prefix, any other key raising ValueError."""
+        if state_dict is None:
+            state_dict = self.state_dict()
+        lm, vh = split_value_head_state_dict(state_dict)
+        self.pretrained_model.save_pretrained(save_directory, safe_serialization=safe_serialization, state_dict=lm,
+                                              **kw)
+        torch.save(vh, f"{save_directory}/value_head.pt")
+
+    def load_value_head(self, directory) -> bool:
+        """value_model.py:189-192: the saved head, when ``directory`` holds one (plain tensors only)."""
+        path = f"{directory}/value_head.pt"
+        try:
+            sd = torch.load(path, map_location="cpu", weights_only=True)
+        except FileNotFoundError:
+            return False
+        self.value_head.load_state_dict(sd)
+        return True
+
+
+def split_value_head_state_dict(state_dict: dict) -> tuple[dict, dict]:
+    """(the LM's state dict in its own namespace, the value head's) from the wrapper's."""
+    lm, vh = {}, {}
+    for k, v in state_dict.items():
+        if k.startswith("value_head."):
+            vh[k[len("value_head."):]] = v
+        elif k.startswith("pretrained_model."):
+            lm[k[len("pretrained_model."):]] = v
+        else:
+            raise ValueError(f"Unexpected key in state dict: {k}. "
+                             "Expected keys should start with 'value_head.' or 'pretrained_model.'.")
+    return lm, vh

@@ -204,6 +204,7 @@ def run_finetuning_loop(cfg, step_fn: Callable = rl_step, model=None, tokenizer=
     update_stream = SingleStreamSpec(exp_path=exp_root, topic=TRAINER_TOPIC)
 
     sharded = fsdp_requested(cfg, args) and ctx.initialized
+    snapshot = weight_snapshot_mode(args)
     if model is None:
         model = load_model(args, args.model_class, current_dir, ctx.device, shard_world=ctx.world if sharded else 1)
     if tokenizer is None:
@@ -262,7 +263,7 @@ def run_finetuning_loop(cfg, step_fn: Callable = rl_step, model=None, tokenizer=
                       overlap=bool(args.get("overlap_weight_updates", True)), is_main=ctx.is_main,
                       timeout_s=args.get("weight_update_timeout_s", 900.0),
                       http_timeout_s=args.get("weight_update_http_timeout_s", 600.0),
-                      snapshot=args.get("weight_snapshot", "zero_copy"))
+                      snapshot=snapshot)
         wum.send_weight_update(metrics.samples)
 
     batch_queue: Queue = Queue(maxsize=1)
@@ -285,6 +286,20 @@ def run_finetuning_loop(cfg, step_fn: Callable = rl_step, model=None, tokenizer=
                 actor_group.close()
             else:
                 dist.destroy_process_group(actor_group)
+
+
+def weight_snapshot_mode(args) -> str:
+    """``finetune.weight_snapshot``: "zero_copy" broadcasts the parameters in place, which needs them
+    re-homed into one flat buffer at load (``finetune.flat_parameters``, the default); with
+    ``flat_parameters: false`` the default is the staging copy, and an explicit "zero_copy" falls
+    back to it (with a warning) rather than re-homing the parameters after the optimizer exists."""
+    flat = bool(args.get("flat_parameters", True))
+    mode = args.get("weight_snapshot", "zero_copy" if flat else "copy")
+    if mode == "zero_copy" and not flat:
+        logger.warning("finetune.weight_snapshot=zero_copy needs finetune.flat_parameters=true; "
+                       "using the staging copy (weight_snapshot=copy)")
+        mode = "copy"
+    return mode
 
 
 class TrainingStateError(RuntimeError):
@@ -549,7 +564,10 @@ def rl_finetuning_worker(args, ctx: Dist, model, optimizer, lr_scheduler, grads:
 
 
 def step_metrics(m: TrainingMetrics, lag, q, tokens, passes, mbs, world, samples_per_step, step_took) -> dict:
-    """The stats/* and throughput/* keys of finetune_loop.py:726-764."""
+    """The stats/* and throughput/* keys of finetune_loop.py:726-764, with the reference's values
+    (``tokens``: this rank's micro-batch token counts; pinned by F7, tests/golden/make_f7.py).
+    ``throughput/real_tokens_per_sec`` is this rank's tokens / step wall time as at :754; the
+    whole job's rate is the added ``throughput/real_tokens_per_sec_all_ranks``."""
     wt = sum(tokens)
     sp = sum(passes)
     return {
@@ -567,7 +585,8 @@ def step_metrics(m: TrainingMetrics, lag, q, tokens, passes, mbs, world, samples
         "throughput/max_tokens_per_micro_batch": max(tokens) if tokens else 0,
         "throughput/tokens_per_micro_batch": wt / len(tokens) if tokens else 0,
         "throughput/tokens_per_sec": wt * world / sp if sp else 0,
-        "throughput/real_tokens_per_sec": wt * world / step_took if step_took else 0,
+        "throughput/real_tokens_per_sec": wt / step_took if step_took else 0,
+        "throughput/real_tokens_per_sec_all_ranks": wt * world / step_took if step_took else 0,
         "throughput/sec_per_pass": sp / len(passes) if passes else 0,
         "throughput/steps_per_sec": 1 / step_took if step_took else 0,
         "throughput/samples_per_sec": samples_per_step / sp if sp else 0,

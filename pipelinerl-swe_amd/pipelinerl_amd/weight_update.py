@@ -164,6 +164,17 @@ def unwrap_model(model):
     return getattr(m, "pretrained_model", m)  # value-head wrapper: broadcast the LM only
 
 
+def lm_namespace(model, named: list[tuple[str, torch.Tensor]]) -> list[tuple[str, torch.Tensor]]:
+    """Names relative to (the FSDP root of) ``model`` -> the language model's own names: under a
+    value-head wrapper (sharded as the root, so its units also hold the LM's embedding, norm and
+    lm_head) the ``pretrained_model.`` prefix goes and the value head's parameters are dropped."""
+    m = getattr(model, "module", model)
+    if not hasattr(m, "pretrained_model"):
+        return named
+    pre = "pretrained_model."
+    return [(n[len(pre):], t) for n, t in named if n.startswith(pre)]
+
+
 class WeightUpdateError(RuntimeError):
     """An actor refused or failed a weight update, or the update did not complete in time."""
 
@@ -204,8 +215,10 @@ class WeightUpdateManager:
             raise ValueError(f"snapshot must be 'zero_copy' or 'copy', got {snapshot!r}")
         self.snapshot = snapshot
         self._flat_params: torch.Tensor | None = None
-        self._read_done = None  # zero-copy: event after the last broadcast read of the parameters
-        self._works: list = []
+        self._snapshot_done = None  # event after the staging copy, or (zero-copy) the broadcast's last read
+        self._works: list = []  # zero-copy: the in-flight broadcast's works
+        self._version: int | None = None
+        self._deadline: float | None = None  # the in-flight update's request time + timeout_s
         self.llm_urls = list(llm_urls)
         self.model = accelerated_model
         self.update_stream = update_stream
@@ -279,7 +292,8 @@ class WeightUpdateManager:
             flat = self._ensure_staging(layout.total, dev) if self.is_main else None
             index = {n: i for i, (n, _) in enumerate(named)}
             seen = set()
-            for unit in gather_units(unwrap_model(self.model)):
+            for unit in gather_units(getattr(self.model, "module", self.model)):  # the FSDP root's units
+                unit = lm_namespace(self.model, unit)
                 seen.update(n for n, _ in unit)
                 if self.is_main:
                     self.packer.flatten([t for _, t in unit], [layout.offsets[index[n]] for n, _ in unit], flat)
@@ -291,6 +305,8 @@ class WeightUpdateManager:
         request = WeightUpdateRequest(version=version, parameters_info=infos, transport=self.transport,
                                       bucket_bytes=self.bucket_bytes if self.transport == "bucketed" else 0)
         t0 = time.time()
+        self._version = version
+        self._deadline = t0 + float(self.timeout_s) if self.timeout_s else None
         futures = [self.pool.submit(self.post, url, request) for url in self.llm_urls]
         logger.info(f"Published weight update request for version {version}")
         params = [p.detach() for _, p in named]
@@ -326,11 +342,13 @@ class WeightUpdateManager:
                     works.append(comm.broadcast(flat[off:off + n].view(shape), self.group, src=0, async_op=True))
             works = [w for w in works if w is not None]  # RcclComm calls are stream-ordered
             done = None
-            if on_gpu:
+            if on_gpu and self._stream_ordered():
                 for w in works:  # RCCL: makes the side stream (not the host) wait for the comm
                     w.wait()
                 done = torch.cuda.Event()
                 done.record(self._stream)
+            # (a gloo group on device tensors — one-GPU tests and rehearsals — completes on gloo's
+            # own threads: the watcher and before_optimizer_step poll its works, never a host wait)
             if in_place is not None:  # the parameters are read until the broadcast ends
                 self._snapshot_done = done
                 self._works = works
@@ -379,16 +397,38 @@ class WeightUpdateManager:
 
     def before_optimizer_step(self) -> None:
         """Order the next in-place parameter update after the snapshot: after the staging copy, or
-        (zero-copy) after the broadcast's last read of the parameters — a device-side wait on an
-        RCCL / stream-ordered group; a host wait for a gloo group's works (tests, rehearsals)."""
+        (zero-copy) after the broadcast's last read of the parameters.  The zero-copy wait is
+        bounded: the host polls the broadcast's completion (its event on a device, the works of a
+        gloo group) between checks of the watcher's error and the update's deadline, and raises
+        WeightUpdateError instead of blocking past ``timeout_s`` on an actor that never receives.
+        The broadcast started one step earlier, so it is normally complete at the first check; the
+        device-side event wait then orders the optimizer's writes after its reads."""
         ev = getattr(self, "_snapshot_done", None)
+        self._snapshot_done = None
+        works, self._works = self._works, []
+        if works and ev is not None:  # zero-copy on a device: the broadcast reads the parameters
+            self._await_reads(ev.query)
+        elif works and not self._stream_ordered():
+            self._await_reads(lambda: all(w.is_completed() for w in works))
+            for w in works:
+                w.wait()  # complete: surfaces a failed work's error
         if ev is not None:
             torch.cuda.current_stream().wait_event(ev)
-            self._snapshot_done = None
-        works, self._works = self._works, []
-        if works and not isinstance(self.group, comm.RcclComm) and "nccl" not in str(_backend_of(self.group)):
-            for w in works:
-                w.wait()
+
+    def _stream_ordered(self) -> bool:
+        """RCCL (an RcclComm or a torch "nccl" group): collectives are ordered on HIP streams."""
+        return isinstance(self.group, comm.RcclComm) or "nccl" in str(_backend_of(self.group))
+
+    def _await_reads(self, done: Callable[[], bool]) -> None:
+        delay = 0.0005
+        while not done():
+            self._raise()  # the watcher's error (an actor's HTTP error, its own timeout)
+            if self._deadline is not None and time.time() > self._deadline:
+                raise WeightUpdateError(f"weight update {self._version} still reading the parameters "
+                                        f"{self.timeout_s:.0f} s after its request: the next optimizer step "
+                                        "cannot write them (an actor is not receiving)")
+            time.sleep(delay)
+            delay = min(delay * 2, 0.02)
 
     def wait(self) -> None:
         """Block until the in-flight update (if any) has been received by every actor."""

@@ -59,3 +59,36 @@ def test_bucketed_receive_unflattens_into_fused_rows():
                            torch.cat([want[pre + "mlp.gate_proj.weight"], want[pre + "mlp.up_proj.weight"]]))
     for n in ("model.embed_tokens.weight", "model.norm.weight", "model.layers.1.mlp.down_proj.weight"):
         assert torch.equal(model.params[n], want[n])
+
+
+@pytest.mark.parametrize("multi_step", [False, True], ids=["Worker", "MultiStepWorker"])
+def test_v0_worker_unflattens_into_fused_rows(multi_step):
+    """vLLM v0's worker classes (make_worker_class over stand-ins of Worker / MultiStepWorker,
+    tests/test_actor_v0_cpu.py): the bucketed receive resolves the fused layout through
+    direct_target on both runner kinds — the multi-step runner's model is its base runner's
+    (vllm0.py:90-93) — and the one HIP unflatten pass equals the per-name load."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    from test_actor_v0_cpu import MultiStepWorker, Worker
+
+    from pipelinerl_amd.actor import make_worker_class
+    from pipelinerl_amd.weight_update import FlatLayout, HipFlatPacker, ParameterInfo
+
+    cls = make_worker_class(multi_step, MultiStepWorker if multi_step else Worker)
+    trainer = _qwen(0)
+    named = list(trainer.named_parameters())
+    layout = FlatLayout.from_infos([ParameterInfo(name=n, shape=list(p.shape), dtype=str(torch.bfloat16))
+                                    for n, p in named])
+    flat = torch.empty(layout.total, dtype=torch.bfloat16, device="cuda")
+    HipFlatPacker().flatten([p.detach() for _, p in named], layout.offsets, flat)
+    w = cls(_qwen(1), device="cuda")
+    assert (w.model_runner._base_model_runner.model if multi_step else w.model_runner.model) is w._inference_model()
+    assert w._direct_targets(layout) is not None
+    w._apply_flat(flat, layout)
+    ref = cls(_qwen(2), device="cuda")
+    for name, shape, n, off in zip(layout.names, layout.shapes, layout.numels, layout.offsets):
+        ref._load_one(name, flat[off:off + n].view(shape))
+    torch.cuda.synchronize()
+    got, want = w._inference_model().params, ref._inference_model().params
+    assert set(got) == set(want)
+    for fname in got:
+        assert torch.equal(got[fname], want[fname]), fname

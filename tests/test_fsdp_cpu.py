@@ -12,6 +12,7 @@ import os
 import sys
 from pathlib import Path
 
+import pytest
 import torch
 import torch.multiprocessing as mp
 
@@ -91,7 +92,7 @@ def test_fsdp_loop_matches_single_rank_and_resumes(tmp_path):
     assert m["steps"] == 3
 
 
-def _bcast_rank(rank, port_default, port_actor, exp):
+def _bcast_rank(rank, port_default, port_actor, exp, value_head=False):
     sys.path[:0] = [str(ROOT), str(ROOT / "tests"), str(ROOT / "pipelinerl-swe_amd")]
     os.environ["OMP_NUM_THREADS"] = "1"
     import torch.distributed as dist
@@ -110,6 +111,11 @@ def _bcast_rank(rank, port_default, port_actor, exp):
         from pipelinerl_amd.finetune.sharding import shard_model
 
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port_default}", rank=rank, world_size=2)
+        lm = model
+        if value_head:  # the root FSDP unit is the wrapper: it holds the LM's embedding / norm / lm_head
+            from pipelinerl_amd.finetune.value_model import AutoModelForCausalLMWithValueHead
+
+            model = AutoModelForCausalLMWithValueHead(model)
         shard_model(model)
         with torch.no_grad():
             for p in model.parameters():
@@ -126,7 +132,7 @@ def _bcast_rank(rank, port_default, port_actor, exp):
         from torch.distributed.tensor import DTensor
 
         full = {n: p.full_tensor().detach().clone() if isinstance(p, DTensor) else p.detach().clone()
-                for n, p in model.named_parameters()}
+                for n, p in lm.named_parameters()}
         if rank == 0:
             torch.save(full, exp / "trainer.pt")
         dist.destroy_process_group()
@@ -141,10 +147,13 @@ def _bcast_rank(rank, port_default, port_actor, exp):
         torch.save({n: p.detach().clone() for n, p in worker.model_runner.model.params.items()}, exp / "actor.pt")
 
 
-def test_sharded_weight_snapshot_reaches_actor(tmp_path):
+@pytest.mark.parametrize("value_head", [False, True], ids=["lm", "value_head"])
+def test_sharded_weight_snapshot_reaches_actor(tmp_path, value_head):
+    """With a value-head wrapper (reference conf/finetune/ppo.yaml) the wrapper is the FSDP root:
+    the snapshot gathers its units, maps them into the LM's names and leaves the value head out."""
     from test_weight_update_cpu import free_port
 
-    mp.spawn(_bcast_rank, args=(free_port(), free_port(), str(tmp_path)), nprocs=3, join=True)
+    mp.spawn(_bcast_rank, args=(free_port(), free_port(), str(tmp_path), value_head), nprocs=3, join=True)
     want = torch.load(tmp_path / "trainer.pt")
     got = torch.load(tmp_path / "actor.pt")
     assert set(got) == set(want)

@@ -116,6 +116,7 @@ def _actor(port, world, idx, transport, exp, nupdates, use_reference_pg, qwen=Fa
                                                          bucket_bytes=1000 if transport == "bucketed" else 0))
     torch.save({n: p.detach().clone() for n, p in worker.model_runner.model.params.items()},
                Path(exp) / f"actor{idx}_params.pt")
+    os._exit(0)  # no gloo teardown at interpreter exit (it aborted once under a loaded pytest -n 4)
 
 
 def _run(rank, port, world, transport, exp, use_reference_pg, qwen=False):
@@ -242,14 +243,31 @@ def _failing_trainer(port, exp, mode):
     mgr = WeightUpdateManager([url], model, None, pg, transport="bucketed", bucket_bytes=1000, overlap=True,
                               packer=TorchFlatPacker(), write_message=lambda s, m: None, timeout_s=3.0,
                               http_timeout_s=5.0)
+    before = [p.detach().clone() for p in model.parameters()]
     t0 = time.time()
     mgr.send_weight_update(1)
-    err = None
-    try:
-        mgr.wait()
-    except WeightUpdateError as e:
-        err = str(e)
-    Path(exp, "result.json").write_text(json.dumps({"error": err, "elapsed": time.time() - t0}))
+    err, stepped = None, False
+    if mode == "silent_step":
+        # the loop's next step while the broadcast still reads the parameters in place
+        # (finetune_loop.py: backward, clip, wum.poll(), wum.before_optimizer_step(), optimizer.step())
+        assert mgr._flat_params is not None, "a bf16 model is broadcast in place (zero-copy)"
+        opt = torch.optim.AdamW(model.parameters(), lr=1e-2)
+        model(torch.arange(8).view(1, 8)).float().square().mean().backward()
+        try:
+            mgr.poll()
+            mgr.before_optimizer_step()
+            opt.step()
+            stepped = True
+        except WeightUpdateError as e:
+            err = str(e)
+    else:
+        try:
+            mgr.wait()
+        except WeightUpdateError as e:
+            err = str(e)
+    unchanged = all(torch.equal(a, p.detach()) for a, p in zip(before, model.parameters()))
+    Path(exp, "result.json").write_text(json.dumps({"error": err, "elapsed": time.time() - t0, "stepped": stepped,
+                                                    "unchanged": unchanged}))
     os._exit(0)  # the never-matched gloo broadcast stays pending: skip its destructor
 
 
@@ -275,12 +293,15 @@ def _run_failing(rank, port, exp, mode):
         _failing_actor(port, exp)
 
 
-@pytest.mark.parametrize("mode", ["http500", "silent"])
+@pytest.mark.parametrize("mode", ["http500", "silent", "silent_step"])
 def test_failed_actor_makes_the_trainer_raise(tmp_path, mode):
     """SURVEY.md §5 failure row: the reference logs an actor's HTTP error and then blocks in the
     broadcast until the process-group timeout (finetune_loop.py:155-172).  Here an HTTP 500
     raises WeightUpdateError from wait() at once; an actor that never joins the broadcast
-    raises after WeightUpdateManager's timeout (3 s in this test)."""
+    raises after WeightUpdateManager's timeout (3 s in this test).  ``silent_step``: the bf16
+    model is broadcast in place (zero-copy, the default) and the trainer reaches its next
+    optimizer step while the broadcast still reads the parameters — before_optimizer_step raises
+    within the timeout (no host wait on the gloo works) and the parameters stay unwritten."""
     port = free_port()
     mp.spawn(_run_failing, args=(port, str(tmp_path), mode), nprocs=2, join=True)
     r = json.loads((tmp_path / "result.json").read_text())
@@ -288,7 +309,8 @@ def test_failed_actor_makes_the_trainer_raise(tmp_path, mode):
     if mode == "http500":
         assert "500" in r["error"] and r["elapsed"] < 3.0
     else:
-        assert "not completed" in r["error"] and 2.5 < r["elapsed"] < 10.0
+        assert ("not completed" in r["error"] or "still reading" in r["error"]) and 2.5 < r["elapsed"] < 4.5, r
+    assert r["unchanged"] and not r["stepped"]
 
 
 def test_f4_request_and_actor_group_layout():
@@ -340,3 +362,18 @@ def test_f4_request_and_actor_group_layout():
             assert all(x[1] == g["weight_update_group_size"] for x in seen)
     finally:
         actor_mod.torch_utils.init_extra_process_group = orig
+
+
+def test_weight_snapshot_follows_flat_parameters(caplog):
+    """finetune.flat_parameters=false opts out of re-homing: the snapshot defaults to the staging
+    copy, and an explicit zero_copy falls back to it with a warning instead of re-homing the
+    parameters after the optimizer exists."""
+    from pipelinerl_amd.config import Cfg
+    from pipelinerl_amd.finetune_loop import weight_snapshot_mode
+
+    assert weight_snapshot_mode(Cfg.wrap({})) == "zero_copy"
+    assert weight_snapshot_mode(Cfg.wrap({"flat_parameters": False})) == "copy"
+    assert weight_snapshot_mode(Cfg.wrap({"weight_snapshot": "copy"})) == "copy"
+    with caplog.at_level("WARNING"):
+        assert weight_snapshot_mode(Cfg.wrap({"flat_parameters": False, "weight_snapshot": "zero_copy"})) == "copy"
+    assert "flat_parameters" in caplog.text
