@@ -44,8 +44,9 @@ copy's own duration.  At N > 1, "communicators" first checks that every communic
 carries, by an all-reduce of ones) the intended rank count: the DP group, the CPU control group and a
 prl_comm RCCL communicator (ncclCommCount); the split pipeline's DP and actor groups are checked in
 its own probe ("split_pipeline.groups").  At N = 1, "loss_head_fp32": the same C2 micro-batch with
-fp32 logits (Accelerate's upcast regime; the part-resident grpo_fwd_hybrid_f32), its kernel time
-and fraction of the HBM peak on 2 x 4 x T x V algorithmic bytes.
+fp32 logits (Accelerate's upcast regime; grpo_fwd_pair_f32, each row resident over two CUs, with the
+round-4 part-resident kernel alternated beside it), its kernel time and fraction of the HBM peak on
+2 x 4 x T x V algorithmic bytes.
 
 Prints ONE JSON line (rank 0).  roofline.achieved = algorithmic bytes per launch
 (T*V*2 read + T*V*2 dlogits write + 37*T side data) / the average duration
@@ -76,11 +77,13 @@ HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md); measured float4 copy
 SIDE_BYTES_PER_TOKEN = 37  # ids 8 + old 4 + ref 4 + adv 4 + w 4 + mask 1 + lp/H/tok_loss 12
 
 
-def fp32_loss_head_probe(T: int, V: int, device, iters: int = 8, warmup: int = 2) -> dict:
+def fp32_loss_head_probe(T: int, V: int, device, iters: int = 8, warmup: int = 2, rounds: int = 2) -> dict:
     """C2's micro-batch with fp32 logits (Accelerate's mixed precision upcasts them,
-    finetune_loop.py:381-385): the fused loss head's forward + gradient (the part-resident
-    grpo_fwd_hybrid_f32 at Qwen2.5 vocabularies), HIP events on its stream; algorithmic bytes =
-    logits read once + dlogits written once + side data."""
+    finetune_loop.py:381-385): the fused loss head's forward + gradient, HIP events on its stream;
+    algorithmic bytes = logits read once + dlogits written once + side data.
+    At Qwen2.5 vocabularies the product kernel is grpo_fwd_pair_f32<19> (each row fully resident
+    over a pair of CUs); the round-4 part-resident grpo_fwd_hybrid_f32<19, 9> (PRL_F32_PAIR=0) is
+    timed in alternation beside it, same process and buffers."""
     from pipelinerl_amd.finetune.rl.fused import GrpoParams, grpo_loss
 
     lb, fields = make_workload(T, V, seq=2048, prompt=256, seed=4321, device=device)
@@ -89,34 +92,53 @@ def fp32_loss_head_probe(T: int, V: int, device, iters: int = 8, warmup: int = 2
     torch.cuda.empty_cache()
     params = GrpoParams(policy_loss="ppo", epsilon=4.0, kl_coef=0.0, entropy_coef=0.0, clamp_log_ratio=5.0,
                         temperature=1.0, batch_size=4096.0)
-    times = []
-    for i in range(warmup + iters):
-        logits.grad = None
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        loss, stats, _ = grpo_loss(logits, fields, params)
-        e1.record()
-        loss.backward()
-        stats.cpu()
-        if i >= warmup:
-            times.append(e0.elapsed_time(e1))
-    ms = float(np.median(times))
+    times: dict[str, list[float]] = {"pair": [], "hybrid": []}
+    prev = os.environ.get("PRL_F32_PAIR")
+    try:
+        for _ in range(rounds):
+            for arm in ("pair", "hybrid"):
+                os.environ["PRL_F32_PAIR"] = "1" if arm == "pair" else "0"  # read per launch
+                for i in range(warmup + iters):
+                    logits.grad = None
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    loss, stats, _ = grpo_loss(logits, fields, params)
+                    e1.record()
+                    loss.backward()
+                    stats.cpu()
+                    if i >= warmup:
+                        times[arm].append(e0.elapsed_time(e1))
+    finally:
+        if prev is None:
+            os.environ.pop("PRL_F32_PAIR", None)
+        else:
+            os.environ["PRL_F32_PAIR"] = prev
+    ms = float(np.median(times["pair"]))
+    ms_h = float(np.median(times["hybrid"]))
     alg = 2.0 * T * V * 4 + SIDE_BYTES_PER_TOKEN * T
     del logits, fields
     torch.cuda.empty_cache()
-    traffic = None  # HBM bytes per launch from the committed PMC passes (tools/profile_bench.sh)
+    traffic = traffic_h = None  # HBM bytes per launch from the committed PMC passes (tools/profile_bench.sh)
+    src = "r05_fp32_pmc.json"
     try:
-        pmc = json.loads((ROOT / "profiles" / "r04_fp32_pmc.json").read_text())["per_launch_median"]
-        hyb = next(v for k, v in pmc.items() if "hybrid" in k)
+        pmc = json.loads((ROOT / "profiles" / src).read_text())["per_launch_median"]
         if T == 65536 and V == 151936:
-            traffic = hyb["fetch_size_bytes"] + hyb["write_size_bytes"]
-    except (OSError, KeyError, StopIteration, ValueError):
+            for k, v in pmc.items():
+                if "pair_f32" in k:
+                    traffic = v["fetch_size_bytes"] + v["write_size_bytes"]
+                elif "hybrid" in k:
+                    traffic_h = v["fetch_size_bytes"] + v["write_size_bytes"]
+    except (OSError, KeyError, ValueError):
         pass
-    return {"kernel": "grpo_fwd_hybrid_f32<19, 9> (+stats/finalize) per prl_grpo_forward", "tokens": T, "vocab": V,
-            "logits_dtype": "fp32", "kernel_ms": round(ms, 4), "algorithmic_bytes": alg,
+    return {"kernel": "grpo_fwd_pair_f32<19> (+slot memset, stats/finalize) per prl_grpo_forward", "tokens": T,
+            "vocab": V, "logits_dtype": "fp32", "kernel_ms": round(ms, 4), "algorithmic_bytes": alg,
             "achieved_GBps": round(alg / ms / 1e6, 1), "frac": round(alg / ms / 1e6 / HBM_PEAK_GBS, 4),
-            "traffic": traffic, "traffic_source": "r04_fp32_pmc.json" if traffic else None,
-            "tokens_per_s": round(T / ms * 1e3, 1), "iters": iters}
+            "traffic": traffic, "traffic_over_algorithmic": round(traffic / alg, 4) if traffic else None,
+            "traffic_source": src if traffic else None,
+            "tokens_per_s": round(T / ms * 1e3, 1), "iters": iters * rounds,
+            "hybrid": {"kernel": "grpo_fwd_hybrid_f32<19, 9> (PRL_F32_PAIR=0, alternated)", "kernel_ms": round(ms_h, 4),
+                       "frac": round(alg / ms_h / 1e6 / HBM_PEAK_GBS, 4),
+                       "traffic_over_algorithmic": round(traffic_h / alg, 4) if traffic_h else None}}
 
 
 def make_workload(T: int, V: int, seq: int, prompt: int, seed: int, device):
@@ -529,7 +551,7 @@ def main():
                                                                       layers=4 if rehearse else None))
     fp32 = None
     if world == 1 and not args.no_fp32:
-        # the loss head in the fp32-logits regime (Accelerate's upcast): the part-resident kernel
+        # the loss head in the fp32-logits regime (Accelerate's upcast): the pair kernel (+ the hybrid A/B)
         fp32 = optional("loss_head_fp32", lambda: fp32_loss_head_probe(T, V, dev))
     fsdp = None
     if world >= 4 and not args.no_fsdp:

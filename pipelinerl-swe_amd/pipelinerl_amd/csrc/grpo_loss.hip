@@ -20,6 +20,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+#include <map>
+#include <mutex>
 #include <type_traits>
 #include <utility>
 
@@ -738,6 +741,189 @@ __global__ __launch_bounds__(1024) void grpo_fwd_hybrid_f32(KArgs a) {
   }
 }
 
+// fp32 rows, fully resident: each row is split over a PAIR of workgroups (one per CU), each holding
+// its half-row (297 KiB at V = 151 936: NV = 19 vectors per lane, as the bf16 kernel holds a whole
+// bf16 row) in VGPRs, so no byte of the row is read twice.  The two halves exchange their partial
+// (max, sum 2^y, sum 2^y y) once per row through a 16-B tagged granule in global memory — one sc1
+// store of {m, s, w, tag} by one lane, sc1 polls by the partner's lane 0 (the data-tagged hand-off
+// of MI355X_MICROARCH.md's price list, handoff-1to1) — and both combine the two partials in half
+// order, so both hold bit-identical row statistics.  Pairs are blocks b and b ^ 8 (one XCD under the
+// round-robin placement: speed only).  Every spin is bounded: a half whose partner has not published
+// within PairArgs::spin_ticks of the realtime clock (100 MHz) computes the partner's partial itself
+// from HBM (the same loads and arithmetic in the same order: the same bits), so a launch that shares
+// the chip with other kernels still completes.  Slots are zeroed by the host before each launch
+// (tag = the pair's row iteration + 1).
+struct PairArgs {
+  uint32_t* slots;      // [pairs][2 halves][2 parities] x 4 words {m, s, w, tag}
+  int64_t slot_bytes;   // bytes of the slot array (its buffer descriptor's range)
+  int64_t spin_ticks;   // realtime ticks a half waits for its partner before computing its partial
+};
+#ifndef PRL_PAIR_SPIN_TICKS
+#define PRL_PAIR_SPIN_TICKS 20000  // 200 us
+#endif
+constexpr int kPairMinNV = 8, kPairMaxNV = 19;  // above 19 the registers spill (hybrid kernel there)
+constexpr int kSc1 = 16;  // aux bit of buffer_load / buffer_store: sc1 (bypass the CU's L1; write through)
+
+// the (m, s, w) state of a half row: its NV vectors per lane from registers (FROM_REGS) or streamed
+// from HBM in the same order, then the wave and block reductions.  The same code computes both, so a
+// half's own partial and the one its partner computes for it on a timeout are the same bits.
+template <int NV, bool FROM_REGS>
+__device__ __forceinline__ Lse half_state(const f32x4 (&buf)[NV], __amdgpu_buffer_rsrc_t rs, int voff, bool last_ok,
+                                          float c, float (*red)[3], int lane, int wid) {
+  constexpr int BLOCK = 1024, NW = BLOCK / 64, VSTRIDE = BLOCK * 16;
+  const f32x4 pad = {kEmptyMax, kEmptyMax, kEmptyMax, kEmptyMax};
+  Lse st = lse_empty();
+  if constexpr (FROM_REGS) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const f32x4 v = (k == NV - 1 && !last_ok) ? pad : buf[k];
+      const float x[4] = {v[0], v[1], v[2], v[3]};
+      lse_add<4>(st, x, c);
+    }
+  } else {
+    constexpr int U = 2;  // few extra registers beside the resident half (this is the rare path)
+#pragma unroll
+    for (int k0 = 0; k0 < NV; k0 += U) {
+      f32x4 t[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (k0 + u < NV) t[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, (k0 + u) * VSTRIDE, kLoadAux));
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (k0 + u < NV) {
+          const f32x4 v = (k0 + u == NV - 1 && !last_ok) ? pad : t[u];
+          const float x[4] = {v[0], v[1], v[2], v[3]};
+          lse_add<4>(st, x, c);
+        }
+      }
+    }
+  }
+  st = wave_reduce_lse(st, c);
+  if (lane == 0) {
+    red[wid][0] = st.m;
+    red[wid][1] = st.s;
+    red[wid][2] = st.w;
+  }
+  __syncthreads();
+  return block_combine<NW>(red, c);
+}
+
+template <int NV>
+__global__ __launch_bounds__(1024) void grpo_fwd_pair_f32(KArgs a, PairArgs pa) {
+  constexpr int BLOCK = 1024, NW = BLOCK / 64, VSTRIDE = BLOCK * 16;
+  __shared__ float red[2][NW][3];
+  __shared__ float red2[NW][3];   // the partner partial, when this half computes it
+  __shared__ uint32_t xch[2][4];  // the partner's published partial and whether it arrived
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int b = blockIdx.x;
+  const int h = (b >> 3) & 1;                          // which half of the row
+  const int64_t npairs = gridDim.x >> 1;               // the host launches a multiple of 16 blocks
+  const int64_t p = (int64_t)(b >> 4) * 8 + (b & 7);   // pair: blocks b and b ^ 8
+  const int64_t nrows = fwd_rows(a);
+  const int nvec = (int)(a.V >> 2);
+  const int n0 = (nvec + 1) >> 1;                      // half 0: vectors [0, n0), half 1: [n0, nvec)
+  const int nmine = h ? nvec - n0 : n0, npart = h ? n0 : nvec - n0;
+  const int64_t off_mine = h ? (int64_t)n0 * 16 : 0, off_part = h ? 0 : (int64_t)n0 * 16;
+  const int col0 = h ? n0 * 4 : 0;                     // first column of this half
+  const float c = kLog2e / a.temperature;
+  const float inv_t = 1.0f / a.temperature;
+  const float* lg = static_cast<const float*>(a.logits);
+  float* dl = static_cast<float*>(a.dlogits);
+  const int voff = tid * 16;
+  const bool last_ok = (NV - 1) * BLOCK + tid < nmine;  // only vector NV-1 can be partial
+  const bool last_ok_part = (NV - 1) * BLOCK + tid < npart;
+  const auto slots = __builtin_amdgcn_make_buffer_rsrc(pa.slots, 0, (int)pa.slot_bytes, 0x00020000);
+  const int my_slot = (int)((p * 2 + h) * 2) * 16, partner_slot = (int)((p * 2 + (h ^ 1)) * 2) * 16;
+  f32x4 buf[NV];
+  auto half_rsrc = [&](int64_t lrow, int64_t off, int n) {
+    return row_rsrc(reinterpret_cast<const char*>(lg + lrow * a.ld) + off, (int64_t)n * 16);
+  };
+  int64_t i = p;
+  if (i < nrows) {
+    int64_t lrow, tok, qo;
+    map_row(a, perm_row(i, nrows), lrow, tok, qo);
+    const auto rs = half_rsrc(lrow, off_mine, nmine);
+#pragma unroll
+    for (int k = 0; k < NV; ++k)
+      buf[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, k * VSTRIDE, kLoadAux));
+  }
+  uint32_t it = 0;
+  for (; i < nrows; i += npairs, ++it) {
+    const int par = (int)(it & 1);
+    const uint32_t tag = it + 1;
+    int64_t lrow, tok, qo;
+    map_row<RowLd>(a, perm_row(i, nrows), lrow, tok, qo);
+    const int64_t tid_raw = RowLd::ld(a.input_ids, tok);
+    TokIn tin = tok_in<RowLd>(a, tok);
+    const bool bad_id = (uint64_t)tid_raw >= (uint64_t)a.V;
+    const int64_t tgt = bad_id ? -1 : tid_raw;
+    float xr = row_logit(lg + lrow * a.ld, bad_id ? 0 : tid_raw);
+    pin_sgpr(tin, xr);
+    const float xt = bad_id ? __builtin_nanf("") : xr;
+
+    // ---- pass 1: this half's state from registers, published for the partner
+    const Lse mine = half_state<NV, true>(buf, slots, voff, last_ok, c, red[par], lane, wid);  // (rsrc unused)
+    if (tid == 0) {
+      const u32x4 g = {__float_as_uint(mine.m), __float_as_uint(mine.s), __float_as_uint(mine.w), tag};
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, g),
+                                             slots, my_slot + par * 16, 0, kSc1);
+      u32x4 v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(slots, partner_slot + par * 16, 0, kSc1));
+      if (v[3] != tag) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (v[3] != tag && (int64_t)(__builtin_amdgcn_s_memrealtime() - t0) < pa.spin_ticks) {
+          __builtin_amdgcn_s_sleep(1);
+          asm volatile("" ::: "memory");  // a fresh load every turn
+          v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(slots, partner_slot + par * 16, 0, kSc1));
+        }
+      }
+      xch[par][0] = v[0];
+      xch[par][1] = v[1];
+      xch[par][2] = v[2];
+      xch[par][3] = v[3] == tag ? 1u : 0u;
+    }
+    __syncthreads();
+    Lse part;
+    if (xch[par][3]) {
+      part = Lse{__uint_as_float(xch[par][0]), __uint_as_float(xch[par][1]), __uint_as_float(xch[par][2])};
+    } else {  // the partner is late (not resident, or behind): its partial from HBM (block-uniform branch)
+      part = half_state<NV, false>(buf, half_rsrc(lrow, off_part, npart), voff, last_ok_part, c, red2, lane, wid);
+    }
+    const Lse tot = h == 0 ? lse_combine(mine, part, c) : lse_combine(part, mine, c);
+    const float l2s = log2f(tot.s);
+    const float M = tot.m;
+    const float lse = M * inv_t + kLn2 * l2s;
+    const float H = kLn2 * (l2s - tot.w / tot.s);
+    const float lp = (xt - M) * inv_t - kLn2 * l2s;
+    const TokGrad core = row_epilogue(a, qo, tin, lp, H, lse, M, l2s, h == 0 && tid == 0);
+#pragma unroll
+    for (int k = 0; k < NV; ++k) asm volatile("" : "+v"(buf[k]));
+
+    // ---- pass 2: this half's gradient from registers, then (stores retired) the next half-row
+    const int64_t in = i + npairs;
+    const bool has_next = in < nrows;
+    if (a.write_grad) {
+      const auto ws = row_rsrc(reinterpret_cast<char*>(dl + lrow * a.ld) + off_mine, (int64_t)nmine * 16);
+      const float alpha = -(core.g_lp + core.g_h * H) * inv_t;
+      const float beta = -core.g_h * kLn2 * inv_t;
+      const float gadd = core.g_lp * inv_t;
+      const bool zero_row = (core.g_lp == 0.f && core.g_h == 0.f);
+      const int rel0 = (int)(tgt < 0 ? -(1 << 30) : tgt - col0) - tid * 4;  // target - this lane's first column
+#pragma unroll
+      for (int k = 0; k < NV; ++k)
+        hyb_store(ws, voff, k * VSTRIDE, rel0 - k * BLOCK * 4, buf[k], zero_row, c, M, l2s, alpha, beta, gadd);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    if (has_next) {
+      int64_t nl, nt, nq;
+      map_row<RowLd>(a, perm_row(in, nrows), nl, nt, nq);
+      const auto rn = half_rsrc(nl, off_mine, nmine);
+#pragma unroll
+      for (int k = 0; k < NV; ++k)
+        buf[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rn, voff, k * VSTRIDE, kLoadAux));
+    }
+  }
+}
+
 // gradient pass from saved per-row coefficients for the upstream gradient *up (device);
 // skip_if_one: dlogits already holds the gradient for *up == grad_scale (fused forward)
 template <typename T, int VEC>
@@ -995,6 +1181,77 @@ static hipError_t launch_resident_nv(int nv, const KArgs& a, int grid, hipStream
   return launch_resident_table(nv, a, grid, s, std::make_integer_sequence<int, kMaxNV>{});
 }
 
+// the fp32 pair kernel: one zeroed slot array per (device, stream), so launches on different streams
+// never share hand-off slots; [pairs][2][2] granules of 16 B for up to 1024 CUs
+constexpr int kPairMaxCUs = 1024;
+constexpr size_t kPairSlotBytes = (size_t)(kPairMaxCUs / 2) * 2 * 2 * 16;
+static std::mutex g_slot_mu;
+static std::map<std::pair<int, hipStream_t>, void*> g_pair_slots;
+
+static hipError_t pair_slots(int dev, hipStream_t s, void** out) {
+  std::lock_guard<std::mutex> lk(g_slot_mu);
+  auto key = std::make_pair(dev, s);
+  auto it = g_pair_slots.find(key);
+  if (it == g_pair_slots.end()) {
+    void* p = nullptr;
+    const hipError_t e = hipMalloc(&p, kPairSlotBytes);
+    if (e != hipSuccess) return e;
+    it = g_pair_slots.emplace(key, p).first;
+  }
+  *out = it->second;
+  return hipSuccess;
+}
+
+// PRL_F32_PAIR=0 keeps the part-resident kernel for fp32 rows (A/B); PRL_PAIR_SPIN_TICKS sets the
+// partner wait (tests force the from-HBM partial with 0)
+static bool pair_f32_enabled() {
+  const char* e = getenv("PRL_F32_PAIR");  // read per launch: tests run both kernels in one process
+  return !(e && e[0] == '0');
+}
+static int64_t pair_spin_ticks() {
+  const char* e = getenv("PRL_PAIR_SPIN_TICKS");  // read per launch: tests switch it
+  return e ? atoll(e) : (int64_t)PRL_PAIR_SPIN_TICKS;
+}
+
+template <int NV>
+static hipError_t launch_pair(const KArgs& a, const PairArgs& pa, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(grpo_fwd_pair_f32<NV>, dim3(grid), dim3(1024), 0, s, a, pa);
+  return hipGetLastError();
+}
+template <int... NVs>
+static hipError_t launch_pair_table(int nv, const KArgs& a, const PairArgs& pa, int grid, hipStream_t s,
+                                    std::integer_sequence<int, NVs...>) {
+  hipError_t e = hipErrorInvalidValue;
+  ((nv == NVs + kPairMinNV ? (e = launch_pair<NVs + kPairMinNV>(a, pa, grid, s), true) : false) || ...);
+  return e;
+}
+
+// fp32 rows of 16-B vectors whose halves fit NV in [kPairMinNV, kPairMaxNV] vectors per lane: the
+// pair kernel over min(#CUs, pairs needed) blocks, rounded down to a multiple of 16 (pairs b, b ^ 8)
+static int pair_nv(int64_t V) {
+  const int64_t half = ((V >> 2) + 1) >> 1;
+  const int64_t nv = (half + 1023) / 1024;
+  return (nv >= kPairMinNV && nv <= kPairMaxNV) ? (int)nv : 0;
+}
+static hipError_t launch_pair_rows(const KArgs& a, int nv, int64_t nrows, int cus, int dev, hipStream_t s) {
+  int grid = cus < kPairMaxCUs ? cus : kPairMaxCUs;
+  const int64_t need = 2 * nrows;
+  if (need < grid) grid = (int)need;
+  grid = (grid + 15) / 16 * 16;
+  if (grid > cus) grid = cus / 16 * 16;
+  if (grid < 16) grid = 16;
+  PairArgs pa{};
+  void* slots = nullptr;
+  hipError_t e = pair_slots(dev, s, &slots);
+  if (e != hipSuccess) return e;
+  pa.slots = static_cast<uint32_t*>(slots);
+  pa.slot_bytes = (int64_t)kPairSlotBytes;
+  pa.spin_ticks = pair_spin_ticks();
+  e = hipMemsetAsync(slots, 0, (size_t)(grid / 2) * 2 * 2 * 16, s);  // tags restart at 1 every launch
+  if (e != hipSuccess) return e;
+  return launch_pair_table(nv, a, pa, grid, s, std::make_integer_sequence<int, kPairMaxNV - kPairMinNV + 1>{});
+}
+
 // per-row outputs (+ dlogits); the row arrays are indexed by batch row q
 static int fill_outputs(KArgs& a, const PrlGrpoBatch* b, const PrlGrpoParams* p, const PrlGrpoOutputs* out,
                         bool need_stats) {
@@ -1038,6 +1295,8 @@ static hipError_t launch_rows(const KArgs& a, const PrlGrpoBatch* b, const PrlGr
     hipLaunchKernelGGL((grpo_fwd_stream<uint16_t, 1>), dim3(grid), dim3(256), 0, s, a);
   } else if (b->V % 4 == 0 && b->ld % 4 == 0 && aligned16(b->logits) &&
              (!p->write_grad || aligned16(out->dlogits))) {
+    const int pnv = pair_f32_enabled() ? pair_nv(b->V) : 0;
+    if (pnv > 0) return launch_pair_rows(a, pnv, nrows, cus, dev, s);  // the row fully resident over two CUs
     if (PRL_HYB_NL >= 0 && b->V / 4 >= (int64_t)(kHybNR + kHybNL) * 1024) {  // a tail to stream: the row part-resident
       const int g1 = (int)(nrows < cus ? nrows : cus);  // one workgroup per CU (the LDS slab)
       hipLaunchKernelGGL((grpo_fwd_hybrid_f32<kHybNR, kHybNL>), dim3(g1), dim3(1024), 0, s, a);

@@ -41,6 +41,8 @@ class Worker:
 
         self.rank = rank
         self.device = torch.device(device)
+        if self.device.type == "cuda" and self.device.index is None:  # as vLLM's worker: an indexed device
+            self.device = torch.device("cuda", torch.cuda.current_device())
         module.to(self.device)
         self.model_config = types.SimpleNamespace(dtype=next(module.parameters()).dtype)
         self.model_runner = ModelRunner(StackedParamsModel(module))  # vLLM's fused Qwen2 layout

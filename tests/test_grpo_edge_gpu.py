@@ -202,17 +202,32 @@ def test_target_columns_at_vector_edges(ent):
         assert abs(got - want) <= 1e-2 * abs(want) + 1e-8, (r, cols[r], got, want)
 
 
-# fp32 logits at a Qwen2.5 vocabulary take the part-resident kernel (grpo_fwd_hybrid_f32<19, 9>):
-# columns [0, 77 824) in registers, [77 824, 114 688) in LDS, the rest streamed and re-read
+# fp32 logits at a Qwen2.5 vocabulary take the pair kernel (grpo_fwd_pair_f32<19>: the row split
+# over two workgroups, columns [0, 75 968) and [75 968, 151 936), each half in registers, 19 vectors
+# per lane, the last one partial) or, with PRL_F32_PAIR=0, the part-resident one
+# (grpo_fwd_hybrid_f32<19, 9>: columns [0, 77 824) in registers, [77 824, 114 688) in LDS, the rest
+# streamed and re-read).  PRL_PAIR_SPIN_TICKS=0: a half never waits for its partner's partial and
+# computes it from HBM whenever it has not arrived yet (the bounded-spin path).
 HYB_EDGES = [0, 3, 4, 77823, 77824, 77827, 114687, 114688, 114691, 151935]
+PAIR_EDGES = [0, 3, 4, 73723, 73727, 73728, 75967, 75968, 75971, 75972, 149503, 149504, 151935]
+F32_KERNELS = {"pair": {}, "pair_nowait": {"PRL_PAIR_SPIN_TICKS": "0"}, "hybrid": {"PRL_F32_PAIR": "0"}}
+
+
+@pytest.fixture(params=list(F32_KERNELS))
+def f32_kernel(request, monkeypatch):
+    for k, v in F32_KERNELS[request.param].items():
+        monkeypatch.setenv(k, v)
+    return request.param
 
 
 @pytest.mark.parametrize("ent", [0.0, 0.01])
-def test_fp32_part_resident_targets_at_region_edges(ent):
-    """Targets on both sides of the register / LDS / streamed boundaries, fp32 at 1e-4."""
-    T, V = 12, 151936
+def test_fp32_resident_targets_at_region_edges(ent, f32_kernel):
+    """Targets on both sides of the half / vector boundaries (pair kernel) and of the register /
+    LDS / streamed boundaries (hybrid), fp32 at 1e-4."""
+    edges = HYB_EDGES if f32_kernel == "hybrid" else PAIR_EDGES
+    T, V = len(edges) + 2, 151936
     b = _batch(T, V, seed=11, lens=[T], prompts=[1])
-    for r, col in enumerate(HYB_EDGES):
+    for r, col in enumerate(edges):
         b["input_ids"][0, 1 + r] = col
         if b["labels"][0, 1 + r] != -100:
             b["labels"][0, 1 + r] = col
@@ -220,22 +235,23 @@ def test_fp32_part_resident_targets_at_region_edges(ent):
     cfg = dict(CFG, entropy_bonus=ent, final_entropy_bonus=ent)
     _, d = _cmp(lg, b, cfg, dtype=torch.float32)
     o = grpo_oracle.rl_step_oracle(lg, b, cfg, 0, 10)
-    for r, col in enumerate(HYB_EDGES):
+    for r, col in enumerate(edges):
         if b["labels"][0, 1 + r] != -100:
             assert rel_close(d[0, r, col], o["dlogits"][0, r, col], 1e-4, 1e-7)[0], col
 
 
-def test_fp32_part_resident_many_rows_per_workgroup_and_non_finite():
-    """~2.3 rows per workgroup (rows with and without a successor on the same CU, the LDS slab
-    reused row after row), a -inf in the streamed tail and one in the LDS share of two rows; two
-    runs bitwise identical."""
+def test_fp32_resident_many_rows_per_workgroup_and_non_finite(f32_kernel):
+    """~2.3 rows per workgroup pair (hybrid: per workgroup) — rows with and without a successor,
+    slots / the LDS slab reused row after row —, a -inf in each half of one row each; two runs
+    bitwise identical (for the pair kernel also against the run that never waits: the partner's
+    partial computed from HBM is the same bits as the one it publishes)."""
     V = 151936
     lens = [150, 200, 251]
     T = sum(lens)
     b = _batch(T, V, seed=12, lens=lens, prompts=[20, 30, 40])
     lg = np.random.default_rng(12).normal(0, 2.5, (1, T, V)).astype(np.float32)
     tgt = b["input_ids"][0, 1:]
-    for r, col in ((40, 140000), (41, 90000)):
+    for r, col in ((40, 140000), (41, 30000)):
         lg[0, r, col if col != tgt[r] else col + 1] = -np.inf
     loss, stats, d1 = _run(lg, b, dtype=torch.float32)
     o = grpo_oracle.rl_step_oracle(lg, b, CFG, 0, 10)
@@ -247,9 +263,18 @@ def test_fp32_part_resident_many_rows_per_workgroup_and_non_finite():
     assert np.all(d1[0, [40, 41]] == 0)
     _, _, d2 = _run(lg, b, dtype=torch.float32)
     assert np.array_equal(d1, d2)
+    if f32_kernel == "pair":
+        import os
+
+        os.environ["PRL_PAIR_SPIN_TICKS"] = "0"
+        try:
+            loss3, stats3, d3 = _run(lg, b, dtype=torch.float32)
+        finally:
+            del os.environ["PRL_PAIR_SPIN_TICKS"]
+        assert np.array_equal(d1, d3) and loss3 == loss and stats3 == stats
 
 
-def test_fp32_part_resident_strided_rows():
+def test_fp32_resident_strided_rows(f32_kernel):
     """fp32 logits sliced out of a wider buffer (row stride V + 64) at a Qwen2.5 vocabulary."""
     from pipelinerl_amd.finetune.rl import RLConfig, rl_step
 
@@ -273,3 +298,14 @@ def test_fp32_part_resident_strided_rows():
     g = base.grad.cpu().numpy()
     assert rel_close(g[:, :, :V], o["dlogits"], 1e-4, 1e-7)[0]
     assert np.all(g[:, :, V:] == 0)
+
+
+@pytest.mark.parametrize("V", [65536, 65536 + 4, 114688, 152064, 196608])
+def test_fp32_pair_kernel_vocab_range(V):
+    """Vocabularies across the pair kernel's range (half rows of 8 .. 19 vectors per lane; odd
+    vector counts give halves of different lengths) and one past it (196 608: the hybrid kernel),
+    a few rows each, fp32 at 1e-4."""
+    T = 6
+    b = _batch(T, V, seed=14)
+    lg = np.random.default_rng(14).normal(0, 2, (1, T, V)).astype(np.float32)
+    _cmp(lg, b, dtype=torch.float32)

@@ -3,6 +3,11 @@
 re-reads the row) at the same packed micro-batch; algorithmic bytes = logits read once + dlogits
 written once (measurement tool).
 
+With ``--f32-kernels``: the fp32 loss head's kernels alternated in one process at C2 (the row split
+over a pair of workgroups, fully resident — the default —; PRL_F32_PAIR=0: the part-resident hybrid;
+PRL_PAIR_SPIN_TICKS=0: the pair kernel whose halves never wait for each other's partial), medians
+of HIP-event times per arm and round, one JSON line per arm.
+
 With ``--inplace``: the bf16 loss head writing dlogits to its own buffer (the bench's form) vs over
 the logits it has just read (dlogits aliasing batch->logits, allowed by include/prl_hip.h): same
 bytes, same kernel, alternating arms, HIP events on the launch stream.
@@ -25,16 +30,66 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 
 
+def f32_kernels_ab(a):
+    import os
+
+    from pipelinerl_amd.finetune.rl.fused import GrpoParams, grpo_loss
+
+    dev = torch.device("cuda", 0)
+    params = GrpoParams(policy_loss="ppo", epsilon=4.0, kl_coef=0.0, entropy_coef=0.0, clamp_log_ratio=5.0,
+                        temperature=1.0, batch_size=4096.0)
+    lb, fields = bench.make_workload(a.tokens, a.vocab, 2048, 256, 4321, dev)
+    logits = lb.detach().float().requires_grad_(True)
+    del lb
+    torch.cuda.empty_cache()
+    arms = {"pair": {"PRL_F32_PAIR": "1"}, "hybrid": {"PRL_F32_PAIR": "0"},
+            "pair_nowait": {"PRL_F32_PAIR": "1", "PRL_PAIR_SPIN_TICKS": "0"}}
+    alg = 2.0 * a.tokens * a.vocab * 4 + bench.SIDE_BYTES_PER_TOKEN * a.tokens
+    res = {k: [] for k in arms}
+    ref = None
+    for r in range(a.rounds):
+        for name, env in arms.items():
+            os.environ.pop("PRL_PAIR_SPIN_TICKS", None)
+            os.environ.update(env)
+            times = []
+            for i in range(8):
+                logits.grad = None
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                loss, stats, _ = grpo_loss(logits, fields, params)
+                e1.record()
+                loss.backward()
+                torch.cuda.synchronize()
+                if i >= 2:
+                    times.append(e0.elapsed_time(e1))
+            out = (float(loss), logits.grad[0, :64].clone())
+            if ref is None:
+                ref = out
+            same = out[0] == ref[0] and torch.equal(out[1], ref[1])
+            res[name].append(float(np.median(times)))
+            print(json.dumps({"round": r, "arm": name, "ms": round(float(np.median(times)), 4),
+                              "frac": round(alg / np.median(times) / 1e6 / bench.HBM_PEAK_GBS, 4),
+                              "loss": out[0], "same_as_first_arm": bool(same)}), flush=True)
+    for name, v in res.items():
+        ms = float(np.median(v))
+        print(json.dumps({"arm": name, "median_ms": round(ms, 4), "frac": round(alg / ms / 1e6 / bench.HBM_PEAK_GBS, 4),
+                          "tokens": a.tokens, "vocab": a.vocab, "algorithmic_bytes": alg}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tokens", type=int, default=65536)
     ap.add_argument("--vocab", type=int, default=151936)
     ap.add_argument("--inplace", action="store_true", help="separate vs aliased dlogits A/B (bf16)")
+    ap.add_argument("--f32-kernels", action="store_true", help="pair vs hybrid fp32 kernels, alternated")
+    ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--dl-offsets", default=None,
                     help="comma-separated byte offsets of the dlogits buffer's start (bf16 A/B of HBM placement)")
     a = ap.parse_args()
     if a.inplace:
         return inplace_ab(a)
+    if a.f32_kernels:
+        return f32_kernels_ab(a)
     if a.dl_offsets:
         return offsets_ab(a, [int(x) for x in a.dl_offsets.split(",")])
     from pipelinerl_amd.finetune.rl.fused import GrpoParams, grpo_loss

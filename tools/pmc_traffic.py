@@ -2,6 +2,8 @@
 bench.py into the per-launch HBM traffic JSON that bench.py's roofline reads.
 
   python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write profiles/r01_pmc_traffic.json
+  python tools/pmc_traffic.py --fp32 gpurun_out/pmc_fetch gpurun_out/pmc_write profiles/r05_fp32_pmc.json
+      (the bench's loss_head_fp32 probe: every fp32 loss-head kernel found, per-launch medians)
 
 Corrections per /opt/skills/guides/MI355X_MICROARCH.md (HBM section, gfx950): FETCH_SIZE is in
 KB and counts 16-B/lane streaming reads at half rate (x1024 x2); WRITE_SIZE is in KB (x1024).
@@ -50,5 +52,41 @@ def main(fetch_dir: str, write_dir: str, out: str) -> None:
     print(json.dumps(res))
 
 
+def fp32_main(fetch_dir: str, write_dir: str, out: str) -> None:
+    """Per-launch medians of every fp32 loss-head kernel the two passes traced (pair / hybrid)."""
+    import statistics
+
+    def rows(d: Path, counter: str) -> dict[str, list[float]]:
+        f = next(d.rglob("*counter_collection.csv"))
+        per: dict[tuple[str, str], float] = {}
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                k = r["Kernel_Name"]
+                if ("pair_f32" in k or "hybrid_f32" in k) and r["Counter_Name"] == counter:
+                    key = (k, r["Dispatch_Id"])
+                    per[key] = per.get(key, 0.0) + float(r["Counter_Value"])
+        out: dict[str, list[float]] = {}
+        for (k, _), v in per.items():
+            out.setdefault(k, []).append(v)
+        return out
+
+    fetch, write = rows(Path(fetch_dir), "FETCH_SIZE"), rows(Path(write_dir), "WRITE_SIZE")
+    alg = 2.0 * T * V * 4 + T * 37
+    res = {"tool": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) of bench.py's loss_head_fp32 probe; "
+                   "FETCH_SIZE x 1024 x 2, WRITE_SIZE x 1024 (MI355X_MICROARCH.md HBM section)",
+           "T": T, "V": V, "per_launch_median": {}}
+    for k in sorted(set(fetch) & set(write)):
+        rd = statistics.median(fetch[k]) * 1024 * 2
+        wr = statistics.median(write[k]) * 1024
+        res["per_launch_median"][k] = {"fetch_size_bytes": rd, "write_size_bytes": wr, "algorithmic_bytes": alg,
+                                       "traffic_over_algorithmic": round((rd + wr) / alg, 4),
+                                       "launches": [len(fetch[k]), len(write[k])]}
+    Path(out).write_text(json.dumps(res, indent=1))
+    print(json.dumps(res))
+
+
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    if sys.argv[1] == "--fp32":
+        fp32_main(*sys.argv[2:5])
+    else:
+        main(*sys.argv[1:4])

@@ -1,7 +1,7 @@
 # The bench's rocprofv3 evidence: kernel stats of the loss-head bench, then FETCH_SIZE and
 # WRITE_SIZE in separate PMC passes (never combined with tracing; each pass under its own limit).
 # Outputs (small CSVs only) under gpurun_out/prof_bench, gpurun_out/pmc_fetch, gpurun_out/pmc_write.
-# The bench's N = 1 loss_head_fp32 probe runs in every pass: the part-resident fp32 kernel is
+# The bench's N = 1 loss_head_fp32 probe runs in every pass: the fp32 kernels (pair + hybrid A/B) are
 # profiled and counted beside the bf16 one.
 set -u
 export TMPDIR=/tmp
