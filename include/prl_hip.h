@@ -209,6 +209,14 @@ int prl_unflatten_bf16(const void* src, void* const* dsts, const int32_t* dtypes
 int prl_grad_scale_bf16(const void* src, int32_t src_dtype, const float* scale, void* dst, int64_t n,
                         int32_t accumulate, void* stream);
 
+/* Measurement helper, not a product path (bench.py snapshot_overlap): emulates the reads an RCCL
+ * broadcast root makes of the buffer it sends (finetune_loop.py:202-205 broadcasts the parameters)
+ * when no receiver exists: `blocks` 256-thread workgroups (the communicator's channels) stream
+ * `bytes` of `src` (16-B aligned; the tail below 16 B is not read) with nontemporal loads, paced to
+ * `gbps` in total against the realtime clock; sink (device, >= blocks words) receives a folded
+ * word of workgroup i only when it matches an internal key (keeps the loads; contents unspecified). */
+int prl_paced_read(const void* src, int64_t bytes, double gbps, int32_t blocks, uint32_t* sink, void* stream);
+
 /* AdamW step over n tensors (csrc/adamw.hip): params / grads / exp_avgs / exp_avg_sqs are device
  * pointers of `dtype` (PRL_BF16 or PRL_F32, all four alike), steps[i] the device float step count
  * of tensor i (already incremented for this step, as torch's fused AdamW expects it), numels[i] its

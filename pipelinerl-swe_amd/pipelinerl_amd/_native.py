@@ -80,6 +80,7 @@ _SIGNATURES = {
     "prl_unflatten_bf16": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_int32), POINTER(c_int64),
                                    POINTER(c_int64), c_int32, c_void_p]),
     "prl_grad_scale_bf16": (c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_int64, c_int32, c_void_p]),
+    "prl_paced_read": (c_int, [c_void_p, c_int64, c_double, c_int32, c_void_p, c_void_p]),
     "prl_adamw_step": (c_int, [c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32,
                                c_double, c_double, c_double, c_double, c_double, c_void_p, c_void_p]),
     "prl_grad_sqnorm": (c_int, [POINTER(c_void_p), POINTER(c_int32), POINTER(c_int64), c_int32,

@@ -178,6 +178,46 @@ static int grid_x_for(const PackGroup& g) {
   return (int)blocks;
 }
 
+// Measurement helper (bench snapshot_overlap): the reads an RCCL broadcast root makes of the
+// parameters it sends, emulated on one GPU with no receiver.  `blocks` workgroups of 256 threads (the
+// communicator's channels: one workgroup per channel, each on its own CU for the whole transfer)
+// stream the buffer with nontemporal 16-B loads, each paced against the realtime clock (100 MHz)
+// to its share of `gbps`, the link rate the root sends at (one xGMI link ~153 GB/s).  What it
+// costs the trainer step running beside it is the contention the zero-copy broadcast adds: CUs
+// held and HBM read while the step's kernels run.  The loaded data is folded per thread and
+// compared with a run-time key (a store only on a match), so the loads cannot be removed.
+__global__ __launch_bounds__(256) void paced_read_kernel(const u32x4* __restrict__ src, int64_t nvec,
+                                                         double vec_per_tick, uint32_t* sink, uint32_t key) {
+  const int64_t per = (nvec + gridDim.x - 1) / gridDim.x;
+  const int64_t a = (int64_t)blockIdx.x * per;
+  const int64_t b = a + per < nvec ? a + per : nvec;
+  constexpr int U = 16;  // 16 vectors per thread in flight: 64 KiB per workgroup per turn
+  uint32_t acc = 0;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  int64_t done = 0;
+  for (int64_t v = a + threadIdx.x; v < b; v += (int64_t)U * 256) {
+    u32x4 x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = v + (int64_t)u * 256;
+      x[u] = i < b ? __builtin_nontemporal_load(src + i) : u32x4{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc ^= x[u][0] ^ x[u][1] ^ x[u][2] ^ x[u][3];
+    done += (int64_t)U * 256;
+    // wait until this workgroup's share of the link rate has caught up with what it has read: the
+    // clock is read once per turn (a realtime read is a message to a chip-wide counter: polling it
+    // in a tight loop delayed every other kernel's start), the wait itself is counted sleeps
+    const uint64_t due = t0 + (uint64_t)((double)done / vec_per_tick);
+    const uint64_t now = __builtin_amdgcn_s_memrealtime();
+    if (now < due) {
+      // s_sleep 127 ~ 127 x 64 cycles ~ 3.4-3.9 us at 2.1-2.4 GHz; a realtime tick is 10 ns
+      for (int64_t k = (int64_t)(due - now) / 400; k > 0; --k) __builtin_amdgcn_s_sleep(127);
+    }
+  }
+  if (acc == key) sink[blockIdx.x] = acc;  // depends on every load: they stay (almost never stores)
+}
+
 }  // namespace prl
 
 using namespace prl;
@@ -277,6 +317,19 @@ int prl_grad_sqnorm(const void* const* srcs, const int32_t* dtypes, const int64_
     if (e != hipSuccess) return (int)e;
   }
   return PRL_OK;
+}
+
+int prl_paced_read(const void* src, int64_t bytes, double gbps, int32_t blocks, uint32_t* sink, void* stream) {
+  // sink: a word per workgroup, written only when a thread's folded data equals the key
+  if (!src || !sink || bytes < 0 || !(gbps > 0.0) || blocks < 1 || blocks > 1024) return PRL_E_INVALID;
+  if (reinterpret_cast<uintptr_t>(src) & 15) return PRL_E_INVALID;
+  const int64_t nvec = bytes / 16;
+  if (nvec == 0) return PRL_OK;
+  // 16-B vectors per realtime tick (10 ns) and workgroup
+  const double vec_per_tick = gbps * 1e9 / 16.0 / 1e8 / (double)blocks;
+  hipLaunchKernelGGL(paced_read_kernel, dim3((unsigned)blocks), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     static_cast<const u32x4*>(src), nvec, vec_per_tick, sink, 0x9E3779B9u);
+  return (int)hipGetLastError();
 }
 
 }  // extern "C"

@@ -272,6 +272,37 @@ class TrainerStep:
             torch.cuda.empty_cache()
 
 
+def step_roofline(ts: "TrainerStep", seconds: float, breakdown: bool = True) -> dict | None:
+    """The step's MFMA roofline (step_flops.py): model FLOPs of this rank's micro-batches, summed over
+    the ranks, per GPU over ``seconds`` (the step time, max over ranks), against the dense bf16 peak;
+    with ``breakdown`` one more step runs under torch.profiler for its GEMM / attention kernel time
+    (every rank runs it: the step's collectives stay matched).  None for a model without a config."""
+    from .step_flops import kernel_breakdown, mfma_roofline, shape_of, step_flops
+
+    cfg = getattr(getattr(ts.model, "module", ts.model), "config", None)
+    if cfg is None or not hasattr(cfg, "num_hidden_layers"):
+        return None
+    flops = step_flops(cfg, [shape_of(b) for b in ts.batches], label_row_head=ts.cfg.fused_lm_head)
+    world = ts.world
+    if world > 1:
+        tot = torch.tensor([float(flops[k]) for k in ("linear", "lm_head", "attention", "total")], dtype=torch.float64,
+                           device=ts.device)
+        dist.all_reduce(tot, group=ts.group)
+        flops = dict(flops, **{k: float(v) / world for k, v in zip(("linear", "lm_head", "attention", "total"),
+                                                                     tot.cpu().tolist())})
+    kb = None
+    if breakdown and ts.device.type == "cuda":
+        try:
+            kb = kernel_breakdown(ts.step, ts.device)
+        except Exception as e:  # noqa: BLE001 - the profiler is measurement only
+            kb = {"error": f"{type(e).__name__}: {e}"[:200]}
+    r = mfma_roofline(flops, seconds, kb if kb and "error" not in kb else None)
+    if kb and "error" in kb:
+        r["kernel_breakdown"] = kb
+    r["per"] = "GPU (this world's model FLOPs per rank, mean over ranks) / step time (max over ranks)"
+    return r
+
+
 def trainer_step_probe(name: str = "1.5b", tokens: int = 16384, seq: int = 2048, prompt: int = 256,
                        micro_batches: int = 4, steps: int = 3, warmup: int = 1, device=None,
                        fused_head: bool = True, grad_ckpt: bool = False, fused_ops: bool = True,
@@ -294,6 +325,7 @@ def trainer_step_probe(name: str = "1.5b", tokens: int = 16384, seq: int = 2048,
         ts.grads = GradBuckets(list(ts.model.parameters()))
     sec = ts.timed(steps, warmup)
     peak = torch.cuda.max_memory_allocated(device) / 1e9
+    roof = step_roofline(ts, sec)
     ts.close()
     total = tokens * micro_batches * world
     out = {"model": f"Qwen2.5-{name} shapes{f' ({layers} layers)' if layers else ''} (random init, bf16)",
@@ -303,6 +335,8 @@ def trainer_step_probe(name: str = "1.5b", tokens: int = 16384, seq: int = 2048,
            "ms_per_optimizer_step": round(sec * 1e3, 2),
            "tokens_per_s": round(total / sec, 1), "tokens_per_s_per_gpu": round(total / sec / world, 1),
            "peak_mem_gb": round(peak, 2), "steps": steps, "warmup": warmup, "world": world}
+    if roof is not None:
+        out["roofline"] = roof
     if local is not None:
         out["local_tokens_per_s_per_gpu"] = round(total / world / local, 1)
         out["ms_per_optimizer_step_local"] = round(local * 1e3, 2)
@@ -325,6 +359,37 @@ def _snapshot_only_group():
     return SnapshotOnlyGroup()
 
 
+def _paced_read_group(gbps: float, blocks: int, device):
+    """An actor group with no receivers whose broadcast READS what it would send, as an RCCL root
+    does, at a link rate: ``blocks`` workgroups (the channels) stream each bucket paced to ``gbps``
+    (prl_paced_read, stream-ordered on the broadcast's side stream).  One xGMI link ~153 GB/s
+    (SURVEY.md §5)."""
+    import ctypes
+
+    from . import _native
+    from .comm import RcclComm
+
+    lib = _native.load()
+    sink = torch.zeros(max(1, blocks), dtype=torch.int32, device=device)
+
+    class PacedReadGroup(RcclComm):
+        def __init__(self):
+            super().__init__(None, 0, 1, None)
+
+        def broadcast(self, t: torch.Tensor, src: int = 0, bucket_bytes: int = 0) -> None:
+            st = torch.cuda.current_stream(t.device).cuda_stream
+            _native.check(lib.prl_paced_read(ctypes.c_void_p(t.data_ptr()), t.numel() * t.element_size(),
+                                             float(gbps), int(blocks), ctypes.c_void_p(sink.data_ptr()), st),
+                          "prl_paced_read")
+
+    return PacedReadGroup()
+
+
+# the broadcast's reads of the parameters emulated at N = 1: (GB/s, channels) of one xGMI link and of
+# four (a 1 -> 4 actors broadcast spread over several rings)
+PACED_ARMS = {"zero_copy_1link": (153.0, 16), "zero_copy_4link": (612.0, 32)}
+
+
 def snapshot_overlap(ts: "TrainerStep", t_ref: float, steps: int, warmup: int, flatten_iters: int = 3,
                      rounds: int = 3) -> dict:
     """The trainer-side half of "weight broadcast fully overlapped" (north_star), on this rank's GPU.
@@ -338,7 +403,13 @@ def snapshot_overlap(ts: "TrainerStep", t_ref: float, steps: int, warmup: int, f
     place; re-homed at load by TrainerStep, as the loop does, so every arm runs the same step).  No receiver: the broadcasts are no-ops, so the arms price the trainer-side snapshot alone
     (the broadcast's own cost needs actors: ``split_pipeline`` at N > 1).  ``exposed_ms`` = median step
     time of an arm − the no-update arm's (the no-update arm's own spread is the noise floor); ``hidden_frac`` = 1 − exposed / snapshot_ms.  The
-    reference blocks the trainer for the whole update instead (finetune_loop.py:174-215)."""
+    reference blocks the trainer for the whole update instead (finetune_loop.py:174-215).
+
+    The zero-copy arm does no device work at all with no receiver, so its hidden_frac is null.  The
+    ``zero_copy_1link`` / ``zero_copy_4link`` arms give it a real number: the same in-place update whose
+    broadcast READS the 15.23 GB of parameters as an RCCL root sending them would — paced to one xGMI
+    link (153 GB/s, 16 channel workgroups) and to four (612 GB/s, 32) — on the side stream while the
+    next step runs; ``device_work_ms`` is those reads alone (HIP events, nothing else running)."""
     from .weight_update import FlatLayout, HipFlatPacker, WeightUpdateManager, parameters_info
 
     rank = dist.get_rank() if dist.is_initialized() else 0
@@ -367,10 +438,28 @@ def snapshot_overlap(ts: "TrainerStep", t_ref: float, steps: int, warmup: int, f
     # the parameters are re-homed at load (TrainerStep, as the loop does; or here, before any arm
     # runs): every arm runs the same step, the fused gate/up weight a view of them
     in_place = managers["zero_copy"]._zero_copy_flat(named, layout) is not None if rank == 0 else False
-    arms = {"no_update": [t_ref], "copy": [], "zero_copy": []}
-    order = ["no_update", "copy", "zero_copy"]
+    paced_ms = {}
+    if in_place:
+        flat_p = managers["zero_copy"]._flat_params
+        for name, (gbps, blocks) in PACED_ARMS.items():
+            grp = _paced_read_group(gbps, blocks, ts.device)
+            managers[name] = WeightUpdateManager([], ts.model, None, grp, transport="bucketed", overlap=True,
+                                                 is_main=rank == 0, write_message=lambda s, m: None,
+                                                 snapshot="zero_copy")
+            with torch.cuda.stream(side):  # the reads alone, nothing else running
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(side)
+                for a, b in layout.buckets(128 << 20):  # 256 MiB buckets of bf16
+                    grp.broadcast(flat_p[a:b])
+                e1.record(side)
+            _sync(ts.device)
+            paced_ms[name] = e0.elapsed_time(e1)
+    arms = {m: [] for m in managers}
+    arms["no_update"] = [t_ref]
+    order = list(managers)
     for r in range(rounds):  # the order rotates every round, so a drift of the clocks hits every arm
-        for mode in order[r % 3:] + order[:r % 3]:
+        k = r % len(order)
+        for mode in order[k:] + order[:k]:
             first = r == 0 and mode != "no_update"
             arms[mode].append(ts.timed(steps, warmup if first else 0, wum=managers[mode]))
             if managers[mode] is not None:
@@ -388,16 +477,25 @@ def snapshot_overlap(ts: "TrainerStep", t_ref: float, steps: int, warmup: int, f
         exposed = max(0.0, delta)
         return {"ms_per_step": round(mean[mode] * 1e3, 2), "step_delta_ms": round(delta, 3),
                 "exposed_ms": round(exposed, 3), "within_noise": abs(delta) <= spread, "device_work_ms": cost_ms,
-                "hidden_frac": (round(1.0 - min(1.0, exposed / cost_ms), 4) if cost_ms > 0 else 1.0)}
+                "hidden_frac": (round(1.0 - min(1.0, exposed / cost_ms), 4) if cost_ms > 0 else None)}
+
+    zc = arm("zero_copy", 0.0 if in_place else round(snap_ms, 3))
+    if in_place:
+        zc["hidden_frac_note"] = "unmeasured at N=1: no receiver, the broadcast reads nothing (see zero_copy_1link/4link)"
+    paced = {}
+    for name, (gbps, blocks) in PACED_ARMS.items():
+        if name in paced_ms:
+            paced[name] = dict(arm(name, round(paced_ms[name], 3)), link_GBps=gbps, channel_workgroups=blocks,
+                               reads="the 15.23 GB flat parameter buffer in 256 MiB buckets, prl_paced_read")
 
     return {"params": len(named), "snapshot_bytes": 2 * layout.total, "snapshot_ms": round(snap_ms, 3),
             "snapshot_GBps": round(nbytes / (snap_ms * 1e-3) / 1e9, 1),
             "ms_per_step_no_update": round(mean["no_update"] * 1e3, 2),
             "no_update_spread_ms": round(spread, 3),
             "copy": arm("copy", round(snap_ms, 3)),
-            # in place there is no per-update device work on the trainer: hidden_frac 1 by construction,
-            # step_delta_ms is the run's noise (compare no_update_spread_ms)
-            "zero_copy": dict(arm("zero_copy", 0.0 if in_place else round(snap_ms, 3)), in_place=in_place),
+            # in place with no receiver there is no device work on the trainer: step_delta_ms is the
+            # run's noise (compare no_update_spread_ms); the paced arms price the broadcast's reads
+            "zero_copy": dict(zc, in_place=in_place), **paced,
             "arms_ms": {k: [round(x * 1e3, 2) for x in v] for k, v in arms.items()},
             "steps_per_arm": steps, "rounds": rounds}
 
@@ -452,6 +550,7 @@ def dp_step_probe(config: str = "c3", micro_batches: int = 4, steps: int = 2, wa
         t_ar = ts.allreduce_alone()
     nbytes = sum(p.numel() * p.element_size() for p in ts.model.parameters())
     peak = torch.cuda.max_memory_allocated(device) / 1e9 if on_gpu else 0.0  # before the staging buffer
+    roof = step_roofline(ts, t_dp, breakdown=on_gpu)
     snap = snapshot_overlap(ts, t_dp, steps, warmup) if snapshot and on_gpu else None
     ts.close()
     stats = torch.tensor([n_tokens, n_samples, t_local], dtype=torch.float64, device=device)
@@ -489,6 +588,7 @@ def dp_step_probe(config: str = "c3", micro_batches: int = 4, steps: int = 2, wa
                              "tokens_per_s_per_gpu": round(tok_per_mb * (mb_real / world) / t_real, 1),
                              "allreduce_share": round(exposed / t_real, 5)},
             "peak_mem_gb": round(peak, 2), "steps": steps, "warmup": warmup, "world": world,
+            **({"roofline": roof} if roof is not None else {}),
             **({"snapshot_overlap": snap} if snap is not None else {})}
 
 

@@ -143,3 +143,32 @@ def test_zero_copy_snapshot_broadcasts_the_parameters_in_place(tmp_path):
         assert [p.data_ptr() for p in m2.parameters()] == ptrs
     finally:
         c.close()
+
+
+def test_paced_read_runs_at_its_rate():
+    """prl_paced_read (the emulated broadcast reads of bench.py's snapshot_overlap): 1 GiB at 153 GB/s
+    over 16 workgroups takes 1 GiB / 153 GB/s within 10 % (paced, not at HBM speed), and at a rate
+    above what 16 workgroups can read it simply runs unpaced."""
+    import ctypes
+
+    from pipelinerl_amd import _native
+
+    lib = _native.load()
+    buf = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
+    sink = torch.zeros(64, dtype=torch.int32, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+
+    def run(gbps, blocks):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        assert lib.prl_paced_read(ctypes.c_void_p(buf.data_ptr()), buf.numel(), gbps, blocks,
+                                  ctypes.c_void_p(sink.data_ptr()), st) == 0
+        e1.record()
+        e1.synchronize()
+        return e0.elapsed_time(e1)
+
+    run(153.0, 16)  # warm-up
+    ms = run(153.0, 16)
+    want = buf.numel() / 153e9 * 1e3
+    assert 0.9 * want <= ms <= 1.1 * want, (ms, want)
+    assert run(1e6, 64) < 0.5 * want

@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--layers", type=int, default=None)
     ap.add_argument("--snapshot", action="store_true")
+    ap.add_argument("--paced-arms", default=None,
+                    help="with --snapshot: the emulated broadcast-read arms as GBps:workgroups,... "
+                         "(default trainer_probe.PACED_ARMS)")
     ap.add_argument("--grad-ckpt", action="store_true", help="gradient checkpointing (the reference config's)")
     ap.add_argument("--keep-layers", type=int, default=0, help="with --grad-ckpt: the last K layers keep activations")
     a = ap.parse_args()
@@ -48,7 +51,12 @@ def main():
             gcs[info["generation"]][0] += 1
             gcs[info["generation"]][1] += (time.perf_counter() - t_gc[0]) * 1e3
 
+    from pipelinerl_amd import trainer_probe
     from pipelinerl_amd.trainer_probe import TrainerStep
+
+    if a.paced_arms:
+        trainer_probe.PACED_ARMS = {f"paced_{g}GBps_{b}wg": (float(g), int(b))
+                                    for g, b in (x.split(":") for x in a.paced_arms.split(","))}
 
     timed = TrainerStep.timed
 
