@@ -98,6 +98,13 @@ def _sync(device) -> None:
         torch.cuda.synchronize(device)
 
 
+def _sync_compute(device) -> None:
+    """Wait for the trainer's compute stream only: a weight update's broadcast still running on its
+    side stream belongs to the steps after it, not to the ones just timed."""
+    if torch.device(device).type == "cuda":
+        torch.cuda.current_stream(device).synchronize()
+
+
 class TrainerStep:
     """One rank's optimizer step as the trainer loop runs it (finetune_loop.py rl_finetuning_worker):
     ``micro_batches`` packed micro-batches (the last one armed so the bucketed gradient all-reduce
@@ -207,12 +214,16 @@ class TrainerStep:
             wum.send_weight_update(version)  # returns at once: overlapped with the next step
 
     def timed(self, steps: int, warmup: int, wum=None, version0: int = 0) -> float:
-        """Seconds per optimizer step (max over the group's ranks)."""
+        """Seconds per optimizer step (max over the group's ranks).  With a weight manager ``wum``
+        every step sends an update that overlaps the NEXT step, as in the trainer loop: the timed
+        region starts with the last warm-up step's update in flight and ends when the compute stream
+        is done (the last update's broadcast tail runs on, outside it: it would overlap the next
+        step), then the whole device is waited for."""
         v = version0
         for _ in range(warmup):
             v += 1
             self.step(wum, v)
-        _sync(self.device)
+        _sync_compute(self.device)
         self._tail_events, self._tail_cpu = [], []
         if self.world > 1:
             dist.barrier(self.group)
@@ -220,10 +231,11 @@ class TrainerStep:
         for _ in range(steps):
             v += 1
             self.step(wum, v)
-        _sync(self.device)
+        _sync_compute(self.device)
         if self.world > 1:
             dist.barrier(self.group)
         dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=self.device)
+        _sync(self.device)
         if self.world > 1:
             dist.all_reduce(dt, op=dist.ReduceOp.MAX, group=self.group)
         return float(dt) / steps
@@ -460,8 +472,9 @@ def snapshot_overlap(ts: "TrainerStep", t_ref: float, steps: int, warmup: int, f
     for r in range(rounds):  # the order rotates every round, so a drift of the clocks hits every arm
         k = r % len(order)
         for mode in order[k:] + order[:k]:
-            first = r == 0 and mode != "no_update"
-            arms[mode].append(ts.timed(steps, warmup if first else 0, wum=managers[mode]))
+            # one warm-up step per arm and round: the first timed step runs with an update in flight
+            wu = max(1, warmup) if mode != "no_update" else (warmup if r == 0 else 0)
+            arms[mode].append(ts.timed(steps, wu, wum=managers[mode]))
             if managers[mode] is not None:
                 managers[mode].wait()
     for m in managers.values():

@@ -318,7 +318,7 @@ class WeightUpdateManager:
         on_gpu = dev.type == "cuda"
         if on_gpu:
             if self._stream is None:
-                self._stream = torch.cuda.Stream(device=dev)
+                self._stream = torch.cuda.Stream(device=dev, priority=side_stream_priority())
             ready = torch.cuda.Event()
             ready.record(torch.cuda.current_stream(dev))
             ctx = torch.cuda.stream(self._stream)
@@ -452,6 +452,16 @@ class WeightUpdateManager:
     def close(self) -> None:
         self.wait()
         self.pool.shutdown(wait=True)
+
+
+def side_stream_priority() -> int:
+    """Priority of the broadcast's side stream (torch: lower is higher).  PRL_WU_STREAM_PRIORITY=high
+    puts it on a high-priority HIP stream, which the runtime maps to hardware queues of its own (a
+    normal-priority stream may share a hardware queue with the trainer's compute stream, and kernels
+    in one hardware queue run in order)."""
+    import os
+
+    return -1 if os.environ.get("PRL_WU_STREAM_PRIORITY", "normal") == "high" else 0
 
 
 def flat_home(named, layout: FlatLayout) -> torch.Tensor | None:
