@@ -94,6 +94,18 @@ def fp32_loss_head_probe(T: int, V: int, device, iters: int = 8, warmup: int = 2
                         temperature=1.0, batch_size=4096.0)
     times: dict[str, list[float]] = {"pair": [], "hybrid": []}
     prev = os.environ.get("PRL_F32_PAIR")
+    import ctypes
+
+    from pipelinerl_amd import _native
+
+    def fallbacks() -> int:  # row halves that computed their partner's partial themselves (read + reset)
+        n = ctypes.c_uint64(0)
+        _native.check(_native.load().prl_grpo_pair_fallbacks(device.index or 0, torch.cuda.current_stream(device).cuda_stream,
+                                                             ctypes.byref(n)), "prl_grpo_pair_fallbacks")
+        return int(n.value)
+
+    fallbacks()
+    fb, pair_launches = 0, 0
     try:
         for _ in range(rounds):
             for arm in ("pair", "hybrid"):
@@ -108,6 +120,9 @@ def fp32_loss_head_probe(T: int, V: int, device, iters: int = 8, warmup: int = 2
                     stats.cpu()
                     if i >= warmup:
                         times[arm].append(e0.elapsed_time(e1))
+                if arm == "pair":
+                    fb += fallbacks()
+                    pair_launches += warmup + iters
     finally:
         if prev is None:
             os.environ.pop("PRL_F32_PAIR", None)
@@ -136,6 +151,8 @@ def fp32_loss_head_probe(T: int, V: int, device, iters: int = 8, warmup: int = 2
             "traffic": traffic, "traffic_over_algorithmic": round(traffic / alg, 4) if traffic else None,
             "traffic_source": src if traffic else None,
             "tokens_per_s": round(T / ms * 1e3, 1), "iters": iters * rounds,
+            "pair_fallbacks_per_launch": round(fb / max(1, pair_launches), 3),
+            "pair_row_halves_per_launch": 2 * T,
             "hybrid": {"kernel": "grpo_fwd_hybrid_f32<19, 9> (PRL_F32_PAIR=0, alternated)", "kernel_ms": round(ms_h, 4),
                        "frac": round(alg / ms_h / 1e6 / HBM_PEAK_GBS, 4),
                        "traffic_over_algorithmic": round(traffic_h / alg, 4) if traffic_h else None}}

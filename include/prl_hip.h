@@ -190,6 +190,12 @@ int prl_grpo_backward(const PrlGrpoBatch* batch, const PrlGrpoParams* params,
 /* Number of statistics (PRL_NSTAT) compiled into the library: bindings check it. */
 int prl_grpo_nstat(void);
 
+/* Observability of the pair kernels (fp32 rows, each split over two workgroups): how many row halves
+ * on (device, stream) computed their partner's partial themselves because the partner had not
+ * published it in time (PRL_PAIR_SPIN_TICKS) since the last call; reads and resets the counter,
+ * synchronising the stream.  0 when no pair launch ran there. */
+int prl_grpo_pair_fallbacks(int device, void* stream, uint64_t* count);
+
 /* Weight broadcast staging: copy n tensors (f32 or bf16, contiguous) into one bf16 buffer
  * at the given element offsets (dst_offsets[i], bf16 elements; 8-element aligned for the
  * vector path), converting with round-to-nearest-even; and the inverse into bf16 or f32

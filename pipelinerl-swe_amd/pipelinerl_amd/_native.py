@@ -81,6 +81,7 @@ _SIGNATURES = {
                                    POINTER(c_int64), c_int32, c_void_p]),
     "prl_grad_scale_bf16": (c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_int64, c_int32, c_void_p]),
     "prl_paced_read": (c_int, [c_void_p, c_int64, c_double, c_int32, c_void_p, c_void_p]),
+    "prl_grpo_pair_fallbacks": (c_int, [c_int, c_void_p, POINTER(ctypes.c_uint64)]),
     "prl_adamw_step": (c_int, [c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32,
                                c_double, c_double, c_double, c_double, c_double, c_void_p, c_void_p]),
     "prl_grad_sqnorm": (c_int, [POINTER(c_void_p), POINTER(c_int32), POINTER(c_int64), c_int32,

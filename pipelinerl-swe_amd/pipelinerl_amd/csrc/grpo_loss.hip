@@ -757,6 +757,7 @@ struct PairArgs {
   uint32_t* slots;      // [pairs][2 halves][2 parities] x 4 words {m, s, w, tag}
   int64_t slot_bytes;   // bytes of the slot array (its buffer descriptor's range)
   int64_t spin_ticks;   // realtime ticks a half waits for its partner before computing its partial
+  uint32_t* fallbacks;  // rows whose partner partial a half computed itself (one vector atomic each)
 };
 #ifndef PRL_PAIR_SPIN_TICKS
 #define PRL_PAIR_SPIN_TICKS 20000  // 200 us
@@ -922,6 +923,7 @@ __global__ __launch_bounds__(1024) void grpo_fwd_pair_f32(KArgs a, PairArgs pa) 
       part = Lse{__uint_as_float(xch[par][0]), __uint_as_float(xch[par][1]), __uint_as_float(xch[par][2])};
     } else {  // the partner is late (not resident, or behind): its partial from HBM (block-uniform branch)
       part = half_state<NV, false>(buf, half_rsrc(lrow, off_part, npart), voff, last_ok_part, c, red2, lane, wid);
+      if (tid == 0) atomicAdd(pa.fallbacks, 1u);
     }
     const Lse tot = h == 0 ? lse_combine(mine, part, c) : lse_combine(part, mine, c);
     const float l2s = log2f(tot.s);
@@ -1132,6 +1134,7 @@ __global__ __launch_bounds__(1024) void grpo_fwd_pair_bf16(KArgs a, PairArgs pa)
       part = Lse{__uint_as_float(xch[par][0]), __uint_as_float(xch[par][1]), __uint_as_float(xch[par][2])};
     } else {  // the partner is late: its partial from HBM (block-uniform branch)
       part = half_state_bf16<NV, false>(x, half_rsrc(lrow, off_part, npart), voff, last_ok_part, c, red2, lane, wid);
+      if (tid == 0) atomicAdd(pa.fallbacks, 1u);
     }
     const Lse tot = h == 0 ? lse_combine(mine, part, c) : lse_combine(part, mine, c);
     const float l2s = log2f(tot.s);
@@ -1463,6 +1466,8 @@ static hipError_t launch_resident_nv(int nv, const KArgs& a, int grid, hipStream
 // never share hand-off slots; [pairs][2][2] granules of 16 B for up to 1024 CUs
 constexpr int kPairMaxCUs = 1024;
 constexpr size_t kPairSlotBytes = (size_t)(kPairMaxCUs / 2) * 2 * 2 * 16;
+// after the slots: the fallback counter (not cleared per launch; prl_grpo_pair_fallbacks reads and resets it)
+constexpr size_t kPairCounterBytes = 16;
 static std::mutex g_slot_mu;
 static std::map<std::pair<int, hipStream_t>, void*> g_pair_slots;
 
@@ -1472,7 +1477,9 @@ static hipError_t pair_slots(int dev, hipStream_t s, void** out) {
   auto it = g_pair_slots.find(key);
   if (it == g_pair_slots.end()) {
     void* p = nullptr;
-    const hipError_t e = hipMalloc(&p, kPairSlotBytes);
+    hipError_t e = hipMalloc(&p, kPairSlotBytes + kPairCounterBytes);
+    if (e != hipSuccess) return e;
+    e = hipMemset(static_cast<char*>(p) + kPairSlotBytes, 0, kPairCounterBytes);
     if (e != hipSuccess) return e;
     it = g_pair_slots.emplace(key, p).first;
   }
@@ -1537,6 +1544,7 @@ static hipError_t launch_pair_rows(const KArgs& a, int nv, int64_t nrows, int cu
   pa.slots = static_cast<uint32_t*>(slots);
   pa.slot_bytes = (int64_t)kPairSlotBytes;
   pa.spin_ticks = pair_spin_ticks();
+  pa.fallbacks = reinterpret_cast<uint32_t*>(static_cast<char*>(slots) + kPairSlotBytes);
   e = hipMemsetAsync(slots, 0, (size_t)(grid / 2) * 2 * 2 * 16, s);  // tags restart at 1 every launch
   if (e != hipSuccess) return e;
   if (bf16) {
@@ -1749,5 +1757,26 @@ int prl_grpo_backward(const PrlGrpoBatch* batch, const PrlGrpoParams* params, co
 }
 
 int prl_grpo_nstat(void) { return PRL_NSTAT; }
+
+int prl_grpo_pair_fallbacks(int device, void* stream, uint64_t* count) {
+  if (!count) return PRL_E_INVALID;
+  *count = 0;
+  void* slots = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_slot_mu);
+    auto it = g_pair_slots.find(std::make_pair(device, static_cast<hipStream_t>(stream)));
+    if (it == g_pair_slots.end()) return PRL_OK;  // no pair launch on this stream yet
+    slots = it->second;
+  }
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  uint32_t* ctr = reinterpret_cast<uint32_t*>(static_cast<char*>(slots) + kPairSlotBytes);
+  uint32_t host = 0;
+  hipError_t e = hipMemcpyAsync(&host, ctr, sizeof(host), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipMemsetAsync(ctr, 0, sizeof(uint32_t), s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return (int)e;
+  *count = host;
+  return PRL_OK;
+}
 
 }  // extern "C"

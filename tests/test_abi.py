@@ -51,6 +51,7 @@ def test_invalid_arguments_rejected_without_gpu():
     # null pointers / zero shapes are rejected before any device call
     assert lib.prl_grpo_forward(ctypes.byref(b), ctypes.byref(p), ctypes.byref(o), None, 0, None) == 1001
     assert lib.prl_flatten_bf16(None, None, None, None, -1, None, None) == 1001
+    assert lib.prl_grpo_pair_fallbacks(0, None, None) == 1001
     assert lib.prl_paced_read(None, 1 << 20, 153.0, 16, None, None) == 1001
     assert lib.prl_paced_read(16, 1 << 20, 0.0, 16, 16, None) == 1001  # a rate must be given
     assert lib.prl_paced_read(16, 1 << 20, 153.0, 0, 16, None) == 1001

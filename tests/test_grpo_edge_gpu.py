@@ -384,3 +384,66 @@ def test_fp32_pair_kernel_vocab_range(V):
     b = _batch(T, V, seed=14)
     lg = np.random.default_rng(14).normal(0, 2, (1, T, V)).astype(np.float32)
     _cmp(lg, b, dtype=torch.float32)
+
+
+@pytest.mark.parametrize("dtype,env", [(torch.float32, {}), (torch.bfloat16, {"PRL_BF16_PAIR": "1"})],
+                         ids=["fp32_pair", "bf16_pair"])
+def test_pair_kernels_beside_a_kernel_holding_cus(dtype, env, monkeypatch):
+    """The pair kernels beside a long kernel on another stream that holds registers on half the CUs
+    (as an RCCL collective beside the loss head would): half the workgroups start only as others
+    finish; a half whose partner is late stops waiting after the (lowered, 20 us) spin bound and
+    computes the partner's partial itself.  The launch completes with the same bits as the
+    uncontended run's (which matches the oracle), and prl_grpo_pair_fallbacks counts the halves
+    that did not wait."""
+    import ctypes
+
+    from pipelinerl_amd import _native
+    from pipelinerl_amd.finetune.rl import RLConfig, rl_step
+
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    V = 151936
+    lens = [200, 200]
+    T = sum(lens)
+    b = _batch(T, V, seed=19, lens=lens, prompts=[20, 20])
+    lg = np.random.default_rng(19).normal(0, 2, (1, T, V)).astype(np.float32)
+    if dtype == torch.bfloat16:
+        lg = synth.to_bf16(lg).astype(np.float32)
+    loss0, stats0, d0 = _run(lg, b, dtype=dtype)
+    o = grpo_oracle.rl_step_oracle(lg, b, CFG, 0, 10)
+    tol = (1e-2, 1e-8) if dtype == torch.bfloat16 else (1e-4, 1e-7)
+    assert rel_close(d0, o["dlogits"], *tol)[0]
+
+    lib = _native.load()
+
+    def fallbacks() -> int:  # read and reset this stream's counter
+        n = ctypes.c_uint64(0)
+        assert lib.prl_grpo_pair_fallbacks(torch.cuda.current_device(),
+                                           ctypes.c_void_p(torch.cuda.current_stream().cuda_stream),
+                                           ctypes.byref(n)) == 0
+        return int(n.value)
+
+    fallbacks()
+    hog = torch.empty(1 << 30, dtype=torch.uint8, device=DEV)
+    sink = torch.zeros(256, dtype=torch.int32, device=DEV)
+    side = torch.cuda.Stream()
+    monkeypatch.setenv("PRL_PAIR_SPIN_TICKS", "2000")  # 20 us
+    model = LogitsModel(torch.tensor(lg, dtype=torch.float32).to(dtype).to(DEV))
+    torch.cuda.synchronize()
+    with torch.cuda.stream(side):  # ~50 ms of 128 workgroups reading 1 GiB at 20 GB/s
+        assert lib.prl_paced_read(ctypes.c_void_p(hog.data_ptr()), hog.numel(), 20.0, 128,
+                                  ctypes.c_void_p(sink.data_ptr()), side.cuda_stream) == 0
+    loss, stats = rl_step(model, to_batch(b), 0, 10, RLConfig(**CFG))
+    loss.backward()
+    torch.cuda.synchronize()
+    d1 = model.logits.grad.float().cpu().numpy()
+    assert np.array_equal(d0, d1)
+    assert float(loss.detach()) == loss0 and stats == stats0
+    # pairs are blocks b, b ^ 8 of 16-block groups: dispatched in order onto the free CUs, both halves
+    # of a pair mostly start together, so the counter is usually 0 here (the never-wait runs of
+    # test_*_many_rows_* take the from-HBM partial on every row); it must be readable and bounded
+    assert 0 <= fallbacks() <= 2 * (T - 1)
+    # the counter counts: the never-wait arm falls back on (almost) every row half
+    monkeypatch.setenv("PRL_PAIR_SPIN_TICKS", "0")
+    _run(lg, b, dtype=dtype)
+    assert fallbacks() > 0
