@@ -764,7 +764,6 @@ struct PairArgs {
 #endif
 constexpr int kPairMinNV = 8, kPairMaxNV = 19;  // above 19 the registers spill (hybrid kernel there)
 constexpr int kSc1 = 16;  // aux bit of buffer_load / buffer_store: sc1 (bypass the CU's L1; write through)
-typedef uint32_t sgpr4_t __attribute__((ext_vector_type(4)));
 
 // One lane of each half: publish this half's partial as one 16-B sc1 granule {m, s, w, tag} (a
 // single vector store: never torn, written through to memory), then poll the partner's granule with
@@ -782,33 +781,6 @@ __device__ __forceinline__ void pair_exchange(__amdgpu_buffer_rsrc_t slots, int 
       __builtin_amdgcn_s_sleep(1);
       asm volatile("" ::: "memory");  // a fresh load every turn
       v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(slots, partner_off, 0, kSc1));
-    }
-  }
-  out[0] = v[0];
-  out[1] = v[1];
-  out[2] = v[2];
-  out[3] = v[3] == tag ? 1u : 0u;
-}
-
-// pair_exchange with the partner's granule polled by SCALAR loads (s_load_dwordx4 glc: L2, not the
-// scalar cache), for a kernel that has the next row's LDS-DMA in flight: vector loads return in
-// order, so a vector poll would wait behind every one of them.  Each poll load and its lgkmcnt wait
-// are one asm statement.  A line of the slot array that another XCD's L2 holds stale can only carry
-// an older tag: the poll then runs into spin_ticks and the half computes the partial itself.
-__device__ __forceinline__ void pair_exchange_scalar(__amdgpu_buffer_rsrc_t slots, const uint32_t* slot_base, int mine_off,
-                                                     int partner_off, uint32_t tag, Lse mine, int64_t spin_ticks,
-                                                     uint32_t* out) {
-  const u32x4 g = {__float_as_uint(mine.m), __float_as_uint(mine.s), __float_as_uint(mine.w), tag};
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, g), slots,
-                                         mine_off, 0, kSc1);
-  const uint64_t addr = reinterpret_cast<uint64_t>(slot_base) + (uint64_t)partner_off;
-  sgpr4_t v;
-  asm volatile("s_load_dwordx4 %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(addr) : "memory");
-  if (v[3] != tag) {
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (v[3] != tag && (int64_t)(__builtin_amdgcn_s_memrealtime() - t0) < spin_ticks) {
-      __builtin_amdgcn_s_sleep(1);
-      asm volatile("s_load_dwordx4 %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(addr) : "memory");
     }
   }
   out[0] = v[0];
@@ -957,250 +929,6 @@ __global__ __launch_bounds__(1024) void grpo_fwd_pair_f32(KArgs a, PairArgs pa) 
 #pragma unroll
       for (int k = 0; k < NV; ++k)
         buf[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rn, voff, k * VSTRIDE, kLoadAux));
-    }
-  }
-}
-
-// bf16 rows over a pair of workgroups, double-buffered (grpo_fwd_pair_bf16<NV>).  The resident
-// kernel above holds a whole bf16 row per CU and, to keep reads and writes apart, loads the next row
-// only after the current row's stores retired: a CU's HBM pipe idles while it computes.  Split over
-// two CUs (blocks b and b ^ 8, the hand-off of grpo_fwd_pair_f32), a half row is NV = 10 vectors per
-// lane (148 KiB), so the NEXT half row fits beside it: its first NV - 1 vectors stream into LDS by
-// LDS-DMA (no registers: each lane's 16 B land in its own slot of slab[k]) and its last into
-// registers, issued at the top of the row, so they arrive while this row's statistics, hand-off and
-// dlogits are computed and stored.  At the next row's top only this row's NV stores may still be in
-// flight (vmcnt(NV), in-order return), the slab is read into registers and refilled at once.  The
-// target column's g_lp term is added in registers by its owner lane (one wave-uniform branch on the
-// vector holding it), so no store waits for another.
-template <int NV, bool FROM_REGS>
-__device__ __forceinline__ Lse half_state_bf16(const u32x4 (&buf)[NV], __amdgpu_buffer_rsrc_t rs, int voff, bool last_ok,
-                                               float c, float (*red)[3], int lane, int wid) {
-  constexpr int BLOCK = 1024, NW = BLOCK / 64, VSTRIDE = BLOCK * 16;
-  Lse st = lse_empty();
-  auto add = [&](u32x4 v, bool pad) {
-    if (pad) v = u32x4{kPadBf16x2, kPadBf16x2, kPadBf16x2, kPadBf16x2};
-    float x[8];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      x[2 * j] = bf_lo(v[j]);
-      x[2 * j + 1] = bf_hi(v[j]);
-    }
-    lse_add<8>(st, x, c);
-  };
-  if constexpr (FROM_REGS) {
-#pragma unroll
-    for (int k = 0; k < NV; ++k) add(buf[k], k == NV - 1 && !last_ok);
-  } else {
-    constexpr int U = 2;
-#pragma unroll
-    for (int k0 = 0; k0 < NV; k0 += U) {
-      u32x4 t[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (k0 + u < NV) t[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, (k0 + u) * VSTRIDE, kLoadAux));
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (k0 + u < NV) add(t[u], k0 + u == NV - 1 && !last_ok);
-    }
-  }
-  st = wave_reduce_lse(st, c);
-  if (lane == 0) {
-    red[wid][0] = st.m;
-    red[wid][1] = st.s;
-    red[wid][2] = st.w;
-  }
-  __syncthreads();
-  return block_combine<NW>(red, c);
-}
-
-constexpr int kPairBf16NV = 10;        // half rows of 9 216 < n <= 10 176 vectors: Qwen2.5 (V = 151 936 / 152 064)
-constexpr int kPairBf16LastLanes = 960;  // LDS slots of the last, partial vector (15 waves): 160 KiB in all
-
-// the 16-B LDS-DMA forms in inline asm (M0 set and restored in the same statement; hipcc does not
-// count these loads: the row top waits for them with its own vmcnt)
-__device__ __forceinline__ void lds_dma16_global(const void* src, uint32_t lds_dst) {
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(src), "s"(lds_dst)
-               : "memory");
-}
-__device__ __forceinline__ void lds_dma16_buffer(sgpr4_t rsrc, int voff, uint32_t soff, uint32_t lds_dst) {
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen nt lds\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(voff), "s"(rsrc), "s"(soff), "s"(lds_dst)
-               : "memory");
-}
-// a raw buffer descriptor (the words __builtin_amdgcn_make_buffer_rsrc builds): bounds-checked
-// loads of [base, base + bytes), out-of-range lanes read 0
-__device__ __forceinline__ sgpr4_t raw_rsrc(const void* base, int64_t bytes) {
-  const uint64_t a = reinterpret_cast<uint64_t>(base);
-  sgpr4_t r;
-  r[0] = __builtin_amdgcn_readfirstlane((uint32_t)a);
-  r[1] = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32) & 0xffffu);
-  r[2] = __builtin_amdgcn_readfirstlane((uint32_t)bytes);
-  r[3] = 0x00020000u;
-  return r;
-}
-
-template <int NV>
-__global__ __launch_bounds__(1024) void grpo_fwd_pair_bf16(KArgs a, PairArgs pa) {
-  constexpr int BLOCK = 1024, NW = BLOCK / 64, VSTRIDE = BLOCK * 16, NL = NV - 1;
-  constexpr int LW = kPairBf16LastLanes / 64;  // waves that load the last vector
-  __shared__ u32x4 slab[NL][BLOCK];                 // the next half row's first NL vectors
-  __shared__ u32x4 slab_last[kPairBf16LastLanes];   // and its last, partial one
-  __shared__ float red[2][NW][3];
-  __shared__ float red2[NW][3];
-  __shared__ uint32_t xch[2][4];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wu = __builtin_amdgcn_readfirstlane(wid);
-  const int b = blockIdx.x;
-  const int h = (b >> 3) & 1;
-  const int64_t npairs = gridDim.x >> 1;
-  const int64_t p = (int64_t)(b >> 4) * 8 + (b & 7);
-  const int64_t nrows = fwd_rows(a);
-  const int nvec = (int)(a.V >> 3);
-  const int n0 = (nvec + 1) >> 1;
-  const int nmine = h ? nvec - n0 : n0, npart = h ? n0 : nvec - n0;
-  const int64_t off_mine = h ? (int64_t)n0 * 16 : 0, off_part = h ? 0 : (int64_t)n0 * 16;
-  const int col0 = h ? n0 * 8 : 0;
-  const float c = kLog2e / a.temperature;
-  const float inv_t = 1.0f / a.temperature;
-  const uint16_t* __restrict__ lg = static_cast<const uint16_t*>(a.logits);
-  uint16_t* __restrict__ dl = static_cast<uint16_t*>(a.dlogits);
-  const int voff = tid * 16;
-  const bool last_ok = (NV - 1) * BLOCK + tid < nmine;
-  const bool last_ok_part = (NV - 1) * BLOCK + tid < npart;
-  const auto slots = __builtin_amdgcn_make_buffer_rsrc(pa.slots, 0, (int)pa.slot_bytes, 0x00020000);
-  const int my_slot = (int)((p * 2 + h) * 2) * 16, partner_slot = (int)((p * 2 + (h ^ 1)) * 2) * 16;
-  auto half_rsrc = [&](int64_t lrow, int64_t off, int n) {
-    return row_rsrc(reinterpret_cast<const char*>(lg + lrow * a.ld) + off, (int64_t)n * 16);
-  };
-  // The next half row streams into LDS by LDS-DMA, all of it: any register load of it would be a
-  // load younger than the previous row's stores that this row must wait for, and vmcnt waits are
-  // in order.  Vectors 0..NL-1 are inside the half row (the host requires (NV - 1) x 1024 full
-  // vectors per half): the unchecked global form; the last, partial vector by the bounds-checked
-  // buffer form, from the first LW waves.
-  auto issue_row = [&](int64_t i) {
-    int64_t lr, tk, qq;
-    map_row<RowLd>(a, perm_row(i, nrows), lr, tk, qq);
-    const char* half = reinterpret_cast<const char*>(lg + lr * a.ld) + off_mine;
-#pragma unroll
-    for (int k = 0; k < NL; ++k)
-      lds_dma16_global(half + (int64_t)k * VSTRIDE + voff,
-                       __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>((lds_void_t*)(&slab[k][wu * 64]))));
-    if (wu < LW)
-      lds_dma16_buffer(raw_rsrc(half, (int64_t)nmine * 16), voff, (uint32_t)(NL * VSTRIDE),
-                       __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>((lds_void_t*)(&slab_last[wu * 64]))));
-  };
-  u32x4 x[NV];
-  int64_t i = p;
-  if (i < nrows) issue_row(i);
-  uint32_t it = 0;
-  for (; i < nrows; i += npairs, ++it) {
-    const int par = (int)(it & 1);
-    const uint32_t tag = it + 1;
-    int64_t lrow, tok, qo;
-    map_row<RowLd>(a, perm_row(i, nrows), lrow, tok, qo);
-    const int64_t tid_raw = RowLd::ld(a.input_ids, tok);
-    TokIn tin = tok_in<RowLd>(a, tok);
-    const bool bad_id = (uint64_t)tid_raw >= (uint64_t)a.V;
-    const int64_t tgt = bad_id ? -1 : tid_raw;
-    float xr = row_logit(lg + lrow * a.ld, bad_id ? 0 : tid_raw);
-    pin_sgpr(tin, xr);
-    const float xt = bad_id ? __builtin_nanf("") : xr;
-    // this row's DMA has landed: only the previous row's NV dlogits stores (issued after it) may
-    // still be in flight; the first row / a forward-only launch has no stores behind it
-    if (it == 0 || !a.write_grad)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NV) : "memory");
-#pragma unroll
-    for (int k = 0; k < NL; ++k) x[k] = slab[k][tid];
-    x[NL] = tid < kPairBf16LastLanes ? slab_last[tid] : u32x4{0u, 0u, 0u, 0u};
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slab read out before it is refilled
-    const int64_t in = i + npairs;
-    if (in < nrows) issue_row(in);
-
-    // ---- pass 1: this half's state, published for the partner
-    const Lse mine = half_state_bf16<NV, true>(x, slots, voff, last_ok, c, red[par], lane, wid);  // (rsrc unused)
-    if (tid == 0)
-      pair_exchange_scalar(slots, pa.slots, my_slot + par * 16, partner_slot + par * 16, tag, mine, pa.spin_ticks,
-                           xch[par]);
-    __syncthreads();
-    Lse part;
-    if (xch[par][3]) {
-      part = Lse{__uint_as_float(xch[par][0]), __uint_as_float(xch[par][1]), __uint_as_float(xch[par][2])};
-    } else {  // the partner is late: its partial from HBM (block-uniform branch)
-      part = half_state_bf16<NV, false>(x, half_rsrc(lrow, off_part, npart), voff, last_ok_part, c, red2, lane, wid);
-      if (tid == 0) atomicAdd(pa.fallbacks, 1u);
-    }
-    const Lse tot = h == 0 ? lse_combine(mine, part, c) : lse_combine(part, mine, c);
-    const float l2s = log2f(tot.s);
-    const float M = tot.m;
-    const float lse = M * inv_t + kLn2 * l2s;
-    const float H = kLn2 * (l2s - tot.w / tot.s);
-    const float lp = (xt - M) * inv_t - kLn2 * l2s;
-    const TokGrad core = row_epilogue(a, qo, tin, lp, H, lse, M, l2s, h == 0 && tid == 0);
-#pragma unroll
-    for (int k = 0; k < NV; ++k) asm volatile("" : "+v"(x[k]));
-
-    // ---- pass 2: this half's dlogits from registers (the next half row is arriving meanwhile)
-    if (a.write_grad) {
-      const auto ws = row_rsrc(reinterpret_cast<char*>(dl + lrow * a.ld) + off_mine, (int64_t)nmine * 16);
-      const float alpha = -(core.g_lp + core.g_h * H) * inv_t;
-      const float beta = -core.g_h * kLn2 * inv_t;
-      const float gadd = core.g_lp * inv_t;
-      const int64_t rel = tgt < 0 ? -1 : tgt - col0;
-      const bool mine_t = rel >= 0 && rel < (int64_t)nmine * 8;
-      const int tv = mine_t ? (int)(rel >> 3) : -1;
-      const int te = (int)(rel & 7);
-      const int kt = mine_t ? tv / BLOCK : -1;
-      const int lt = mine_t ? tv - kt * BLOCK : -1;
-      const bool zero_row = (core.g_lp == 0.f && core.g_h == 0.f);
-      auto row_pass = [&](auto mode) {
-        constexpr int kMode = decltype(mode)::value;
-#pragma unroll
-        for (int k = 0; k < NV; ++k) {
-          u32x4 o;
-          if constexpr (kMode == 0) {
-            o = u32x4{0u, 0u, 0u, 0u};
-          } else {
-            float d[8];
-            u32x4 v = x[k];
-            asm volatile("" : "+v"(v));
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const float x0 = bf_lo(v[j]), x1 = bf_hi(v[j]);
-              const float t0 = __builtin_fmaf(x0 - M, c, -l2s), t1 = __builtin_fmaf(x1 - M, c, -l2s);
-              const float p0 = fexp2(t0), p1 = fexp2(t1);
-              if constexpr (kMode == 1) {
-                d[2 * j] = p0 * alpha;
-                d[2 * j + 1] = p1 * alpha;
-              } else {
-                d[2 * j] = p0 * __builtin_fmaf(beta, t0, alpha);
-                d[2 * j + 1] = p1 * __builtin_fmaf(beta, t1, alpha);
-              }
-            }
-            if (__builtin_amdgcn_readfirstlane(k == kt)) {  // the vector holding the target: its owner lane
-              if (tid == lt) {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) d[j] = (j == te) ? __fadd_rn(d[j], gadd) : d[j];
-              }
-            }
-#pragma unroll
-            for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(d[2 * j], d[2 * j + 1]);
-          }
-          store_row_b128(o, ws, voff, k * VSTRIDE);
-        }
-      };
-      if (zero_row)
-        row_pass(std::integral_constant<int, 0>{});
-      else if (beta == 0.f)
-        row_pass(std::integral_constant<int, 1>{});
-      else
-        row_pass(std::integral_constant<int, 2>{});
     }
   }
 }
@@ -1518,19 +1246,7 @@ static int pair_nv(int64_t V) {
   const int64_t nv = (half + 1023) / 1024;
   return (nv >= kPairMinNV && nv <= kPairMaxNV) ? (int)nv : 0;
 }
-// PRL_BF16_PAIR=1: bf16 rows of a Qwen2.5 vocabulary take the double-buffered pair kernel
-static bool pair_bf16_enabled() {
-  const char* e = getenv("PRL_BF16_PAIR");
-  return e && e[0] == '1';
-}
-static bool pair_bf16_fits(int64_t V) {  // both halves: NV - 1 full vectors per lane, the rest <= the last slots
-  const int64_t nvec = V >> 3;
-  return (nvec >> 1) >= (int64_t)(kPairBf16NV - 1) * 1024 &&
-         ((nvec + 1) >> 1) <= (int64_t)(kPairBf16NV - 1) * 1024 + kPairBf16LastLanes;
-}
-
-static hipError_t launch_pair_rows(const KArgs& a, int nv, int64_t nrows, int cus, int dev, hipStream_t s,
-                                   bool bf16 = false) {
+static hipError_t launch_pair_rows(const KArgs& a, int nv, int64_t nrows, int cus, int dev, hipStream_t s) {
   int grid = cus < kPairMaxCUs ? cus : kPairMaxCUs;
   const int64_t need = 2 * nrows;
   if (need < grid) grid = (int)need;
@@ -1547,10 +1263,6 @@ static hipError_t launch_pair_rows(const KArgs& a, int nv, int64_t nrows, int cu
   pa.fallbacks = reinterpret_cast<uint32_t*>(static_cast<char*>(slots) + kPairSlotBytes);
   e = hipMemsetAsync(slots, 0, (size_t)(grid / 2) * 2 * 2 * 16, s);  // tags restart at 1 every launch
   if (e != hipSuccess) return e;
-  if (bf16) {
-    hipLaunchKernelGGL(grpo_fwd_pair_bf16<kPairBf16NV>, dim3(grid), dim3(1024), 0, s, a, pa);
-    return hipGetLastError();
-  }
   return launch_pair_table(nv, a, pa, grid, s, std::make_integer_sequence<int, kPairMaxNV - kPairMinNV + 1>{});
 }
 
@@ -1586,8 +1298,6 @@ static hipError_t launch_rows(const KArgs& a, const PrlGrpoBatch* b, const PrlGr
   const bool bf16 = b->logits_dtype == PRL_BF16;
   const bool vec_ok_bf = bf16 && b->V % 8 == 0 && b->ld % 8 == 0 && aligned16(b->logits) &&
                          (!p->write_grad || aligned16(out->dlogits));
-  if (vec_ok_bf && pair_bf16_enabled() && pair_bf16_fits(b->V))  // A/B: double-buffered half rows over CU pairs
-    return launch_pair_rows(a, kPairBf16NV, nrows, cus, dev, s, true);
   const int nv = vec_ok_bf ? resident_nv(b->V / 8) : 0;  // row <= 24*16 KiB
   if (nv > 0) return launch_resident_nv(nv, a, (int)(nrows < cus ? nrows : cus), s);
   const int64_t want = (int64_t)cus * 4;

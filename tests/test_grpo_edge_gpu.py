@@ -165,27 +165,10 @@ def test_unpacked_bf16_value_head_ragged():
     _cmp(lg, b, dict(CFG, value_loss_coef=0.1), values=values)
 
 
-# bf16 rows of a Qwen2.5 vocabulary: the resident kernel (default) or, with PRL_BF16_PAIR=1, the
-# double-buffered pair kernel (grpo_fwd_pair_bf16<10>: half rows [0, 75 968) and [75 968, 151 936)
-# over two workgroups, the next half row streamed into LDS while this one is computed);
-# PRL_PAIR_SPIN_TICKS=0: its halves never wait for the partner's partial.
-BF16_KERNELS = {"resident": {"PRL_BF16_PAIR": "0"}, "pair": {"PRL_BF16_PAIR": "1"},
-                "pair_nowait": {"PRL_BF16_PAIR": "1", "PRL_PAIR_SPIN_TICKS": "0"}}
-
-
-@pytest.fixture(params=list(BF16_KERNELS))
-def bf16_kernel(request, monkeypatch):
-    for k, v in BF16_KERNELS[request.param].items():
-        monkeypatch.setenv(k, v)
-    return request.param
-
-
-def test_multi_row_per_workgroup(bf16_kernel):
-    """Qwen2.5's vocab (the resident kernel's NV = 19, read / write phased schedule; the pair
-    kernel's double-buffered half rows) with ~2.3 rows per workgroup (pair) of the persistent grid,
-    so rows with and without a next row are both taken: every row's dlogits and every statistic
-    against the oracle, and two runs bitwise identical (the pair kernel also against the run whose
-    halves never wait for each other)."""
+def test_multi_row_per_workgroup():
+    """Qwen2.5's vocab (the resident kernel's NV = 19, read / write phased schedule) with ~2.3 rows
+    per workgroup of the persistent grid, so rows with and without a next row are both taken: every
+    row's dlogits and every statistic against the oracle, and two runs bitwise identical."""
     V = 151936
     lens = [150, 200, 251]
     T = sum(lens)
@@ -194,43 +177,12 @@ def test_multi_row_per_workgroup(bf16_kernel):
     _, d1 = _cmp(lg, b)
     _, _, d2 = _run(lg, b)
     assert np.array_equal(d1, d2)
-    if bf16_kernel == "pair":
-        import os
-
-        os.environ["PRL_PAIR_SPIN_TICKS"] = "0"
-        try:
-            _, _, d3 = _run(lg, b)
-        finally:
-            del os.environ["PRL_PAIR_SPIN_TICKS"]
-        assert np.array_equal(d1, d3)
-
-
-PAIR_BF16_EDGES = [0, 7, 8, 65535, 65536, 73727, 73728, 75967, 75968, 75975, 75976, 149695, 149696, 151935]
-
-
-@pytest.mark.parametrize("ent", [0.0, 0.01])
-def test_pair_bf16_targets_at_half_and_vector_edges(ent, bf16_kernel):
-    """Targets on the pair kernel's half boundary (column 75 968), its LDS-slab / last-vector seam
-    (column 73 728 of each half) and vector edges, with and without the entropy term."""
-    T, V = len(PAIR_BF16_EDGES) + 2, 151936
-    b = _batch(T, V, seed=17, lens=[T], prompts=[1])
-    for r, col in enumerate(PAIR_BF16_EDGES):
-        b["input_ids"][0, 1 + r] = col
-        if b["labels"][0, 1 + r] != -100:
-            b["labels"][0, 1 + r] = col
-    lg = synth.to_bf16(np.random.default_rng(17).normal(0, 2, (1, T, V))).astype(np.float32)
-    cfg = dict(CFG, entropy_bonus=ent, final_entropy_bonus=ent)
-    _, d = _cmp(lg, b, cfg)
-    o = grpo_oracle.rl_step_oracle(lg, b, cfg, 0, 10)
-    for r, col in enumerate(PAIR_BF16_EDGES):
-        if b["labels"][0, 1 + r] != -100:
-            got, want = d[0, r, col], o["dlogits"][0, r, col]
-            assert abs(got - want) <= 1e-2 * abs(want) + 1e-8, (r, col, got, want)
 
 
 @pytest.mark.parametrize("V", [151936, 152064])
-def test_pair_bf16_strided_and_both_vocabularies(V, bf16_kernel):
-    """Both Qwen2.5 vocabularies, logits sliced out of a wider buffer (row stride V + 64)."""
+def test_resident_strided_rows_both_vocabularies(V):
+    """Both Qwen2.5 vocabularies on the resident kernel, logits sliced out of a wider buffer (row
+    stride V + 64)."""
     from pipelinerl_amd.finetune.rl import RLConfig, rl_step
 
     T, W = 9, V + 64
@@ -386,10 +338,9 @@ def test_fp32_pair_kernel_vocab_range(V):
     _cmp(lg, b, dtype=torch.float32)
 
 
-@pytest.mark.parametrize("dtype,env", [(torch.float32, {}), (torch.bfloat16, {"PRL_BF16_PAIR": "1"})],
-                         ids=["fp32_pair", "bf16_pair"])
+@pytest.mark.parametrize("dtype,env", [(torch.float32, {})], ids=["fp32_pair"])
 def test_pair_kernels_beside_a_kernel_holding_cus(dtype, env, monkeypatch):
-    """The pair kernels beside a long kernel on another stream that holds registers on half the CUs
+    """The fp32 pair kernel beside a long kernel on another stream that holds registers on half the CUs
     (as an RCCL collective beside the loss head would): half the workgroups start only as others
     finish; a half whose partner is late stops waiting after the (lowered, 20 us) spin bound and
     computes the partner's partial itself.  The launch completes with the same bits as the

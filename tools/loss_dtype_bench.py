@@ -30,7 +30,7 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 
 
-def f32_kernels_ab(a, bf16: bool = False):
+def f32_kernels_ab(a):
     import os
 
     from pipelinerl_amd.finetune.rl.fused import GrpoParams, grpo_loss
@@ -39,15 +39,10 @@ def f32_kernels_ab(a, bf16: bool = False):
     params = GrpoParams(policy_loss="ppo", epsilon=4.0, kl_coef=0.0, entropy_coef=0.0, clamp_log_ratio=5.0,
                         temperature=1.0, batch_size=4096.0)
     lb, fields = bench.make_workload(a.tokens, a.vocab, 2048, 256, 4321, dev)
-    if bf16:
-        logits = lb
-        arms = {"resident": {"PRL_BF16_PAIR": "0"}, "pair": {"PRL_BF16_PAIR": "1"},
-                "pair_nowait": {"PRL_BF16_PAIR": "1", "PRL_PAIR_SPIN_TICKS": "0"}}
-    else:
-        logits = lb.detach().float().requires_grad_(True)
-        del lb
-        arms = {"pair": {"PRL_F32_PAIR": "1"}, "hybrid": {"PRL_F32_PAIR": "0"},
-                "pair_nowait": {"PRL_F32_PAIR": "1", "PRL_PAIR_SPIN_TICKS": "0"}}
+    logits = lb.detach().float().requires_grad_(True)
+    del lb
+    arms = {"pair": {"PRL_F32_PAIR": "1"}, "hybrid": {"PRL_F32_PAIR": "0"},
+            "pair_nowait": {"PRL_F32_PAIR": "1", "PRL_PAIR_SPIN_TICKS": "0"}}
     torch.cuda.empty_cache()
     alg = 2.0 * a.tokens * a.vocab * logits.element_size() + bench.SIDE_BYTES_PER_TOKEN * a.tokens
     res = {k: [] for k in arms}
@@ -87,7 +82,7 @@ def main():
     ap.add_argument("--vocab", type=int, default=151936)
     ap.add_argument("--inplace", action="store_true", help="separate vs aliased dlogits A/B (bf16)")
     ap.add_argument("--f32-kernels", action="store_true", help="pair vs hybrid fp32 kernels, alternated")
-    ap.add_argument("--bf16-kernels", action="store_true", help="resident vs pair bf16 kernels, alternated")
+
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--dl-offsets", default=None,
                     help="comma-separated byte offsets of the dlogits buffer's start (bf16 A/B of HBM placement)")
@@ -96,8 +91,7 @@ def main():
         return inplace_ab(a)
     if a.f32_kernels:
         return f32_kernels_ab(a)
-    if a.bf16_kernels:
-        return f32_kernels_ab(a, bf16=True)
+
     if a.dl_offsets:
         return offsets_ab(a, [int(x) for x in a.dl_offsets.split(",")])
     from pipelinerl_amd.finetune.rl.fused import GrpoParams, grpo_loss
