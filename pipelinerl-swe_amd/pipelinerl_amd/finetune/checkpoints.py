@@ -92,6 +92,7 @@ def load_model(args, model_class: str, current_dir: Path, device: torch.device, 
         model = AutoModelForCausalLMWithValueHead(model)
         if src == str(current_dir):  # resume: the saved head too (value_model.py:189-192)
             model.load_value_head(current_dir)
+    model.prl_memory_plan = plan  # the FSDP wrap reads gathered_layers (finetune_loop.py, shard_model)
     return model.to(device)
 
 

@@ -18,6 +18,18 @@ forward is the same deterministic kernels on the same inputs).
                       when K = 0.  The results are the same for every K.
   ``always``          the reference's behaviour: checkpoint whenever gradient_checkpointing is set
 ``finetune.gradient_checkpointing_keep_layers`` (build-only, optional int): K itself (A/B runs).
+``finetune.fsdp_keep_gathered_layers`` (build-only, FSDP only): ``auto`` (default) | an int R.
+                      FSDP2 frees each decoder layer's unsharded parameters after its forward and
+                      all-gathers them again for its backward (two all-gathers and a reduce-scatter
+                      per layer and step).  The last R layers instead stay gathered from their forward
+                      to their backward (``reshard_after_forward=False``; they reshard after their
+                      backward, which comes first): one all-gather fewer per layer, at R unsharded
+                      layers more memory at the start of the backward.  ``auto`` spends what the
+                      recompute plan leaves of the device on it (R = spare // a layer's unsharded
+                      parameters, after the allocator's rounding) — activations first, since a
+                      recompute costs a third of a layer's compute and a re-gather only overlappable
+                      communication; ``auto`` needs a sized plan (gradient checkpointing on, a HIP
+                      device), else R = 0, FSDP's default.  0 turns it off.
 
 The estimate is deliberately conservative (upper bounds, measured against the trainer probes'
 peak memory in DESIGN.md): model state = parameters x (weight + gradient + two AdamW moments),
@@ -64,12 +76,15 @@ class RecomputePlan:
     device_bytes: int = 0
     need_bytes: int = 0  # the terms after the allocator's rounding, plus the headroom
     keep_layers: int = -1  # checkpoint: the last keep_layers decoder layers keep their activations
+    gathered_layers: int = 0  # FSDP: the last gathered_layers decoder layers stay unsharded forward -> backward
+    gathered_bytes: int = 0  # what they hold beyond FSDP's default (in need_bytes)
 
     def as_dict(self) -> dict:
         return {"checkpoint": self.checkpoint, "reason": self.reason, "state_gb": round(self.state_bytes / 1e9, 2),
                 "activation_gb": round(self.activation_bytes / 1e9, 2), "logits_gb": round(self.logits_bytes / 1e9, 2),
                 "buffer_gb": round(self.buffer_bytes / 1e9, 2), "device_gb": round(self.device_bytes / 1e9, 2),
-                "need_gb": round(self.need_bytes / 1e9, 2), "keep_layers": self.keep_layers}
+                "need_gb": round(self.need_bytes / 1e9, 2), "keep_layers": self.keep_layers,
+                "gathered_layers": self.gathered_layers, "gathered_gb": round(self.gathered_bytes / 1e9, 2)}
 
 
 def activation_bytes_per_token(config, dtype_bytes: int = 2) -> int:
@@ -143,10 +158,50 @@ def fsdp_transient_bytes(model, shard_world: int, act: int, logits: int, head_gr
     return max(start, end) - act
 
 
+def gathered_layer_bytes(model) -> int:
+    """The largest decoder layer's unsharded parameters as FSDP2 allocates them (one block per
+    parameter, reused across gathers) after the device allocator's rounding."""
+    from ..devalloc import round_size
+    from .sharding import decoder_layers
+
+    return max((sum(round_size(p.numel() * p.element_size()) for p in m.parameters())
+                for m in decoder_layers(model)), default=0)
+
+
+def plan_fsdp_gathering(args, model, plan: RecomputePlan, shard_world: int) -> RecomputePlan:
+    """``plan`` with ``gathered_layers`` / ``gathered_bytes`` set (finetune.fsdp_keep_gathered_layers,
+    module docstring); ``need_bytes`` grows by the gathered bytes."""
+    policy = args.get("fsdp_keep_gathered_layers", "auto")
+    if policy != "auto" and (isinstance(policy, bool) or not isinstance(policy, int) or policy < 0):
+        raise ValueError(f"fsdp_keep_gathered_layers must be 'auto' or an int >= 0, got {policy!r}")
+    if int(shard_world) <= 1:
+        return plan
+    from .sharding import decoder_layers
+
+    L = len(decoder_layers(model))
+    per = gathered_layer_bytes(model)
+    if policy == "auto":
+        if plan.need_bytes <= 0 or plan.device_bytes <= 0 or per <= 0:
+            return plan  # unsized: FSDP's default
+        n = min(L, max(0, (plan.device_bytes - plan.need_bytes) // per))
+    else:
+        n = min(L, int(policy))
+    plan.gathered_layers, plan.gathered_bytes = int(n), int(n) * per
+    if plan.need_bytes > 0:
+        plan.need_bytes += plan.gathered_bytes
+    return plan
+
+
 def plan_gradient_checkpointing(args, model, device: torch.device, shard_world: int = 1,
                                 device_bytes: int | None = None) -> RecomputePlan:
     """The decision for ``model`` (already built) under the trainer config ``args``;
-    ``device_bytes``: the device's memory (default: queried from the HIP device)."""
+    ``device_bytes``: the device's memory (default: queried from the HIP device).  Under FSDP
+    (``shard_world`` > 1) also how many decoder layers stay gathered (plan_fsdp_gathering)."""
+    return plan_fsdp_gathering(args, model, _plan_recompute(args, model, device, shard_world, device_bytes),
+                               shard_world)
+
+
+def _plan_recompute(args, model, device: torch.device, shard_world: int, device_bytes: int | None) -> RecomputePlan:
     if not args.get("gradient_checkpointing", False):
         return RecomputePlan(False, "gradient_checkpointing is off")
     policy = str(args.get("gradient_checkpointing_policy", "auto"))

@@ -47,8 +47,12 @@ def decoder_layers(model) -> list[torch.nn.Module]:
     return [m for m in model.modules() if type(m).__name__.endswith("DecoderLayer")]
 
 
-def shard_model(model, fsdp_cfg=None, grad_reduce: str = "mean", reshard_after_forward: bool = True):
-    """Shard ``model`` in place over the default process group; returns it (an FSDPModule)."""
+def shard_model(model, fsdp_cfg=None, grad_reduce: str = "mean", reshard_after_forward: bool = True,
+                keep_gathered: int = 0):
+    """Shard ``model`` in place over the default process group; returns it (an FSDPModule).
+    ``keep_gathered``: the last that many decoder layers keep their unsharded parameters from their
+    forward to their backward (``reshard_after_forward=False``: one all-gather per step instead of
+    two; sized by finetune/recompute.py plan_fsdp_gathering)."""
     from torch.distributed.device_mesh import init_device_mesh
     from torch.distributed.fsdp import MixedPrecisionPolicy, fully_shard
 
@@ -65,8 +69,10 @@ def shard_model(model, fsdp_cfg=None, grad_reduce: str = "mean", reshard_after_f
     mp = MixedPrecisionPolicy(param_dtype=pd if pd not in (None, store) else None,
                               reduce_dtype=rd if rd not in (None, store) else None)
     layers = decoder_layers(model)
-    for layer in layers:
-        fully_shard(layer, mesh=mesh, mp_policy=mp, reshard_after_forward=reshard_after_forward)
+    first_gathered = len(layers) - max(0, min(int(keep_gathered), len(layers)))
+    for i, layer in enumerate(layers):
+        fully_shard(layer, mesh=mesh, mp_policy=mp,
+                    reshard_after_forward=reshard_after_forward and i < first_gathered)
     fully_shard(model, mesh=mesh, mp_policy=mp, reshard_after_forward=reshard_after_forward)
     for m in [*layers, model]:
         if grad_reduce == "sum":
@@ -74,7 +80,8 @@ def shard_model(model, fsdp_cfg=None, grad_reduce: str = "mean", reshard_after_f
         if "nccl" not in str(dist.get_backend()):  # gloo has no PREMUL_SUM / AVG: plain SUM + a scale
             m.set_force_sum_reduction_for_comms(True)
     logger.info(f"FSDP: {len(layers)} decoder layers + root sharded over {dist.get_world_size()} ranks "
-                f"(param_dtype {mp.param_dtype}, reduce_dtype {mp.reduce_dtype})")
+                f"(param_dtype {mp.param_dtype}, reduce_dtype {mp.reduce_dtype}; the last "
+                f"{len(layers) - first_gathered} layers stay gathered from forward to backward)")
     return model
 
 

@@ -210,7 +210,9 @@ def run_finetuning_loop(cfg, step_fn: Callable = rl_step, model=None, tokenizer=
     if tokenizer is None:
         tokenizer = load_tokenizer(args.config_name, getattr(getattr(model, "config", None), "eos_token_id", None))
     if sharded:  # before the optimizer: it must see the sharded parameters
-        model = shard_model(model, cfg.get("fsdp"), grad_reduce=args.get("grad_reduce", "mean"))
+        plan = getattr(model, "prl_memory_plan", None)  # load_model's (finetune/recompute.py)
+        model = shard_model(model, cfg.get("fsdp"), grad_reduce=args.get("grad_reduce", "mean"),
+                            keep_gathered=plan.gathered_layers if plan is not None else 0)
     elif args.get("flat_parameters", True):
         # every bf16 parameter into one buffer in the weight broadcast's layout (weight_update.py):
         # in-place broadcasts, the gate / up projections one tensor without a concatenation copy

@@ -37,6 +37,15 @@ def _loop_rank(rank, world, port, exp, steps, passes, extra):
     captured = {}
 
     def step(model, batch, cur, mx, config):
+        if "model" not in captured:
+            from pipelinerl_amd.finetune.sharding import decoder_layers
+
+            def at_final_norm(mod, inp):  # every decoder layer's forward is done, no backward yet
+                captured["unsharded_at_norm"] = [not any(isinstance(p, DTensor) for p in layer.parameters())
+                                                 for layer in decoder_layers(model)]
+
+            norm = next(m for n, m in model.named_modules() if n.endswith("model.norm"))
+            norm.register_forward_pre_hook(at_final_norm)
         captured["model"] = model
         return cpu_rl_step(model, batch, cur, mx, config)
 
@@ -47,8 +56,9 @@ def _loop_rank(rank, world, port, exp, steps, passes, extra):
     from pipelinerl_amd.finetune.sharding import decoder_layers
 
     flags = [bool(getattr(layer, "gradient_checkpointing", False)) for layer in decoder_layers(captured["model"])]
-    (exp / f"metrics_w{world}_r{rank}.json").write_text(json.dumps({"steps": m.completed_steps,
-                                                                    "samples": m.samples, "ckpt_flags": flags}))
+    (exp / f"metrics_w{world}_r{rank}.json").write_text(json.dumps({
+        "steps": m.completed_steps, "samples": m.samples, "ckpt_flags": flags,
+        "unsharded_at_norm": captured.get("unsharded_at_norm")}))
     if dist.is_initialized():
         dist.destroy_process_group()
 
@@ -180,3 +190,25 @@ def test_fsdp_loop_with_partial_recompute_matches(tmp_path):
         assert flags == ([False, False] if name == "plain" else [True, False]), (name, flags)
     worst = max(float((runs["plain"][n] - runs["ckpt"][n]).abs().max()) for n in runs["plain"])
     assert worst < 2e-6, worst
+
+
+def test_fsdp_loop_keeps_planned_layers_gathered(tmp_path):
+    """finetune.fsdp_keep_gathered_layers (finetune/recompute.py plan_fsdp_gathering -> shard_model):
+    the last decoder layer keeps its unsharded parameters from its forward to its backward (seen
+    from a hook at the final norm: every forward done, no backward yet), the first one is resharded
+    as FSDP2 does by default; the parameters after two steps are bit-identical to the default wrap
+    (the same all-gathered values feed the same computation)."""
+    from test_finetune_loop_cpu import free_port
+
+    runs = {}
+    for name, extra in (("plain", {"sharding": "fsdp"}),
+                        ("gathered", {"sharding": "fsdp", "fsdp_keep_gathered_layers": 1})):
+        exp = tmp_path / name
+        exp.mkdir()
+        per_step, _ = _setup(exp, 2)
+        mp.spawn(_loop_rank, args=(2, free_port(), str(exp), 2, per_step, extra), nprocs=2, join=True)
+        runs[name] = torch.load(exp / "params_w2_r0.pt")
+        seen = json.loads((exp / "metrics_w2_r0.json").read_text())["unsharded_at_norm"]
+        assert seen == ([False, False] if name == "plain" else [False, True]), (name, seen)
+    for n in runs["plain"]:
+        assert torch.equal(runs["plain"][n], runs["gathered"][n]), n

@@ -194,7 +194,8 @@ def test_partial_recompute_keeps_the_layers_that_fit(monkeypatch):
     # fewer kept layers need less; keeping all 64 is the no-recompute plan
     lo = plan_gradient_checkpointing(_args(gradient_checkpointing_keep_layers=0), m32, cuda, shard_world=4,
                                      device_bytes=dev)
-    assert lo.checkpoint and lo.keep_layers == 0 and lo.need_bytes < p.need_bytes
+    # (before the spare memory goes to FSDP layers kept gathered, plan_fsdp_gathering)
+    assert lo.checkpoint and lo.keep_layers == 0 and lo.need_bytes - lo.gathered_bytes < p.need_bytes - p.gathered_bytes
     allk = plan_gradient_checkpointing(_args(gradient_checkpointing_keep_layers=64), m32, cuda, shard_world=4,
                                        device_bytes=dev)
     assert not allk.checkpoint
@@ -229,3 +230,48 @@ def test_keep_activations_flags_the_last_layers_and_gradients_are_unchanged():
     for keep in (0, 2, 4):
         for n, g in grads[None].items():
             assert torch.equal(g, grads[keep][n]), (keep, n)
+
+
+def test_fsdp_gathered_layers_spend_the_spare_memory(monkeypatch):
+    """plan_fsdp_gathering: under FSDP the spare device memory after the recompute plan keeps the
+    last R decoder layers' unsharded parameters from forward to backward (R = spare // a layer's
+    rounded unsharded bytes); need_bytes grows by them and stays within the device; the explicit
+    int overrides, 0 turns it off; unsharded (shard_world 1) or unsized plans keep FSDP's default."""
+    from pipelinerl_amd import devalloc
+    from pipelinerl_amd.finetune.recompute import gathered_layer_bytes, plan_gradient_checkpointing
+
+    for k in devalloc.ENV_KEYS:
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setattr(devalloc, "_applied", devalloc.DEFAULT_SETTINGS)
+    m32 = _meta_model("32b")
+    cuda, dev = torch.device("cuda"), 288 * 2 ** 30
+    per = gathered_layer_bytes(m32)
+    raw = (2 * 5120 * 5120 + 2 * 1024 * 5120 + 3 * 27648 * 5120 + 5120 + 2 * 1024 + 2 * 5120) * 2
+    assert raw <= per <= 1.1 * raw
+    # C5 on 8 ranks at 4 096 tokens: no recompute, the spare holds every layer
+    p8 = plan_gradient_checkpointing(_args(seq_length=4096), m32, cuda, shard_world=8, device_bytes=dev)
+    base = plan_gradient_checkpointing(_args(seq_length=4096, fsdp_keep_gathered_layers=0), m32, cuda,
+                                       shard_world=8, device_bytes=dev)
+    assert not p8.checkpoint and base.gathered_layers == 0
+    assert p8.gathered_layers == min(64, (dev - base.need_bytes) // per) > 0, p8.as_dict()
+    assert p8.need_bytes == base.need_bytes + p8.gathered_layers * per <= dev
+    # C5 on 4 ranks at 12 000 tokens (partial recompute): what is left after the kept activations
+    p4 = plan_gradient_checkpointing(_args(), m32, cuda, shard_world=4, device_bytes=dev)
+    assert p4.checkpoint and 0 <= p4.gathered_layers <= (dev - (p4.need_bytes - p4.gathered_bytes)) // per
+    assert p4.need_bytes <= dev
+    # a tighter device gathers fewer: as many as fit, not one more
+    tdev = base.need_bytes + 3 * per + per // 2
+    tight = plan_gradient_checkpointing(_args(seq_length=4096), m32, cuda, shard_world=8, device_bytes=tdev)
+    assert 0 < tight.gathered_layers < p8.gathered_layers, tight.as_dict()
+    assert tight.need_bytes <= tdev < tight.need_bytes + per
+    # explicit R; unsharded; unsized (policy always); invalid values
+    assert plan_gradient_checkpointing(_args(seq_length=4096, fsdp_keep_gathered_layers=5), m32, cuda,
+                                       shard_world=8, device_bytes=dev).gathered_layers == 5
+    assert plan_gradient_checkpointing(_args(seq_length=4096), m32, cuda, shard_world=1,
+                                       device_bytes=dev).gathered_layers == 0
+    assert plan_gradient_checkpointing(_args(gradient_checkpointing_policy="always"), m32, cuda, shard_world=8,
+                                       device_bytes=dev).gathered_layers == 0
+    for bad in (-1, "all", True):
+        with pytest.raises(ValueError):
+            plan_gradient_checkpointing(_args(fsdp_keep_gathered_layers=bad), m32, cuda, shard_world=8,
+                                        device_bytes=dev)
