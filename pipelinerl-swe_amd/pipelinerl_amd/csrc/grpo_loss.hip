@@ -190,6 +190,46 @@ __device__ __forceinline__ int64_t perm_row(int64_t i, int64_t n) {
 #endif
 }
 
+#ifndef PRL_FOLD_EXP
+// 1: the exponent arguments on element pairs (packed FP32 ops): pass 1 y = (x - m) c with two
+// partial sums per lane; pass 2 t = (x - M) c + k with a per-row constant k, and without an entropy
+// term d = sign(alpha) 2^((x - M) c + log2|alpha| - log2 S): alpha folded into the exponent, its
+// sign applied to the packed bf16 result, no multiply.  x - M stays an exact subtraction (x c - M c
+// would lose |M c| ulp-scale accuracy at large logits: the scale-2000 edge test).  0: the scalar
+// forms of the other kernels.  Results agree within the fp32 rounding of the exponent's argument.
+#define PRL_FOLD_EXP 1
+#endif
+constexpr bool kFoldExp = PRL_FOLD_EXP != 0;
+
+// Pass 1's online state on element pairs: (max, pairwise sums of 2^y and 2^y y).
+struct Lse2 {
+  float m;
+  f32x2 s, w;
+};
+template <int N>
+__device__ __forceinline__ void lse2_add(Lse2& st, const float (&x)[N], float c) {
+  float vm = x[0];
+#pragma unroll
+  for (int j = 1; j < N; ++j) vm = fmaxf(vm, x[j]);
+  if ((vm - st.m) * c > kRescaleSlack) {  // lse_rebase on both halves
+    const float d = (st.m - vm) * c;
+    const float f = fexp2(d);
+    st.w = f * (st.s * d + st.w);
+    st.s = st.s * f;
+    st.m = vm;
+  }
+  const f32x2 cc = {c, c}, mm = {st.m, st.m};
+#pragma unroll
+  for (int j = 0; j < N; j += 2) {
+    const f32x2 xv = {x[j], x[j + 1]};
+    const f32x2 y = (xv - mm) * cc;
+    const f32x2 e = {fexp2(y.x), fexp2(y.y)};
+    st.s += e;
+    st.w = e * y + st.w;
+  }
+  if (vm != vm) st.m = __builtin_nanf("");  // a NaN logit poisons the state
+}
+
 template <int NV>
 __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
   constexpr int BLOCK = 1024, NW = BLOCK / 64;
@@ -245,6 +285,7 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
 
     // ---- pass 1: row statistics from registers
     Lse st = lse_empty();
+    Lse2 st2 = {kEmptyMax, {0.f, 0.f}, {0.f, 0.f}};
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
       u32x4 v = buf[k];
@@ -255,8 +296,12 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
         x[2 * j] = bf_lo(v[j]);
         x[2 * j + 1] = bf_hi(v[j]);
       }
-      lse_add<8>(st, x, c);
+      if constexpr (kFoldExp)
+        lse2_add<8>(st2, x, c);
+      else
+        lse_add<8>(st, x, c);
     }
+    if constexpr (kFoldExp) st = Lse{st2.m, st2.s.x + st2.s.y, st2.w.x + st2.w.y};
     st = wave_reduce_lse(st, c);
     if (lane == 0) {
       red[par][wid][0] = st.m;
@@ -290,6 +335,11 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
       const float alpha = -(core.g_lp + core.g_h * H) * inv_t;
       const float beta = -core.g_h * kLn2 * inv_t;
       const float gadd = core.g_lp * inv_t;
+      // folded forms (kFoldExp): t = (x - M) c + k2 (k2 = -log2 S); without an entropy term
+      // d = sign(alpha) 2^((x - M) c + k1), k1 = log2|alpha| - log2 S (alpha = 0: -inf, d = 0)
+      const float k2 = -l2s;
+      const float k1 = log2f(fabsf(alpha)) - l2s;
+      const uint32_t sgn2 = alpha < 0.f ? 0x80008000u : 0u;
       const int tv = tgt < 0 ? -1 : (int)(tgt >> 3);
       const int te = (int)(tgt & 7);
       const int kt = tv < 0 ? -1 : tv / BLOCK;
@@ -314,6 +364,24 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
             // form branch (8 instead of 4 live VGPRs per vector: spills)
             u32x4 v = buf[k];
             asm volatile("" : "+v"(v));
+            if constexpr (kFoldExp && kTargetFixup) {
+              const f32x2 cc = {c, c}, mm = {M, M}, kk = {kMode == 1 ? k1 : k2, kMode == 1 ? k1 : k2};
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                const f32x2 xv = {bf_lo(v[j]), bf_hi(v[j])};
+                const f32x2 t = (xv - mm) * cc + kk;
+                const f32x2 p = {fexp2(t.x), fexp2(t.y)};
+                if constexpr (kMode == 1) {
+                  o[j] = pack_bf16x2(p.x, p.y) ^ sgn2;
+                } else {
+                  const f32x2 g = t * f32x2{beta, beta} + f32x2{alpha, alpha};
+                  const f32x2 dd = p * g;
+                  o[j] = pack_bf16x2(dd.x, dd.y);
+                }
+              }
+              store_row_b128(o, ws, voff, k * VSTRIDE);
+              continue;
+            }
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               const float x0 = bf_lo(v[j]), x1 = bf_hi(v[j]);
@@ -381,8 +449,19 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
           // (so this 2-B store lands after the 16-B store of the same bytes): the same operations
           // as the vector loop on the same bf16 value, rounded the same way (no contraction)
           if (tid == lt && !zero_row) {
-            const float tt = __builtin_fmaf(xt - M, c, -l2s);
-            const float dm = __fmul_rn(fexp2(tt), beta == 0.f ? alpha : __builtin_fmaf(beta, tt, alpha));
+            float dm;
+            if constexpr (kFoldExp) {
+              if (kNoEntropyForm && beta == 0.f) {
+                const float pt = fexp2(__builtin_fmaf(xt - M, c, k1));
+                dm = alpha < 0.f ? -pt : pt;
+              } else {
+                const float tt = __builtin_fmaf(xt - M, c, k2);
+                dm = __fmul_rn(fexp2(tt), __builtin_fmaf(tt, beta, alpha));
+              }
+            } else {
+              const float tt = __builtin_fmaf(xt - M, c, -l2s);
+              dm = __fmul_rn(fexp2(tt), beta == 0.f ? alpha : __builtin_fmaf(beta, tt, alpha));
+            }
             dl[lrow * a.ld + tgt] = f_to_bf(__fadd_rn(dm, gadd));
           }
         }

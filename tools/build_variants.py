@@ -21,7 +21,8 @@ VARIANTS = {  # the loss head's A/B builds (csrc/grpo_loss.hip macros); profiles
     "stream_store_nt": {"PRL_STREAM_STORE_SC1": "0"},
     "vec_row_inputs": {"PRL_SCALAR_ROW_INPUTS": "0"},
     "target_select": {"PRL_TARGET_FIXUP": "0"},
-    "hyb_off": {"PRL_HYB_NL": "-1"},  # fp32 rows on the streaming kernel instead of the part-resident one
+    "hyb_off": {"PRL_HYB_NL": "-1"},
+    "fold_off": {"PRL_FOLD_EXP": "0"},  # the bf16 kernel's (x - M) c exponent forms (round 2-5)  # fp32 rows on the streaming kernel instead of the part-resident one
 }
 
 if __name__ == "__main__":
