@@ -6,7 +6,12 @@ One step = what rl_step does for a micro-batch after the model forward (rl/__ini
 fused HIP forward (log-softmax + gather + entropy + PPO/KL loss + stats + dlogits), the
 autograd backward (upstream-gradient check on device), the one D2H read of the statistics,
 and for N > 1 the per-pass sample-count exchange of the DP loop (finetune_loop.py:613,
-all-reduce of one int64 over RCCL).
+all-reduce of one int64 over RCCL).  The statistics are read back as the trainer loop reads them
+(rl_step(defer_stats=True): an async copy into pinned memory, resolved later) so the GPU queue
+does not drain between micro-batches: in the loop the model's backward is queued when a
+micro-batch's statistics are resolved; here the loss head's backward is a few microseconds, so a
+micro-batch's statistics are resolved once the next micro-batch is queued (every step's are read
+inside the timed region; the last one's before the closing synchronize).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...     (one rank per GPU)
@@ -472,8 +477,14 @@ def main():
                         temperature=1.0, batch_size=4096.0)
     samples = torch.zeros(1, dtype=torch.int64, device=dev)
     fwd_ev = []
+    # the statistics' read-back as rl_step(defer_stats=True) does it: one async D2H copy into pinned
+    # memory per micro-batch (two slots: one resolving while the next is written), waited on later
+    from pipelinerl_amd._native import NSTAT
 
-    def step(timed: bool):
+    host_stats = [torch.empty(NSTAT, dtype=torch.float64, pin_memory=True) for _ in range(2)]
+    resolved = []
+
+    def step(timed: bool, i: int):
         logits.grad = None
         if timed:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -482,22 +493,35 @@ def main():
         if timed:
             e1.record()
             fwd_ev.append((e0, e1))
+        host_stats[i % 2].copy_(stats, non_blocking=True)  # the one statistics read-back per micro-batch
+        copied = torch.cuda.Event()
+        copied.record()
         loss.backward()
-        host = stats.cpu()  # the one statistics read-back per micro-batch
         if world > 1:
             samples.fill_(T // 2048)
             dist.all_reduce(samples)
-        return host
+        return copied, i % 2
 
-    for _ in range(args.warmup):
-        step(False)
+    def resolve(pending):
+        if pending is not None:
+            pending[0].synchronize()
+            resolved.append(float(host_stats[pending[1]][0]))  # (the loss term, kept as a use of the read)
+
+    def run(n: int, timed: bool):
+        pending = None
+        for i in range(n):
+            nxt = step(timed, i)
+            resolve(pending)  # micro-batch i - 1's statistics, micro-batch i queued behind them
+            pending = nxt
+        resolve(pending)
+
+    run(args.warmup, False)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
+    run(args.steps, True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
