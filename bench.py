@@ -602,7 +602,9 @@ def main():
         fsdp = optional("fsdp_32b", lambda: fsdp_step_probe("32b", tokens=2048 if rehearse else 4096, micro_batches=1,
                                                              steps=2, warmup=1,
                                                              device=dev, kl_coef=0.001,
-                                                             layers=2 if rehearse else None))
+                                                             layers=2 if rehearse else None,
+                                                             # (gloo on one GPU: ~100 s per FSDP step)
+                                                             gathered_ab=not rehearse))
     split = None
     if world > 1 and not args.no_split_pipeline:
         # configs[3] (C4): half the ranks train Qwen2.5-7B shapes data-parallel, the other half are

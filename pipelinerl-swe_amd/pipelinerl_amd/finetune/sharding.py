@@ -85,6 +85,17 @@ def shard_model(model, fsdp_cfg=None, grad_reduce: str = "mean", reshard_after_f
     return model
 
 
+def set_kept_gathered(model, keep: int) -> int:
+    """At run time: the last ``keep`` decoder layers of a sharded model stay gathered from forward to
+    backward, the others reshard after their forward (FSDPModule.set_reshard_after_forward).
+    Returns how many layers stay gathered."""
+    layers = decoder_layers(model)
+    first = len(layers) - max(0, min(int(keep), len(layers)))
+    for i, layer in enumerate(layers):
+        layer.set_reshard_after_forward(i < first, recurse=False)
+    return len(layers) - first
+
+
 def set_gradient_sync(model, enabled: bool) -> None:
     if is_sharded(model):
         model.set_requires_gradient_sync(enabled)

@@ -212,3 +212,43 @@ def test_fsdp_loop_keeps_planned_layers_gathered(tmp_path):
         assert seen == ([False, False] if name == "plain" else [False, True]), (name, seen)
     for n in runs["plain"]:
         assert torch.equal(runs["plain"][n], runs["gathered"][n]), n
+
+
+def _toggle_rank(rank, port, out):
+    sys.path[:0] = [str(ROOT), str(ROOT / "pipelinerl-swe_amd")]
+    os.environ["OMP_NUM_THREADS"] = "1"
+    import torch.distributed as dist
+    from torch.distributed.tensor import DTensor
+    from transformers import AutoModelForCausalLM, Qwen2Config
+
+    from pipelinerl_amd.finetune.sharding import decoder_layers, set_kept_gathered, shard_model
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=2)
+    torch.manual_seed(0)
+    cfg = Qwen2Config(vocab_size=64, hidden_size=32, intermediate_size=64, num_hidden_layers=4,
+                      num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=64)
+    model = shard_model(AutoModelForCausalLM.from_config(cfg, dtype=torch.float32))
+    seen = []
+    model.model.norm.register_forward_pre_hook(lambda m, a: seen.append(
+        [not any(isinstance(p, DTensor) for p in layer.parameters()) for layer in decoder_layers(model)]))
+    ids = torch.randint(0, 64, (1, 12), generator=torch.Generator().manual_seed(rank))
+    res = []
+    for keep in (0, 2, 4, 0):
+        res.append(set_kept_gathered(model, keep))
+        model(input_ids=ids, labels=ids).loss.backward()
+    if rank == 0:
+        Path(out).write_text(json.dumps({"returned": res, "seen": seen}))
+    dist.destroy_process_group()
+
+
+def test_set_kept_gathered_toggles_at_run_time(tmp_path):
+    """sharding.set_kept_gathered on an already sharded model (the bench's fsdp_32b A/B): the last
+    ``keep`` layers hold their unsharded parameters at the final norm, the rest are resharded."""
+    from test_weight_update_cpu import free_port
+
+    out = tmp_path / "seen.json"
+    mp.spawn(_toggle_rank, args=(free_port(), str(out)), nprocs=2, join=True)
+    r = json.loads(out.read_text())
+    assert r["returned"] == [0, 2, 4, 0]
+    F, T = False, True
+    assert r["seen"] == [[F, F, F, F], [F, F, T, T], [T, T, T, T], [F, F, F, F]], r["seen"]
