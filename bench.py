@@ -40,7 +40,9 @@ At N > 1, last, BASELINE.json configs[3] (C4) is measured under "split_pipeline"
 broadcasts each step's weights to them (WeightUpdateManager -> WorkerExtension) while the
 trainers run the next step.  The trainers' step time with and without the broadcast in flight
 gives hidden_frac (1.0 = the broadcast latency is fully overlapped).  At N >= 4, "fsdp_32b":
-BASELINE.json configs[4] (C5), Qwen2.5-32B shapes sharded with FSDP2 over all ranks, KL on.
+BASELINE.json configs[4] (C5), Qwen2.5-32B shapes sharded with FSDP2 over all ranks, KL on; last,
+"fsdp_32b_kept_gathered": the same with the memory plan's decoder layers kept gathered from forward
+to backward (one all-gather per layer fewer), and its speedup over "fsdp_32b".
 
 At N = 1, "snapshot_overlap" prices the trainer-side half of "weight broadcast fully overlapped":
 C3's 7B step with no weight update, with WeightUpdateManager's staging copy in flight after each
@@ -602,9 +604,7 @@ def main():
         fsdp = optional("fsdp_32b", lambda: fsdp_step_probe("32b", tokens=2048 if rehearse else 4096, micro_batches=1,
                                                              steps=2, warmup=1,
                                                              device=dev, kl_coef=0.001,
-                                                             layers=2 if rehearse else None,
-                                                             # (gloo on one GPU: ~100 s per FSDP step)
-                                                             gathered_ab=not rehearse))
+                                                             layers=2 if rehearse else None))
     split = None
     if world > 1 and not args.no_split_pipeline:
         # configs[3] (C4): half the ranks train Qwen2.5-7B shapes data-parallel, the other half are
@@ -641,6 +641,22 @@ def main():
                     "weight_broadcast": comm_probe.broadcast_probe(shapes, dev, iters=3)}
 
         comm = optional("exchange", exchange)
+    fsdp_kept = None
+    if world >= 4 and not args.no_fsdp and not rehearse:
+        # C5 again with the loop's memory plan applied: the last R decoder layers kept gathered from
+        # forward to backward (finetune.fsdp_keep_gathered_layers), beside fsdp_32b's FSDP2 default.
+        # Last, as its own probe: it holds up to every layer unsharded, and a failure here costs no
+        # other probe.  (Not in a one-GPU rehearsal: ~100 s per FSDP step over gloo.)
+        from pipelinerl_amd.trainer_probe import fsdp_step_probe
+
+        def kept_run():
+            r = fsdp_step_probe("32b", tokens=4096, micro_batches=1, steps=2, warmup=1, device=dev, kl_coef=0.001,
+                                keep_gathered="plan")
+            if isinstance(fsdp, dict) and fsdp.get("ms_per_optimizer_step"):
+                r["speedup_vs_fsdp_32b"] = round(fsdp["ms_per_optimizer_step"] / r["ms_per_optimizer_step"], 4)
+            return r
+
+        fsdp_kept = optional("fsdp_32b_kept_gathered", kept_run)
 
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
@@ -694,7 +710,7 @@ def main():
             out["snapshot_overlap"] = dict(c3.pop("snapshot_overlap"), step="c3_dp (Qwen2.5-7B, 4 micro-batches)")
         for key, res in (("communicators", census), ("c3_dp", c3), ("trainer_step", trainer),
                          ("loss_head_fp32", fp32), ("fsdp_32b", fsdp),
-                         ("split_pipeline", split), ("exchange", comm)):
+                         ("split_pipeline", split), ("exchange", comm), ("fsdp_32b_kept_gathered", fsdp_kept)):
             if res is not None:
                 out[key] = res
         out["probe_wall_s"] = probe_wall

@@ -607,48 +607,43 @@ def dp_step_probe(config: str = "c3", micro_batches: int = 4, steps: int = 2, wa
 
 def fsdp_step_probe(name: str = "32b", tokens: int = 4096, seq: int = 2048, prompt: int = 256,
                     micro_batches: int = 1, steps: int = 2, warmup: int = 1, device=None, kl_coef: float = 0.001,
-                    layers: int | None = None, gathered_ab: bool = True) -> dict:
+                    layers: int | None = None, keep_gathered: int | str = 0) -> dict:
     """BASELINE.json configs[4] (C5): Qwen2.5-32B shapes sharded with FSDP2 over every rank (RCCL
     all-gather / reduce-scatter), KL-to-reference on, packed micro-batches; the whole optimizer
     step as the trainer runs it with ``sharding: fsdp``.  Collective over the default group.
 
-    Timed first with FSDP2's default (every decoder layer resharded after its forward, gathered
-    again for its backward), then, under "kept_gathered", with the loop's memory plan applied
-    (finetune/recompute.py plan_fsdp_gathering: the last R layers stay gathered forward -> backward,
-    one all-gather per layer fewer), the same model and batches (``gathered_ab``)."""
+    ``keep_gathered``: how many of the last decoder layers stay gathered from forward to backward
+    (0: FSDP2's default, every layer resharded after its forward and gathered again for its
+    backward); "plan": as many as the loop's memory plan gives for this micro-batch size
+    (finetune/recompute.py plan_fsdp_gathering, gradient checkpointing as the reference config sets
+    it, policy auto) — one all-gather per kept layer and step fewer."""
     from .finetune.recompute import plan_gradient_checkpointing
     from .finetune.sharding import set_kept_gathered
 
     device = device or torch.device("cuda", torch.cuda.current_device())
     torch.cuda.reset_peak_memory_stats(device)
     ts = TrainerStep(name, tokens, seq, prompt, micro_batches, device, fsdp=True, kl_coef=kl_coef, layers=layers)
-    sec = ts.timed(steps, warmup)
     world = ts.world
+    plan = None
+    if keep_gathered == "plan":
+        plan = plan_gradient_checkpointing({"gradient_checkpointing": True, "seq_length": tokens}, ts.model, device,
+                                           shard_world=world)
+        keep_gathered = 0 if plan.checkpoint else plan.gathered_layers
+    kept = set_kept_gathered(ts.model, int(keep_gathered))
+    sec = ts.timed(steps, warmup)
     peak = torch.cuda.max_memory_allocated(device) / 1e9
-    total = tokens * micro_batches * world
-    # the plan the loop would make for this micro-batch size (gradient checkpointing as the reference
-    # config sets it, policy auto): how many layers the spare memory keeps gathered
-    plan = plan_gradient_checkpointing({"gradient_checkpointing": True, "seq_length": tokens}, ts.model, device,
-                                       shard_world=world)
-    kept = None
-    if gathered_ab and plan.gathered_layers > 0 and not plan.checkpoint:
-        R = set_kept_gathered(ts.model, plan.gathered_layers)
-        torch.cuda.reset_peak_memory_stats(device)
-        sec_g = ts.timed(steps, warmup)
-        kept = {"layers": R, "plan_gathered_gb": round(plan.gathered_bytes / 1e9, 2),
-                "ms_per_optimizer_step": round(sec_g * 1e3, 2), "tokens_per_s": round(total / sec_g, 1),
-                "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 1e9, 2),
-                "speedup_vs_default": round(sec / sec_g, 4)}
     ts.close()
+    total = tokens * micro_batches * world
     n_layers = layers or QWEN[name]["num_hidden_layers"]
-    return {"model": f"Qwen2.5-{name} shapes ({n_layers} layers, random init, bf16), FSDP2 over {world} ranks",
-            "kl_coef": kl_coef, "tokens_per_micro_batch": tokens, "micro_batches_per_step": micro_batches,
-            "seq_len": seq, "ms_per_optimizer_step": round(sec * 1e3, 2), "tokens_per_s": round(total / sec, 1),
-            "tokens_per_s_per_gpu": round(total / sec / world, 1), "peak_mem_gb": round(peak, 2),
-            "steps": steps, "warmup": warmup,
-            "kept_gathered": kept if kept is not None else
-            {"layers": 0, "reason": "not measured" if not gathered_ab else
-             plan.reason if plan.checkpoint else "no spare memory in the plan"}}
+    out = {"model": f"Qwen2.5-{name} shapes ({n_layers} layers, random init, bf16), FSDP2 over {world} ranks",
+           "kl_coef": kl_coef, "tokens_per_micro_batch": tokens, "micro_batches_per_step": micro_batches,
+           "seq_len": seq, "ms_per_optimizer_step": round(sec * 1e3, 2), "tokens_per_s": round(total / sec, 1),
+           "tokens_per_s_per_gpu": round(total / sec / world, 1), "peak_mem_gb": round(peak, 2),
+           "steps": steps, "warmup": warmup, "kept_gathered_layers": kept}
+    if plan is not None:
+        out["plan"] = {k: v for k, v in plan.as_dict().items() if k in ("reason", "need_gb", "device_gb",
+                                                                        "gathered_layers", "gathered_gb")}
+    return out
 
 
 def split_pipeline_probe(actors: int, steps: int = 2, warmup: int = 1, device=None, transport: str = "bucketed",

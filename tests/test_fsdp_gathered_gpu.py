@@ -120,3 +120,33 @@ def test_c5_shapes_layers_kept_gathered(tmp_path):
         grow = x[g]["peak_bytes"] - x["0"]["peak_bytes"]
         assert per <= grow <= x[g]["gathered_bytes"], (i, grow / 1e9, per / 1e9)
         assert x[g]["peak_bytes"] <= x[g]["estimate_bytes"], (i, summary)
+
+
+def _probe_rank(rank: int, port: int, tmp: str):
+    sys.path[:0] = [str(ROOT), str(ROOT / "pipelinerl-swe_amd"), str(ROOT / "tests")]
+    os.environ["OMP_NUM_THREADS"] = "4"
+    import torch.distributed as dist
+
+    from pipelinerl_amd.trainer_probe import fsdp_step_probe
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("cpu:gloo,cuda:gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=2)
+    r = fsdp_step_probe("32b", tokens=2048, micro_batches=1, steps=1, warmup=0, device=torch.device("cuda:0"),
+                        layers=2, keep_gathered="plan")
+    if rank == 0:
+        (Path(tmp) / "probe.json").write_text(json.dumps(r))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_fsdp_probe_applies_the_plan(tmp_path):
+    """bench.py's fsdp_32b_kept_gathered probe path: fsdp_step_probe(keep_gathered="plan") sizes R
+    with the loop's plan on the sharded model and keeps that many layers gathered (2 of 2 here)."""
+    from test_weight_update_cpu import free_port
+
+    mp.spawn(_probe_rank, args=(free_port(), str(tmp_path)), nprocs=2, join=True)
+    r = json.loads((tmp_path / "probe.json").read_text())
+    print(json.dumps(r))
+    assert r["kept_gathered_layers"] == 2 and r["plan"]["gathered_layers"] == 2, r
+    assert r["ms_per_optimizer_step"] > 0 and r["tokens_per_s"] > 0
