@@ -371,11 +371,12 @@ def _snapshot_only_group():
     return SnapshotOnlyGroup()
 
 
-def _paced_read_group(gbps: float, blocks: int, device):
+def _paced_read_group(gbps: float, blocks: int, device, asleep: bool = False):
     """An actor group with no receivers whose broadcast READS what it would send, as an RCCL root
     does, at a link rate: ``blocks`` workgroups (the channels) stream each bucket paced to ``gbps``
     (prl_paced_read, stream-ordered on the broadcast's side stream).  One xGMI link ~153 GB/s
-    (SURVEY.md §5)."""
+    (SURVEY.md §5).  ``asleep`` (a control): the same workgroups resident for the same time per
+    bucket, reading two 64 KiB turns each — the CUs held without the memory traffic."""
     import ctypes
 
     from . import _native
@@ -390,9 +391,12 @@ def _paced_read_group(gbps: float, blocks: int, device):
 
         def broadcast(self, t: torch.Tensor, src: int = 0, bucket_bytes: int = 0) -> None:
             st = torch.cuda.current_stream(t.device).cuda_stream
-            _native.check(lib.prl_paced_read(ctypes.c_void_p(t.data_ptr()), t.numel() * t.element_size(),
-                                             float(gbps), int(blocks), ctypes.c_void_p(sink.data_ptr()), st),
-                          "prl_paced_read")
+            nbytes, rate = t.numel() * t.element_size(), float(gbps)
+            if asleep:
+                small = min(nbytes, 2 * int(blocks) * 65536)
+                nbytes, rate = small, rate * small / max(1, nbytes)
+            _native.check(lib.prl_paced_read(ctypes.c_void_p(t.data_ptr()), nbytes, rate, int(blocks),
+                                             ctypes.c_void_p(sink.data_ptr()), st), "prl_paced_read")
 
     return PacedReadGroup()
 
@@ -453,15 +457,18 @@ def snapshot_overlap(ts: "TrainerStep", t_ref: float, steps: int, warmup: int, f
     paced_ms = {}
     if in_place:
         flat_p = managers["zero_copy"]._flat_params
-        for name, (gbps, blocks) in PACED_ARMS.items():
-            grp = _paced_read_group(gbps, blocks, ts.device)
+        for name, (gbps, blocks, *mode) in PACED_ARMS.items():
+            # mode flags (measurement controls): "asleep" (the workgroups held, almost no reads),
+            # "one" (one launch for the whole buffer instead of one per 256 MiB bucket)
+            grp = _paced_read_group(gbps, blocks, ts.device, asleep="asleep" in mode)
+            bucket = (1 << 40) if "one" in mode else (256 << 20)
             managers[name] = WeightUpdateManager([], ts.model, None, grp, transport="bucketed", overlap=True,
                                                  is_main=rank == 0, write_message=lambda s, m: None,
-                                                 snapshot="zero_copy")
+                                                 snapshot="zero_copy", bucket_bytes=bucket)
             with torch.cuda.stream(side):  # the reads alone, nothing else running
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(side)
-                for a, b in layout.buckets(128 << 20):  # 256 MiB buckets of bf16
+                for a, b in layout.buckets(bucket // 2):  # buckets of bf16
                     grp.broadcast(flat_p[a:b])
                 e1.record(side)
             _sync(ts.device)
@@ -496,7 +503,7 @@ def snapshot_overlap(ts: "TrainerStep", t_ref: float, steps: int, warmup: int, f
     if in_place:
         zc["hidden_frac_note"] = "unmeasured at N=1: no receiver, the broadcast reads nothing (see zero_copy_1link/4link)"
     paced = {}
-    for name, (gbps, blocks) in PACED_ARMS.items():
+    for name, (gbps, blocks, *mode) in PACED_ARMS.items():
         if name in paced_ms:
             paced[name] = dict(arm(name, round(paced_ms[name], 3)), link_GBps=gbps, channel_workgroups=blocks,
                                reads="the 15.23 GB flat parameter buffer in 256 MiB buckets, prl_paced_read")

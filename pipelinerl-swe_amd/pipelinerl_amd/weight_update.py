@@ -32,6 +32,7 @@ from __future__ import annotations
 
 import ctypes
 import functools
+import os
 import logging
 import threading
 import time
@@ -356,7 +357,8 @@ class WeightUpdateManager:
         def finish():
             try:
                 deadline = None if not self.timeout_s else t0 + float(self.timeout_s)
-                delay = 0.001
+                fixed = os.environ.get("PRL_WU_POLL_S")  # measurement control: a fixed poll interval
+                delay = float(fixed) if fixed else 0.001
                 while True:  # an actor's HTTP error ends the wait at once, not the collective
                     for url, f in zip(self.llm_urls, futures):
                         if f.done() and f.exception() is not None:
@@ -370,7 +372,7 @@ class WeightUpdateManager:
                             f"weight update {version} not completed after {self.timeout_s:.0f} s "
                             f"(broadcast {'done' if comm_done else 'in flight'}; actors not answered: {waiting})")
                     time.sleep(delay)
-                    delay = min(delay * 2, 0.02)
+                    delay = delay if fixed else min(delay * 2, 0.02)
                 if done is None:
                     for w in works:  # gloo: surfaces a failed work's error
                         w.wait()

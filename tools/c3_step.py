@@ -28,7 +28,7 @@ def main():
     ap.add_argument("--layers", type=int, default=None)
     ap.add_argument("--snapshot", action="store_true")
     ap.add_argument("--paced-arms", default=None,
-                    help="with --snapshot: the emulated broadcast-read arms as GBps:workgroups,... "
+                    help="with --snapshot: the emulated broadcast-read arms as GBps:workgroups[:asleep][:one],... "
                          "(default trainer_probe.PACED_ARMS)")
     ap.add_argument("--grad-ckpt", action="store_true", help="gradient checkpointing (the reference config's)")
     ap.add_argument("--keep-layers", type=int, default=0, help="with --grad-ckpt: the last K layers keep activations")
@@ -55,8 +55,11 @@ def main():
     from pipelinerl_amd.trainer_probe import TrainerStep
 
     if a.paced_arms:
-        trainer_probe.PACED_ARMS = {f"paced_{g}GBps_{b}wg": (float(g), int(b))
-                                    for g, b in (x.split(":") for x in a.paced_arms.split(","))}
+        # GBps:workgroups[:asleep][:one] (asleep: the workgroups held as long, two 64 KiB reads each per
+        # bucket; one: a single launch for the whole buffer instead of one per 256 MiB bucket)
+        trainer_probe.PACED_ARMS = {f"paced_{x[0]}GBps_{x[1]}wg" + "".join("_" + f for f in x[2:]):
+                                    (float(x[0]), int(x[1]), *x[2:])
+                                    for x in (y.split(":") for y in a.paced_arms.split(","))}
 
     timed = TrainerStep.timed
 

@@ -1,13 +1,14 @@
 """How much a side-stream kernel holding a few CUs slows the trainer step's own kernels (the
 zero-copy weight broadcast's cost: its channels are workgroups that stay resident for the whole
 transfer).  Each kernel under test is timed alone, then beside prl_paced_read on a side stream in
-two forms: reading at one xGMI link's rate (153 GB/s, the emulated broadcast) and nearly asleep
-(0.01 GB/s: the same resident workgroups, almost no memory traffic), so CU occupancy and memory
-contention separate.
+three forms: reading at one xGMI link's rate (153 GB/s, the emulated broadcast), nearly asleep
+(0.01 GB/s: the same resident workgroups, almost no memory traffic) and ONE asleep workgroup, so CU
+occupancy and memory contention separate.
 
     python tools/side_contention.py [--blocks 16] [--reps 30]
 
-Kernels: the HIP attention forward at C3-like packing (7B heads 28 / 4, D 128; 12 000 tokens in
+Kernels: the 7B gate/up GEMMs through libprl_gemm (forward, input and weight gradient) and
+torch.matmul, the HIP attention forward at C3-like packing (7B heads 28 / 4, D 128; 12 000 tokens in
 three sequences), the fused residual-add RMSNorm (12 000 x 3584) and, as a control, torch's copy of
 the same bytes.  Prints one JSON line."""
 
@@ -26,6 +27,7 @@ sys.path.insert(0, str(ROOT / "pipelinerl-swe_amd"))
 
 from pipelinerl_amd import _native  # noqa: E402
 from pipelinerl_amd.finetune.attention import PackedCausalAttention  # noqa: E402
+from pipelinerl_amd import gemm as prl_gemm  # noqa: E402
 from pipelinerl_amd.finetune.model_ops import AddRMSNormFn  # noqa: E402
 
 
@@ -62,7 +64,14 @@ def main():
     w = torch.ones(3584, device=dev, dtype=torch.bfloat16)
     big = torch.empty(2 * T * 3584, dtype=torch.bfloat16, device=dev)
     dst = torch.empty_like(big)
+    # the 7B MLP's gate/up and down GEMMs at 12 000 tokens: forward, input and weight gradient
+    wgu = torch.randn((2 * 18944, 3584), generator=g, device=dev).to(torch.bfloat16) * 0.02
+    dy = torch.randn((T, 2 * 18944), generator=g, device=dev).to(torch.bfloat16)
     kernels = {
+        "gemm_fwd_gate_up": lambda: prl_gemm.linear_fwd(x, wgu),
+        "gemm_dgrad_gate_up": lambda: prl_gemm.linear_dgrad(dy, wgu),
+        "gemm_wgrad_gate_up": lambda: prl_gemm.linear_wgrad(dy, x),
+        "torch_matmul_gate_up": lambda: torch.matmul(x, wgu.t()),
         "attn_fwd": lambda: PackedCausalAttention.apply(q, k, v, cu, max(lens), bounds),
         "add_rmsnorm_fwd": lambda: AddRMSNormFn.apply(r, x, w, 1e-6),
         "torch_copy_same_bytes": lambda: dst.copy_(big),
@@ -78,16 +87,17 @@ def main():
             alone = med_ms(fn, a.reps)
             row = {"alone": round(alone, 4)}
             span_s = 3 * a.reps * alone / 1e3 + 0.05  # the side kernel outlasts the timed loop
-            for arm, gbps in (("reading_153GBps", 153.0), ("asleep", 0.01)):
-                nbytes = min(src.numel(), max(a.blocks * 65536, int(gbps * 1e9 * span_s)))
+            for arm, gbps, blocks in (("reading_153GBps", 153.0, a.blocks), ("asleep", 0.01, a.blocks),
+                                      ("asleep_1wg", 0.01, 1)):
+                nbytes = min(src.numel(), max(blocks * 65536, int(gbps * 1e9 * span_s)))
                 if gbps < 1:  # two turns per workgroup, the second one due after span_s
-                    nbytes = 2 * a.blocks * 65536
+                    nbytes = 2 * blocks * 65536
                     gbps_eff = nbytes / span_s / 1e9
                 else:
                     gbps_eff = gbps
                 torch.cuda.synchronize()
                 with torch.cuda.stream(side):
-                    _native.check(lib.prl_paced_read(ctypes.c_void_p(src.data_ptr()), nbytes, gbps_eff, a.blocks,
+                    _native.check(lib.prl_paced_read(ctypes.c_void_p(src.data_ptr()), nbytes, gbps_eff, blocks,
                                                      ctypes.c_void_p(sink.data_ptr()), side.cuda_stream),
                                   "prl_paced_read")
                 torch.cuda._sleep(2_000_000)  # ~1 ms: the side kernel's workgroups are resident first
@@ -95,6 +105,7 @@ def main():
                 torch.cuda.synchronize()
             row["ratio_reading"] = round(row["reading_153GBps"] / alone, 3)
             row["ratio_asleep"] = round(row["asleep"] / alone, 3)
+            row["ratio_asleep_1wg"] = round(row["asleep_1wg"] / alone, 3)
             out["ms"][name] = row
     print(json.dumps(out))
 
