@@ -56,7 +56,11 @@ def _rank_main(rank, world, port, exp, steps, passes, extra):
         dist.destroy_process_group()
 
 
-def _setup(tmp: Path, world: int, n_groups=4, attempts=4, seq_length=28):
+def _setup(tmp: Path, world: int, n_groups=4, attempts=4, seq_length=28, tail_groups=0):
+    """``tail_groups``: groups written after the two steps' data (never trained on) so the packer
+    finishes the second step's last round of writes — with finite data the protocol's round ends
+    only when more samples arrive (preprocess.py:557-626), which at 4 and 8 ranks starves the
+    ranks after the last write."""
     sys.path[:0] = [str(ROOT / "tests")]
     from loop_helpers import rollouts, tiny_model_dir, write_training_data
     from pipelinerl_amd.streams import reset_streams_backend, set_streams_backend
@@ -64,32 +68,37 @@ def _setup(tmp: Path, world: int, n_groups=4, attempts=4, seq_length=28):
     reset_streams_backend()
     set_streams_backend("files")
     tiny_model_dir(tmp)
-    data = rollouts(n_groups, attempts)
-    total = len(data)
+    data = rollouts(n_groups + tail_groups, attempts)  # the first n_groups groups as rollouts(n_groups)
+    total = n_groups * attempts
     per_step = total // 2  # two optimizer steps
     writes = write_training_data(tmp, data, world, seq_length, per_step // world)
     reset_streams_backend()
     return per_step, writes
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_dp_loop_matches_single_rank(tmp_path, world):
-    # world-2 run
-    exp2 = tmp_path / "w2"
+    """The DP loop at world 2, 4 and 8 (the driver's N = 8 scaling run has 8 ranks in lockstep:
+    sample quotas, sentinels, per-pass exchange) ends with the parameters of one rank trained on
+    all the data."""
+    exp2 = tmp_path / f"w{world}"
     exp2.mkdir()
-    per_step, writes = _setup(exp2, world)
-    assert any(b.sentinel for _, b in writes), "the packing should have produced sentinel batches"
+    ng = max(4, 2 * world)  # 4 samples per rank and optimizer step
+    per_step, writes = _setup(exp2, world, n_groups=ng, tail_groups=ng)
+    if world == 2:
+        assert any(b.sentinel for _, b in writes), "the packing should have produced sentinel batches"
     mp.spawn(_rank_main, args=(world, free_port(), str(exp2), 2, per_step, {}), nprocs=world, join=True)
-    p0 = torch.load(exp2 / "params_w2_r0.pt")
-    p1 = torch.load(exp2 / "params_w2_r1.pt")
-    for n in p0:
-        assert torch.equal(p0[n], p1[n]), n  # replicas stay identical
-    m0 = json.loads((exp2 / "metrics_w2_r0.json").read_text())
+    p0 = torch.load(exp2 / f"params_w{world}_r0.pt")
+    for r in range(1, world):
+        pr = torch.load(exp2 / f"params_w{world}_r{r}.pt")
+        for n in p0:
+            assert torch.equal(p0[n], pr[n]), (r, n)  # replicas stay identical
+    m0 = json.loads((exp2 / f"metrics_w{world}_r0.json").read_text())
     assert m0["steps"] == 2 and m0["samples"] == 2 * per_step
     # world-1 run on the same rollouts
     exp1 = tmp_path / "w1"
     exp1.mkdir()
-    _setup(exp1, 1)
+    _setup(exp1, 1, n_groups=ng, tail_groups=ng)
     mp.spawn(_rank_main, args=(1, free_port(), str(exp1), 2, per_step, {}), nprocs=1, join=True)
     q = torch.load(exp1 / "params_w1_r0.pt")
     worst = max(float((p0[n] - q[n]).abs().max()) for n in q)
