@@ -127,7 +127,9 @@ def _run(rank, port, world, transport, exp, use_reference_pg, qwen=False):
         _actor(port, world, rank - 1, transport, exp, 2, use_reference_pg, qwen)
 
 
-@pytest.mark.parametrize("transport,world", [("per_tensor", 2), ("bucketed", 2), ("bucketed", 3)])
+# world 5: C4's actor group (1 trainer + 4 actor GPUs, weight_update_group_size 5, world.py:184)
+@pytest.mark.parametrize("transport,world", [("per_tensor", 2), ("bucketed", 2), ("bucketed", 3), ("per_tensor", 5),
+                                             ("bucketed", 5)])
 def test_broadcast_roundtrip(tmp_path, transport, world):
     port = free_port()
     mp.spawn(_run, args=(port, world, transport, str(tmp_path), False), nprocs=world, join=True)
