@@ -57,7 +57,7 @@ def _run(rank, port, world, actors, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,actors", [(2, 1), (4, 2)])
+@pytest.mark.parametrize("world,actors", [(2, 1), (4, 2), (8, 4)])  # (8, 4): C4 on one node
 def test_split_pipeline_gloo(tmp_path, world, actors):
     from test_weight_update_cpu import free_port
 
