@@ -76,9 +76,9 @@ def _setup(tmp: Path, world: int, n_groups=4, attempts=4, seq_length=28, tail_gr
     return per_step, writes
 
 
-@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("world", [2, 8])
 def test_dp_loop_matches_single_rank(tmp_path, world):
-    """The DP loop at world 2, 4 and 8 (the driver's N = 8 scaling run has 8 ranks in lockstep:
+    """The DP loop at world 2 and 8 (the driver's N = 8 scaling run has 8 ranks in lockstep:
     sample quotas, sentinels, per-pass exchange) ends with the parameters of one rank trained on
     all the data."""
     exp2 = tmp_path / f"w{world}"

@@ -24,13 +24,26 @@ pytestmark = pytest.mark.skipif(not Path("/opt/rocm/bin/hipcc").exists() and not
                                 reason="hipcc not installed")
 
 
+_ISA: dict = {}
+
+
+def _isa(src: str, defines: dict) -> str:
+    """compile_isa, once per (source, defines) in this session (each compile of grpo_loss.hip takes ~25 s)."""
+    from isa_store_hazard_scan import compile_isa
+
+    key = (src, tuple(sorted(defines.items())))
+    if key not in _ISA:
+        _ISA[key] = compile_isa(CSRC / src, defines, include=[ROOT / "include", CSRC])
+    return _ISA[key]
+
+
 @pytest.mark.parametrize("src,defines", [("grpo_loss.hip", {}), ("grpo_loss.hip", {"PRL_PHASED_MAX_NV": "24"}),
                                          ("model_ops.hip", {}), ("flat_pack.hip", {}), ("adamw.hip", {}),
                                          ("attn_bwd.hip", {})])
 def test_no_store_data_hazard(src, defines):
     from isa_store_hazard_scan import compile_isa, scan
 
-    isa = compile_isa(CSRC / src, defines, include=[ROOT / "include", CSRC])
+    isa = _isa(src, defines)
     assert "grpo_fwd_resident" in isa or src != "grpo_loss.hip"
     assert "attn_bwd" in isa or src != "attn_bwd.hip"
     hits = scan(isa)
@@ -65,7 +78,7 @@ def test_resident_loss_head_reads_row_inputs_through_the_scalar_cache():
     this function and 2 vmcnt waits between the barrier and the first store: it fails here.)"""
     from isa_store_hazard_scan import compile_isa
 
-    isa = compile_isa(CSRC / "grpo_loss.hip", {}, include=[ROOT / "include", CSRC])
+    isa = _isa("grpo_loss.hip", {})
     fn = _function(isa, "_ZN3prl17grpo_fwd_residentILi19EEEvNS_5KArgsE")
     lines = [ln.strip() for ln in fn.splitlines()]
     vloads = [ln for ln in lines if ln.startswith(("global_load", "flat_load", "buffer_load"))]
