@@ -148,6 +148,9 @@ struct KArgs {
   // row selection (prl_grpo_forward_rows): logits row i scores batch row row_ids[i]
   const int64_t* row_ids;
   int64_t nsel;
+  // grpo_fwd_resident: rows after each workgroup's first are claimed from this counter (zeroed
+  // before the launch); null: the static stride q += gridDim.x
+  uint32_t* row_ctr;
 };
 
 // Per-token quantities of rl/__init__.py:212-292 for one loss row.

@@ -246,6 +246,7 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
   constexpr bool kCopyCeiling = false;
 #endif
   __shared__ float red[2][NW][3];
+  __shared__ int64_t next_q[2];  // the workgroup's next row, by row parity (published at the row's barrier)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int64_t nrows = fwd_rows(a);
   const int nvec = (int)(a.V >> 3);
@@ -268,7 +269,16 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
       buf[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, k * VSTRIDE, kLoadAux));
   }
   int par = 0;
-  for (; q < nrows; q += gridDim.x, par ^= 1) {
+  int64_t qn = q + gridDim.x;
+  for (; q < nrows; q = qn, par ^= 1) {
+    // Dynamic rows (a.row_ctr): the workgroup claims its next row now, while this row's loads are
+    // in flight (one vector atomic by one thread; its latency hides behind the row's loads), and
+    // publishes it at the row's barrier.  A workgroup that starts late — its CU held by another
+    // queue's kernel (an RCCL channel, a side-stream kernel) — then takes fewer rows instead of
+    // finishing a full static share after everyone else.  Rows are independent, so the results do
+    // not depend on which workgroup computes which row.
+    uint32_t claim = 0;
+    if (a.row_ctr && tid == 0) claim = atomicAdd(a.row_ctr, 1u);
     // The row's token inputs and its target logit come through the scalar cache while the row's
     // vector loads are in flight: nothing here waits for them, and the epilogue after the
     // barrier finds its inputs in SGPRs (with vector loads this was a chain of four waits per
@@ -308,7 +318,13 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
       red[par][wid][1] = st.s;
       red[par][wid][2] = st.w;
     }
+    if (tid == 0) next_q[par] = a.row_ctr ? (int64_t)gridDim.x + (int64_t)claim : q + gridDim.x;
     __syncthreads();
+    {  // wave-uniform in SGPRs: the next row's scalar loads and buffer descriptors are built from it
+      const int64_t v = next_q[par];
+      qn = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
+                     (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)v));
+    }
     const Lse tot = block_combine<NW>(red[par], c);
     const float l2s = log2f(tot.s);
     const float M = tot.m;
@@ -322,7 +338,6 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
     for (int k = 0; k < NV; ++k) asm volatile("" : "+v"(buf[k]));
 
     // ---- pass 2: gradient from registers; the next row streams into the freed registers
-    const int64_t qn = q + gridDim.x;
     const bool has_next = qn < nrows;
     int64_t nlrow = lrow;
     if (has_next) {
@@ -1273,8 +1288,10 @@ static hipError_t launch_resident_nv(int nv, const KArgs& a, int grid, hipStream
 // never share hand-off slots; [pairs][2][2] granules of 16 B for up to 1024 CUs
 constexpr int kPairMaxCUs = 1024;
 constexpr size_t kPairSlotBytes = (size_t)(kPairMaxCUs / 2) * 2 * 2 * 16;
-// after the slots: the fallback counter (not cleared per launch; prl_grpo_pair_fallbacks reads and resets it)
+// after the slots: the fallback counter (not cleared per launch; prl_grpo_pair_fallbacks reads and resets it),
+// then the resident kernel's row counter (zeroed before every launch)
 constexpr size_t kPairCounterBytes = 16;
+constexpr size_t kRowCounterBytes = 16;
 static std::mutex g_slot_mu;
 static std::map<std::pair<int, hipStream_t>, void*> g_pair_slots;
 
@@ -1284,9 +1301,9 @@ static hipError_t pair_slots(int dev, hipStream_t s, void** out) {
   auto it = g_pair_slots.find(key);
   if (it == g_pair_slots.end()) {
     void* p = nullptr;
-    hipError_t e = hipMalloc(&p, kPairSlotBytes + kPairCounterBytes);
+    hipError_t e = hipMalloc(&p, kPairSlotBytes + kPairCounterBytes + kRowCounterBytes);
     if (e != hipSuccess) return e;
-    e = hipMemset(static_cast<char*>(p) + kPairSlotBytes, 0, kPairCounterBytes);
+    e = hipMemset(static_cast<char*>(p) + kPairSlotBytes, 0, kPairCounterBytes + kRowCounterBytes);
     if (e != hipSuccess) return e;
     it = g_pair_slots.emplace(key, p).first;
   }
@@ -1345,6 +1362,25 @@ static hipError_t launch_pair_rows(const KArgs& a, int nv, int64_t nrows, int cu
   return launch_pair_table(nv, a, pa, grid, s, std::make_integer_sequence<int, kPairMaxNV - kPairMinNV + 1>{});
 }
 
+// PRL_ROW_CLAIM=0: the resident kernel's static row stride (A/B); read per launch
+static bool row_claim_enabled() {
+  const char* e = getenv("PRL_ROW_CLAIM");
+  return !(e && e[0] == '0');
+}
+
+static hipError_t launch_resident_rows(KArgs a, int nv, int grid, int dev, hipStream_t s) {
+  a.row_ctr = nullptr;
+  if (row_claim_enabled()) {
+    void* scratch = nullptr;
+    hipError_t e = pair_slots(dev, s, &scratch);
+    if (e != hipSuccess) return e;
+    a.row_ctr = reinterpret_cast<uint32_t*>(static_cast<char*>(scratch) + kPairSlotBytes + kPairCounterBytes);
+    e = hipMemsetAsync(a.row_ctr, 0, sizeof(uint32_t), s);
+    if (e != hipSuccess) return e;
+  }
+  return launch_resident_nv(nv, a, grid, s);
+}
+
 // per-row outputs (+ dlogits); the row arrays are indexed by batch row q
 static int fill_outputs(KArgs& a, const PrlGrpoBatch* b, const PrlGrpoParams* p, const PrlGrpoOutputs* out,
                         bool need_stats) {
@@ -1378,7 +1414,7 @@ static hipError_t launch_rows(const KArgs& a, const PrlGrpoBatch* b, const PrlGr
   const bool vec_ok_bf = bf16 && b->V % 8 == 0 && b->ld % 8 == 0 && aligned16(b->logits) &&
                          (!p->write_grad || aligned16(out->dlogits));
   const int nv = vec_ok_bf ? resident_nv(b->V / 8) : 0;  // row <= 24*16 KiB
-  if (nv > 0) return launch_resident_nv(nv, a, (int)(nrows < cus ? nrows : cus), s);
+  if (nv > 0) return launch_resident_rows(a, nv, (int)(nrows < cus ? nrows : cus), dev, s);
   const int64_t want = (int64_t)cus * 4;
   int grid = (int)(nrows < want ? nrows : want);
   if (grid > kMaxGrid) grid = kMaxGrid;

@@ -17,6 +17,7 @@ from __future__ import annotations
 import argparse
 import ctypes
 import json
+import os
 import sys
 from pathlib import Path
 
@@ -67,7 +68,22 @@ def main():
     # the 7B MLP's gate/up and down GEMMs at 12 000 tokens: forward, input and weight gradient
     wgu = torch.randn((2 * 18944, 3584), generator=g, device=dev).to(torch.bfloat16) * 0.02
     dy = torch.randn((T, 2 * 18944), generator=g, device=dev).to(torch.bfloat16)
+    # the fused loss head on a C2-shaped micro-batch slice (8192 x 151936 bf16 logits; persistent
+    # grid of one 1024-thread workgroup per CU)
+    from pipelinerl_amd.finetune.rl.fused import GrpoParams, grpo_loss
+    sys.path.insert(0, str(ROOT))
+    from bench import make_workload
+
+    lg, fields = make_workload(8192, 151936, seq=2048, prompt=256, seed=0, device=dev)
+    params = GrpoParams(policy_loss="ppo", epsilon=4.0, kl_coef=0.0, entropy_coef=0.0, clamp_log_ratio=5.0,
+                        temperature=1.0, batch_size=4096.0)
+    lg.requires_grad_(True)
     kernels = {
+        "loss_head_fwd_8192_rows": lambda: grpo_loss(lg, fields, params),
+        # the same with the static row stride (PRL_ROW_CLAIM=0, read per launch)
+        "loss_head_fwd_8192_rows_static": lambda: (os.environ.__setitem__("PRL_ROW_CLAIM", "0"),
+                                                   grpo_loss(lg, fields, params),
+                                                   os.environ.pop("PRL_ROW_CLAIM")),
         "gemm_fwd_gate_up": lambda: prl_gemm.linear_fwd(x, wgu),
         "gemm_dgrad_gate_up": lambda: prl_gemm.linear_dgrad(dy, wgu),
         "gemm_wgrad_gate_up": lambda: prl_gemm.linear_wgrad(dy, x),
