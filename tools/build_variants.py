@@ -15,6 +15,7 @@ VARIANTS = {  # the loss head's A/B builds (csrc/grpo_loss.hip macros); profiles
     "copy_ceiling": {"PRL_COPY_CEILING": "1"},  # same schedule, no math: the kernel's own ceiling
     "row_sequential": {"PRL_ROW_PERMUTE": "0"},
     "unphased": {"PRL_PHASED": "0"},
+    "phased_nowait": {"PRL_PHASED": "2"},  # phased order, no wait for the stores before the next row's loads
     "phased24": {"PRL_PHASED_MAX_NV": "24"},
     "nofence": {"PRL_STORE_FENCE": "0"},  # the round-2 store hazard (wrong results: probes only)
     "f32_u2": {"PRL_STREAM_F32_U": "2"},
