@@ -14,6 +14,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+#include <map>
+#include <mutex>
 #include <utility>
 
 #include "prl_hip.h"
@@ -567,11 +570,28 @@ __global__ __launch_bounds__(256) void swiglu_bwd(const u32x4* __restrict__ dh, 
 #define PRL_SWIGLU_ROWS_PHASED 0
 #endif
 constexpr int kPhFwdU = 8, kPhBwdU = 6;
+// Chunks after each workgroup's first are claimed from `ctr` (zeroed before the launch; null: the
+// static stride), as the loss head claims rows (csrc/grpo_loss.hip): a workgroup whose CU is held by
+// another queue's kernel (an RCCL channel during the overlapped gradient all-reduce) takes fewer
+// chunks instead of a full static share after the others.  One vector atomic per chunk by thread 0,
+// issued behind the chunk's loads; the index is published in LDS at the chunk's end (the store wait
+// covers the atomic) — results are unchanged.
+__device__ __forceinline__ int64_t next_chunk(uint32_t* ctr, uint32_t claim, int64_t cur, int64_t* slot) {
+  if (threadIdx.x == 0) *slot = ctr ? (int64_t)gridDim.x + (int64_t)claim : cur + gridDim.x;
+  __syncthreads();
+  const int64_t v = *slot;
+  __syncthreads();  // every wave has read the slot before thread 0 writes the next chunk's
+  return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
+                   (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)v));
+}
 __global__ __launch_bounds__(1024) void swiglu_fwd_phased(const u32x4* __restrict__ g, const u32x4* __restrict__ u,
-                                                         u32x4* __restrict__ h, int64_t n8) {
+                                                         u32x4* __restrict__ h, int64_t n8, uint32_t* ctr) {
   constexpr int U = kPhFwdU;
   const int64_t chunk = 1024 * U;
-  for (int64_t base = (int64_t)blockIdx.x * chunk; base < n8; base += (int64_t)gridDim.x * chunk) {
+  const int64_t nchunks = (n8 + chunk - 1) / chunk;
+  __shared__ int64_t slot;
+  for (int64_t c = blockIdx.x; c < nchunks;) {
+    const int64_t base = c * chunk;
     u32x4 gv[U], uv[U];
 #pragma unroll
     for (int k = 0; k < U; ++k) {
@@ -579,20 +599,26 @@ __global__ __launch_bounds__(1024) void swiglu_fwd_phased(const u32x4* __restric
       gv[k] = i < n8 ? __builtin_nontemporal_load(g + i) : u32x4{0, 0, 0, 0};
       uv[k] = i < n8 ? __builtin_nontemporal_load(u + i) : u32x4{0, 0, 0, 0};
     }
+    uint32_t claim = 0;
+    if (ctr && threadIdx.x == 0) claim = atomicAdd(ctr, 1u);
 #pragma unroll
     for (int k = 0; k < U; ++k) {
       const int64_t i = base + k * 1024 + threadIdx.x;
       if (i < n8) __builtin_nontemporal_store(swiglu_vec(gv[k], uv[k]), h + i);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    c = next_chunk(ctr, claim, c, &slot);
   }
 }
 __global__ __launch_bounds__(1024) void swiglu_bwd_phased(const u32x4* __restrict__ dh, const u32x4* __restrict__ g,
                                                          const u32x4* __restrict__ u, u32x4* __restrict__ dg,
-                                                         u32x4* __restrict__ du, int64_t n8) {
+                                                         u32x4* __restrict__ du, int64_t n8, uint32_t* ctr) {
   constexpr int U = kPhBwdU;
   const int64_t chunk = 1024 * U;
-  for (int64_t base = (int64_t)blockIdx.x * chunk; base < n8; base += (int64_t)gridDim.x * chunk) {
+  const int64_t nchunks = (n8 + chunk - 1) / chunk;
+  __shared__ int64_t slot;
+  for (int64_t c = blockIdx.x; c < nchunks;) {
+    const int64_t base = c * chunk;
     u32x4 dv[U], gv[U], uv[U];
 #pragma unroll
     for (int k = 0; k < U; ++k) {
@@ -601,6 +627,8 @@ __global__ __launch_bounds__(1024) void swiglu_bwd_phased(const u32x4* __restric
       gv[k] = i < n8 ? __builtin_nontemporal_load(g + i) : u32x4{0, 0, 0, 0};
       uv[k] = i < n8 ? __builtin_nontemporal_load(u + i) : u32x4{0, 0, 0, 0};
     }
+    uint32_t claim = 0;
+    if (ctr && threadIdx.x == 0) claim = atomicAdd(ctr, 1u);
 #pragma unroll
     for (int k = 0; k < U; ++k) {
       const int64_t i = base + k * 1024 + threadIdx.x;
@@ -612,6 +640,7 @@ __global__ __launch_bounds__(1024) void swiglu_bwd_phased(const u32x4* __restric
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    c = next_chunk(ctr, claim, c, &slot);
   }
 }
 
@@ -858,6 +887,32 @@ bool a8(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7u) == 0; }
 #ifndef PRL_SWIGLU_PHASED_WG
 #define PRL_SWIGLU_PHASED_WG 1
 #endif
+// the phased SwiGLU kernels' chunk counter: one per (device, stream), zeroed before each launch
+// (PRL_CHUNK_CLAIM=0: the static stride, A/B; read per launch)
+static std::mutex g_ctr_mu;
+static std::map<std::pair<int, hipStream_t>, uint32_t*> g_ctrs;
+static hipError_t chunk_counter(hipStream_t s, uint32_t** out) {
+  *out = nullptr;
+  const char* env = getenv("PRL_CHUNK_CLAIM");
+  if (env && env[0] == '0') return hipSuccess;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  {
+    std::lock_guard<std::mutex> lk(g_ctr_mu);
+    auto key = std::make_pair(dev, s);
+    auto it = g_ctrs.find(key);
+    if (it == g_ctrs.end()) {
+      void* p = nullptr;
+      e = hipMalloc(&p, 16);
+      if (e != hipSuccess) return e;
+      it = g_ctrs.emplace(key, static_cast<uint32_t*>(p)).first;
+    }
+    *out = it->second;
+  }
+  return hipMemsetAsync(*out, 0, sizeof(uint32_t), s);
+}
+
 static int phased_grid() {
   static int cus = 0;
   if (!cus) {
@@ -969,8 +1024,11 @@ int prl_swiglu_forward(const void* gate, const void* up, void* out, int64_t n, v
   if (PRL_SWIGLU_PHASED) {
     const int64_t chunks = (n8 + 1024 * kPhFwdU - 1) / (1024 * kPhFwdU);
     const int grid = (int)(chunks < phased_grid() ? chunks : phased_grid());
+    uint32_t* ctr = nullptr;
+    const hipError_t e = chunk_counter(static_cast<hipStream_t>(stream), &ctr);
+    if (e != hipSuccess) return (int)e;
     hipLaunchKernelGGL(swiglu_fwd_phased, dim3(grid), dim3(1024), 0, static_cast<hipStream_t>(stream),
-                       (const u32x4*)gate, (const u32x4*)up, (u32x4*)out, n8);
+                       (const u32x4*)gate, (const u32x4*)up, (u32x4*)out, n8, ctr);
     return (int)hipGetLastError();
   }
   hipLaunchKernelGGL(swiglu_fwd, dim3(ew_grid(n8)), dim3(256), 0, static_cast<hipStream_t>(stream),
@@ -987,8 +1045,11 @@ int prl_swiglu_backward(const void* dout, const void* gate, const void* up, void
   if (PRL_SWIGLU_PHASED) {
     const int64_t chunks = (n8 + 1024 * kPhBwdU - 1) / (1024 * kPhBwdU);
     const int grid = (int)(chunks < phased_grid() ? chunks : phased_grid());
+    uint32_t* ctr = nullptr;
+    const hipError_t e = chunk_counter(static_cast<hipStream_t>(stream), &ctr);
+    if (e != hipSuccess) return (int)e;
     hipLaunchKernelGGL(swiglu_bwd_phased, dim3(grid), dim3(1024), 0, static_cast<hipStream_t>(stream),
-                       (const u32x4*)dout, (const u32x4*)gate, (const u32x4*)up, (u32x4*)dgate, (u32x4*)dup, n8);
+                       (const u32x4*)dout, (const u32x4*)gate, (const u32x4*)up, (u32x4*)dgate, (u32x4*)dup, n8, ctr);
     return (int)hipGetLastError();
   }
   hipLaunchKernelGGL(swiglu_bwd, dim3(ew_grid(n8)), dim3(256), 0, static_cast<hipStream_t>(stream),
