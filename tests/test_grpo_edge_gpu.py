@@ -168,15 +168,24 @@ def test_unpacked_bf16_value_head_ragged():
 def test_multi_row_per_workgroup():
     """Qwen2.5's vocab (the resident kernel's NV = 19, read / write phased schedule) with ~2.3 rows
     per workgroup of the persistent grid, so rows with and without a next row are both taken: every
-    row's dlogits and every statistic against the oracle, and two runs bitwise identical."""
+    row's dlogits and every statistic against the oracle, two runs bitwise identical, and the static
+    row stride (PRL_ROW_CLAIM=0) bitwise identical to the claimed rows."""
+    import os
+
     V = 151936
     lens = [150, 200, 251]
     T = sum(lens)
     b = _batch(T, V, seed=9, lens=lens, prompts=[20, 30, 40])
     lg = synth.to_bf16(np.random.default_rng(9).normal(0, 2.5, (1, T, V))).astype(np.float32)
-    _, d1 = _cmp(lg, b)
+    stats1, d1 = _cmp(lg, b)
     _, _, d2 = _run(lg, b)
     assert np.array_equal(d1, d2)
+    os.environ["PRL_ROW_CLAIM"] = "0"
+    try:
+        loss3, stats3, d3 = _run(lg, b)
+    finally:
+        del os.environ["PRL_ROW_CLAIM"]
+    assert np.array_equal(d1, d3) and stats3 == stats1
 
 
 @pytest.mark.parametrize("V", [151936, 152064])

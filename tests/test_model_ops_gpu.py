@@ -71,6 +71,35 @@ def test_swiglu(shape):
     assert ok, err
 
 
+def test_swiglu_phased_chunks_claimed_and_static():
+    """The phased kernels at a size with many chunks per workgroup (4096 x 8960: 4480 forward chunks
+    for a 256-workgroup grid): claimed chunks (default) and the static stride (PRL_CHUNK_CLAIM=0)
+    give bit-identical outputs, equal to the eager forward."""
+    import os
+
+    from pipelinerl_amd.finetune.model_ops import SwiGLUFn
+
+    g0 = torch.Generator(device=DEV).manual_seed(2)
+    gate = (torch.randn((4096, 8960), generator=g0, device=DEV) * 3).to(torch.bfloat16)
+    up = torch.randn((4096, 8960), generator=g0, device=DEV).to(torch.bfloat16)
+    dh = torch.randn((4096, 8960), generator=g0, device=DEV).to(torch.bfloat16)
+    outs = {}
+    for arm in ("claim", "static"):
+        if arm == "static":
+            os.environ["PRL_CHUNK_CLAIM"] = "0"
+        try:
+            gb, ub = gate.clone().requires_grad_(), up.clone().requires_grad_()
+            hb = SwiGLUFn.apply(gb, ub)
+            hb.backward(dh)
+            torch.cuda.synchronize()
+        finally:
+            os.environ.pop("PRL_CHUNK_CLAIM", None)
+        outs[arm] = (hb.detach(), gb.grad, ub.grad)
+    for a, b in zip(outs["claim"], outs["static"]):
+        assert torch.equal(a, b)
+    assert torch.equal(outs["claim"][0], torch.nn.functional.silu(gate) * up)
+
+
 @pytest.mark.parametrize("heads", [(12, 2), (14, 2), (28, 4), (40, 8)])  # 1.5B, 0.5B, 7B, 32B
 def test_rope_matches_hf(heads):
     from transformers.models.qwen2 import modeling_qwen2 as mq
