@@ -4,7 +4,8 @@
 // Reference: pipelinerl/finetune/rl/__init__.py:199-366 (ATen op chain over [1, T, V]) and
 // its autograd backward.  Kernels:
 //   grpo_fwd_resident<NV>  bf16 logits, V % 8 == 0 (Qwen2.5: V = 151936 / 152064).
-//       Persistent grid, one 1024-thread workgroup per CU, one vocab row per iteration.
+//       Persistent grid, one 1024-thread workgroup per CU, one vocab row per iteration; rows after
+//       a workgroup's first are claimed from a per-stream counter (KArgs.row_ctr).
 //       The whole row (V*2 B = 297 KiB) is held in VGPRs (NV x 16 B per lane), so the
 //       gradient pass re-reads nothing.  Read / write phases: the row's dlogits stores retire,
 //       then the whole next row (~300 KiB per CU) is loaded at once, so a CU never mixes HBM
