@@ -407,3 +407,40 @@ def test_pair_kernels_beside_a_kernel_holding_cus(dtype, env, monkeypatch):
     monkeypatch.setenv("PRL_PAIR_SPIN_TICKS", "0")
     _run(lg, b, dtype=dtype)
     assert fallbacks() > 0
+
+
+def test_claimed_rows_on_concurrent_streams():
+    """Two loss-head launches in flight at once on two streams (each workgroup claims rows from its
+    stream's own counter, grpo_loss.hip launch_resident_rows): both results equal the same launches
+    run one after the other."""
+    from pipelinerl_amd.finetune.rl.fused import GrpoParams, grpo_loss, prepare_fields
+
+    V = 151936
+    params = GrpoParams(policy_loss="ppo", epsilon=0.2, kl_coef=0.05, entropy_coef=0.0, clamp_log_ratio=5.0,
+                        temperature=1.0, batch_size=4.0)
+    runs = []
+    for seed in (21, 22):
+        lens = [900, 1100]
+        b = _batch(sum(lens), V, seed=seed, lens=lens, prompts=[30, 40])
+        lg = torch.tensor(synth.to_bf16(np.random.default_rng(seed).normal(0, 2.5, (1, sum(lens), V))),
+                          dtype=torch.float32).to(torch.bfloat16).to(DEV)
+        runs.append((lg, prepare_fields(to_batch(b), DEV)))
+
+    def launch(lg, fields):
+        x = lg.detach().clone().requires_grad_(True)
+        loss, stats, rows = grpo_loss(x, fields, params)
+        loss.backward()
+        return x.grad, stats, rows
+
+    seq = [launch(*r) for r in runs]
+    torch.cuda.synchronize()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    out = [None, None]
+    for i, (st, r) in enumerate(zip((s1, s2), runs)):
+        st.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(st):
+            out[i] = launch(*r)
+    torch.cuda.synchronize()
+    for a, b in zip(seq, out):
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
