@@ -237,8 +237,10 @@ int prl_adamw_step(int32_t n, void* const* params, const void* const* grads, voi
                    double lr, double beta1, double beta2, double weight_decay, double eps, const void* grad_scale,
                    void* stream);
 
-/* Sum of squares of n device tensors (f32 or bf16) accumulated into *out (device f64).
- * *out is overwritten. */
+/* Sum of squares of n device tensors (f32 or bf16) into *out (device f64; overwritten).
+ * Deterministic: a fixed 256 partials per tensor (fp64 accumulation) in `workspace`, then one
+ * fixed-order fold — no atomics.  workspace: device memory of at least n * 256 * 8 bytes
+ * (PRL_E_WORKSPACE otherwise). */
 int prl_grad_sqnorm(const void* const* srcs, const int32_t* dtypes, const int64_t* numels,
                     int32_t n, double* out, void* workspace, size_t workspace_bytes,
                     void* stream);

@@ -100,25 +100,41 @@ __global__ __launch_bounds__(256) void unflatten_bf16_kernel(PackGroup g, const 
   }
 }
 
-// sum of squares (double accumulation; one double atomic per block)
-__global__ __launch_bounds__(256) void sqnorm_kernel(PackGroup g, double* __restrict__ out) {
+// sum of squares, deterministic: block (x, t) of a group accumulates (double) a fixed grid-stride
+// share of tensor t and writes its partial to part[(group * kGroup + t) * gridDim.x + x]; sqnorm_fold
+// adds every partial in a fixed order.  No atomics: the bits do not depend on scheduling.
+__global__ __launch_bounds__(256) void sqnorm_kernel(PackGroup g, double* __restrict__ part) {
   const int t = blockIdx.y;
-  if (t >= g.n) return;
-  const int64_t n = g.numel[t];
-  const int dt = g.dtype[t];
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   double acc = 0.0;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const float v = load_as_f(g.src[t], dt, i);
-    acc += (double)v * (double)v;
+  if (t < g.n) {
+    const int64_t n = g.numel[t];
+    const int dt = g.dtype[t];
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+      const float v = load_as_f(g.src[t], dt, i);
+      acc += (double)v * (double)v;
+    }
   }
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
-  __shared__ double part[4];
+  __shared__ double w[4];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  if (lane == 0) part[wid] = acc;
+  if (lane == 0) w[wid] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(out, part[0] + part[1] + part[2] + part[3]);
+  if (threadIdx.x == 0) part[(int64_t)t * gridDim.x + blockIdx.x] = (w[0] + w[1]) + (w[2] + w[3]);
+}
+
+// one workgroup: thread i adds partials i, i + 256, ... in order, then a fixed tree
+__global__ __launch_bounds__(256) void sqnorm_fold(const double* __restrict__ part, int64_t n, double* __restrict__ out) {
+  double acc = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += 256) acc += part[i];
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  __shared__ double w[4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) w[wid] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) *out = (w[0] + w[1]) + (w[2] + w[3]);
 }
 
 // Gradient scale / accumulate for the fused lm_head's weight gradient (finetune/rl/fused_linear.py):
@@ -295,12 +311,15 @@ int prl_grad_scale_bf16(const void* src, int32_t src_dtype, const float* scale, 
 
 int prl_grad_sqnorm(const void* const* srcs, const int32_t* dtypes, const int64_t* numels, int32_t n,
                     double* out, void* workspace, size_t workspace_bytes, void* stream) {
-  (void)workspace;
-  (void)workspace_bytes;
   if (!out || n < 0 || (n > 0 && (!srcs || !dtypes || !numels))) return PRL_E_INVALID;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  hipError_t e = hipMemsetAsync(out, 0, sizeof(double), s);
-  if (e != hipSuccess) return (int)e;
+  if (n == 0) return (int)hipMemsetAsync(out, 0, sizeof(double), s);
+  // one partial per (tensor, block): a fixed kSqBlocks blocks per tensor, so the layout (and the
+  // summation order) depends only on n
+  constexpr int kSqBlocks = 256;
+  const size_t need = sizeof(double) * (size_t)n * kSqBlocks;
+  double* part = static_cast<double*>(workspace);
+  if (!part || workspace_bytes < need) return PRL_E_WORKSPACE;
   for (int base = 0; base < n; base += kGroup) {
     PackGroup g{};
     g.n = (n - base) < kGroup ? (n - base) : kGroup;
@@ -310,13 +329,12 @@ int prl_grad_sqnorm(const void* const* srcs, const int32_t* dtypes, const int64_
       g.dtype[i] = dtypes[base + i];
       g.numel[i] = numels[base + i];
     }
-    int gx = grid_x_for(g) * 8;
-    if (gx > 1024) gx = 1024;
-    hipLaunchKernelGGL(sqnorm_kernel, dim3(gx, g.n), dim3(256), 0, s, g, out);
-    e = hipGetLastError();
+    hipLaunchKernelGGL(sqnorm_kernel, dim3(kSqBlocks, g.n), dim3(256), 0, s, g, part + (size_t)base * kSqBlocks);
+    const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
   }
-  return PRL_OK;
+  hipLaunchKernelGGL(sqnorm_fold, dim3(1), dim3(256), 0, s, part, (int64_t)n * kSqBlocks, out);
+  return (int)hipGetLastError();
 }
 
 int prl_paced_read(const void* src, int64_t bytes, double gbps, int32_t blocks, uint32_t* sink, void* stream) {

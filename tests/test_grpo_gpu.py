@@ -457,7 +457,14 @@ def test_flatten_unflatten_and_sqnorm():
     for t, u in zip(ts, outs):
         assert torch.equal(u, t.to(torch.bfloat16).to(t.dtype))
     res = torch.zeros(1, dtype=torch.float64, device=DEV)
-    _native.check(lib.prl_grad_sqnorm(P, D, N, n, ctypes.cast(res.data_ptr(), ctypes.POINTER(ctypes.c_double)),
-                                      None, 0, st), "sqnorm")
+    rp = ctypes.cast(res.data_ptr(), ctypes.POINTER(ctypes.c_double))
+    assert lib.prl_grad_sqnorm(P, D, N, n, rp, None, 0, st) == 1003  # PRL_E_WORKSPACE
+    ws = torch.empty(n * 256, dtype=torch.float64, device=DEV)
+    _native.check(lib.prl_grad_sqnorm(P, D, N, n, rp, ws.data_ptr(), ws.numel() * 8, st), "sqnorm")
     want = sum(float((t.double() ** 2).sum()) for t in ts)
     assert abs(float(res) - want) <= 1e-9 * want
+    # deterministic: the same bits on every call (fixed partials, fixed fold; no atomics)
+    bits = float(res)
+    for _ in range(5):
+        _native.check(lib.prl_grad_sqnorm(P, D, N, n, rp, ws.data_ptr(), ws.numel() * 8, st), "sqnorm")
+        assert float(res) == bits
