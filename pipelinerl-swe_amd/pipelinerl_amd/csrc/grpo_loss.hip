@@ -246,6 +246,13 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
 #else
   constexpr bool kCopyCeiling = false;
 #endif
+#ifdef PRL_NO_PASS1
+  // measurement only (with PRL_COPY_CEILING): pass 1's statistics skipped too — wrong results,
+  // the schedule's pure data movement
+  constexpr bool kNoPass1 = true;
+#else
+  constexpr bool kNoPass1 = false;
+#endif
   __shared__ float red[2][NW][3];
   __shared__ int64_t next_q[2];  // the workgroup's next row, by row parity (published at the row's barrier)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -307,10 +314,13 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
         x[2 * j] = bf_lo(v[j]);
         x[2 * j + 1] = bf_hi(v[j]);
       }
-      if constexpr (kFoldExp)
+      if constexpr (kNoPass1) {
+        st2.s.x += x[0];  // keeps the loads' consumers (one add per vector)
+      } else if constexpr (kFoldExp) {
         lse2_add<8>(st2, x, c);
-      else
+      } else {
         lse_add<8>(st, x, c);
+      }
     }
     if constexpr (kFoldExp) st = Lse{st2.m, st2.s.x + st2.s.y, st2.w.x + st2.w.y};
     st = wave_reduce_lse(st, c);

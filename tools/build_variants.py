@@ -13,6 +13,7 @@ VARIANTS = {  # the loss head's A/B builds (csrc/grpo_loss.hip macros); profiles
     "st_sc1_nt": {"PRL_STORE_AUX": "18"},
     "ld_sc1_nt_st_sc1_nt": {"PRL_LOAD_AUX": "18", "PRL_STORE_AUX": "18"},
     "copy_ceiling": {"PRL_COPY_CEILING": "1"},  # same schedule, no math: the kernel's own ceiling
+    "no_math": {"PRL_COPY_CEILING": "1", "PRL_NO_PASS1": "1"},  # neither pass's math (measurement only)
     "row_sequential": {"PRL_ROW_PERMUTE": "0"},
     "unphased": {"PRL_PHASED": "0"},
     "phased_nowait": {"PRL_PHASED": "2"},  # phased order, no wait for the stores before the next row's loads
