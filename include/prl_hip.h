@@ -237,6 +237,22 @@ int prl_adamw_step(int32_t n, void* const* params, const void* const* grads, voi
                    double lr, double beta1, double beta2, double weight_decay, double eps, const void* grad_scale,
                    void* stream);
 
+/* AdamW with fp32 master weights (csrc/adamw.hip): the optimizer state of the reference's default
+ * backend, DeepSpeed's bf16 ZeRO optimizer (conf/deepspeed/deepspeed_stage3_bf16.json: fp32 master
+ * partitions, fp32 Adam states) and of its FSDP mixed precision (accelerate upcasts the parameters
+ * to fp32 in prepare, pipelinerl/finetune_loop.py:355-396).  Per tensor i: grads[i] (grad_dtype,
+ * PRL_BF16 or PRL_F32) is read, multiplied in fp32 by *grad_scale (device float; NULL = none: the
+ * clip coefficient, as clip_grad_norm_'s foreach_mul_ on fp32 gradients), and the fp32 masters[i],
+ * exp_avgs[i], exp_avg_sqs[i] take torch's fused-AdamW fp32 update (ADAMW mode, steps[i] already
+ * incremented); params[i] (bf16) receives the round-to-nearest-even of the new master.  One pass:
+ * 14 B read + 14 B written per parameter with bf16 gradients.  Host arrays of length n; every
+ * entry is validated before the first launch.  Replaces clip_grad_norm_'s multiply +
+ * optimizer.step() + the bf16 copy-back at pipelinerl/finetune_loop.py:700-719. */
+int prl_adamw_master_step(int32_t n, void* const* params, const void* const* grads, float* const* masters,
+                          float* const* exp_avgs, float* const* exp_avg_sqs, const float* const* steps,
+                          const int64_t* numels, int32_t grad_dtype, double lr, double beta1, double beta2,
+                          double weight_decay, double eps, const float* grad_scale, void* stream);
+
 /* Sum of squares of n device tensors (f32 or bf16) into *out (device f64; overwritten).
  * Deterministic: a fixed 256 partials per tensor (fp64 accumulation) in `workspace`, then one
  * fixed-order fold — no atomics.  workspace: device memory of at least n * 256 * 8 bytes

@@ -84,6 +84,9 @@ _SIGNATURES = {
     "prl_grpo_pair_fallbacks": (c_int, [c_int, c_void_p, POINTER(ctypes.c_uint64)]),
     "prl_adamw_step": (c_int, [c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32,
                                c_double, c_double, c_double, c_double, c_double, c_void_p, c_void_p]),
+    "prl_adamw_master_step": (c_int, [c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                      c_int32, c_double, c_double, c_double, c_double, c_double, c_void_p,
+                                      c_void_p]),
     "prl_grad_sqnorm": (c_int, [POINTER(c_void_p), POINTER(c_int32), POINTER(c_int64), c_int32,
                                 POINTER(c_double), c_void_p, c_size_t, c_void_p]),
     "prl_rmsnorm_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_float, c_void_p]),

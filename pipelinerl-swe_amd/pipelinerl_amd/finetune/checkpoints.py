@@ -51,10 +51,13 @@ def has_weights(d: Path) -> bool:
     return any((Path(d) / f).exists() for f in WEIGHT_FILES)
 
 
-def load_model(args, model_class: str, current_dir: Path, device: torch.device, shard_world: int = 1):
+def load_model(args, model_class: str, current_dir: Path, device: torch.device, shard_world=1,
+               master_weights: bool | None = None):
     """HF causal LM from ``current_dir`` (resume) or ``args.config_name``; optional value head.
     Gradient checkpointing as the config asks, unless its activations fit the device
-    (``gradient_checkpointing_policy``, finetune/recompute.py; ``shard_world``: the FSDP world)."""
+    (``gradient_checkpointing_policy``, finetune/recompute.py; ``shard_world``: the FSDP world, or a
+    callable deciding it from the built model — finetune/sharding.py decide_sharding;
+    ``master_weights``: the optimizer keeps fp32 masters, counted in the memory plan)."""
     from transformers import AutoConfig, AutoModelForCausalLM
 
     src = str(current_dir) if has_weights(current_dir) else args.config_name
@@ -79,7 +82,9 @@ def load_model(args, model_class: str, current_dir: Path, device: torch.device, 
         patch_model(model)
     from .recompute import plan_gradient_checkpointing
 
-    plan = plan_gradient_checkpointing(args, model, device, shard_world)
+    if callable(shard_world):
+        shard_world = int(shard_world(model))
+    plan = plan_gradient_checkpointing(args, model, device, shard_world, master_weights=master_weights)
     if args.get("gradient_checkpointing", False):
         logger.info(f"gradient checkpointing: {plan.as_dict()}")
     if plan.checkpoint:
@@ -146,6 +151,10 @@ def save_model_and_tokenizer(output_dir: Path, model, tokenizer, *, safe_seriali
                 # namespace: a value-head wrapper splits them (value_model.save_pretrained)
                 sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
             if sd is not None:
+                save_dtype = getattr(m, "_prl_save_dtype", None)
+                if save_dtype is not None:  # fp32 master shards: save the model's own dtype, as DeepSpeed's
+                    # stage3_gather_16bit_weights_on_model_save does (conf/deepspeed/deepspeed_stage3_bf16.json)
+                    sd = {k: v.to(save_dtype) if v.is_floating_point() else v for k, v in sd.items()}
                 if getattr(getattr(m, "config", None), "tie_word_embeddings", False):
                     # tied copy (finetune_loop.py:228-231), under the wrapper's prefix too
                     lm_prefix = "pretrained_model." if hasattr(m, "pretrained_model") else ""

@@ -32,8 +32,9 @@ forward is the same deterministic kernels on the same inputs).
                       device), else R = 0, FSDP's default.  0 turns it off.
 
 The estimate is deliberately conservative (upper bounds, measured against the trainer probes'
-peak memory in DESIGN.md): model state = parameters x (weight + gradient + two AdamW moments),
-divided by the FSDP world when sharded; activations = the tensors a patched Qwen2-style decoder
+peak memory in DESIGN.md): model state = parameters x (weight + gradient + two AdamW moments; with
+fp32 master weights, the reference default's optimizer state, 16 B per parameter), divided by the
+FSDP world when sharded — a model state that alone exceeds the device raises ModelStateTooLarge; activations = the tensors a patched Qwen2-style decoder
 layer keeps for its backward per token (the normed inputs of the q/k/v and gate/up GEMMs, q, k,
 v, the attention output, the residual stream, gate, up and the SwiGLU output), times
 ``seq_length`` tokens, times the layers, times a 1.25 allowance for backward temporaries; one
@@ -192,16 +193,69 @@ def plan_fsdp_gathering(args, model, plan: RecomputePlan, shard_world: int) -> R
     return plan
 
 
+class ModelStateTooLarge(MemoryError):
+    """The model state alone (weights, gradients, optimizer state) does not fit one device: no
+    recompute plan can help; the model must be sharded (FSDP)."""
+
+
+def state_bytes_per_param(param_bytes: int, master_weights: bool) -> int:
+    """Model-state bytes per parameter: weight + gradient + the two AdamW moments in the parameter
+    dtype (pure bf16: 8 B), or with fp32 master weights (finetune/optim.py; an FSDP-sharded model
+    keeps its sharded parameters and gradients in fp32 instead, finetune/sharding.py) a bf16
+    weight + gradient and an fp32 master + two fp32 moments: 16 B."""
+    if master_weights and param_bytes == 2:
+        return 16
+    return 4 * param_bytes
+
+
+def model_state_bytes(model, shard_world: int = 1, master_weights: bool = True) -> int:
+    params = list(model.parameters())
+    pbytes = params[0].element_size() if params else 2
+    return state_bytes_per_param(pbytes, master_weights) * sum(p.numel() for p in params) // max(1, int(shard_world))
+
+
+def _master_weights_of(args, master_weights: bool | None) -> bool:
+    if master_weights is not None:
+        return bool(master_weights)
+    mode = args.get("master_weights", "auto")
+    return mode if isinstance(mode, bool) else True  # auto: the reference default's (masters)
+
+
+def check_model_state_fits(model, device: torch.device, shard_world: int = 1, master_weights: bool = True,
+                           device_bytes: int | None = None) -> None:
+    """Raise ModelStateTooLarge when the model state alone exceeds the device (less the plan's
+    headroom); silently returns when the device cannot be sized (not a HIP device, no size given)."""
+    if device_bytes is None:
+        if device.type != "cuda":
+            return
+        device_bytes = int(torch.cuda.get_device_properties(device).total_memory)
+    state = model_state_bytes(model, shard_world, master_weights)
+    room = int(device_bytes) - int(HEADROOM_FRAC * int(device_bytes)) - HEADROOM_BYTES
+    if state > room:
+        n = sum(p.numel() for p in model.parameters())
+        raise ModelStateTooLarge(
+            f"model state {state / 1e9:.1f} GB ({n / 1e9:.2f} B parameters x "
+            f"{state_bytes_per_param(next(model.parameters()).element_size(), master_weights)} B"
+            f"{'' if shard_world <= 1 else f' / {shard_world} ranks'}) exceeds the device's "
+            f"{room / 1e9:.1f} GB usable: shard the model (use_fsdp=true, finetune.sharding=fsdp, or the "
+            "reference's default DeepSpeed ZeRO-3 config with finetune.sharding=auto) over more ranks")
+
+
 def plan_gradient_checkpointing(args, model, device: torch.device, shard_world: int = 1,
-                                device_bytes: int | None = None) -> RecomputePlan:
+                                device_bytes: int | None = None, master_weights: bool | None = None) -> RecomputePlan:
     """The decision for ``model`` (already built) under the trainer config ``args``;
-    ``device_bytes``: the device's memory (default: queried from the HIP device).  Under FSDP
-    (``shard_world`` > 1) also how many decoder layers stay gathered (plan_fsdp_gathering)."""
-    return plan_fsdp_gathering(args, model, _plan_recompute(args, model, device, shard_world, device_bytes),
+    ``device_bytes``: the device's memory (default: queried from the HIP device); ``master_weights``:
+    the optimizer keeps fp32 masters (default: ``args.master_weights``, ``auto`` counting them).
+    Under FSDP (``shard_world`` > 1) also how many decoder layers stay gathered
+    (plan_fsdp_gathering).  Raises ModelStateTooLarge when the model state alone cannot fit."""
+    master = _master_weights_of(args, master_weights)
+    check_model_state_fits(model, device, shard_world, master, device_bytes)
+    return plan_fsdp_gathering(args, model, _plan_recompute(args, model, device, shard_world, device_bytes, master),
                                shard_world)
 
 
-def _plan_recompute(args, model, device: torch.device, shard_world: int, device_bytes: int | None) -> RecomputePlan:
+def _plan_recompute(args, model, device: torch.device, shard_world: int, device_bytes: int | None,
+                    master: bool = True) -> RecomputePlan:
     if not args.get("gradient_checkpointing", False):
         return RecomputePlan(False, "gradient_checkpointing is off")
     policy = str(args.get("gradient_checkpointing_policy", "auto"))
@@ -228,8 +282,9 @@ def _plan_recompute(args, model, device: torch.device, shard_world: int, device_
     pbytes = params[0].element_size() if params else 2
     sw = max(1, int(shard_world))
     L = int(config.num_hidden_layers)
-    # weight + gradient + exp_avg + exp_avg_sq, all in the parameter dtype (torch / PrlAdamW)
-    state = 4 * n * pbytes // sw
+    # weight + gradient + exp_avg + exp_avg_sq in the parameter dtype, or with fp32 masters
+    # (PrlAdamW master_weights / FSDP's fp32 shards) 16 B per parameter
+    state = state_bytes_per_param(pbytes, master) * n // sw
     act = int(ACT_ALLOWANCE * int(seq) * activation_bytes_per_token(config, pbytes))
     vocab = int(getattr(config, "vocab_size", 0))
     rl = args.get("rl", None) or {}
@@ -278,6 +333,11 @@ def _plan_recompute(args, model, device: torch.device, shard_world: int, device_
     while keep > 0 and need_for(keep)[0] > total:
         keep -= 1
     need_k, _, buffers_k = need_for(keep)
+    if keep == 0 and need_k > total:
+        raise ModelStateTooLarge(
+            f"the model does not fit the device even with every layer recomputed: {need_k / 1e9:.1f} GB needed "
+            f"(model state {state / 1e9:.1f} GB{'' if sw <= 1 else f' per rank over {sw}'}) of {total / 1e9:.1f} GB: "
+            "shard the model (use_fsdp=true, finetune.sharding=fsdp) over more ranks, or shorten seq_length")
     reason = (f"activations of the last {keep} of {L} layers fit: {L - keep} recompute" if keep > 0
               else "activations do not fit: recompute")
     return RecomputePlan(True, reason, state, act, logits, buffers_k, total, need_k, keep)

@@ -42,10 +42,10 @@ import torch.distributed as dist
 from .finetune.checkpoints import (load_model, load_tokenizer, load_training_state, remove_results,
                                    save_model_and_tokenizer, save_training_state)
 from .finetune.grad_sync import GradBuckets
-from .finetune.optim import clip_grad_norm, get_optimizer
+from .finetune.optim import clip_grad_norm, get_optimizer, master_weights_requested
 from .finetune.rl import RLConfig, RLStats, rl_step
 from .finetune.rl.utils import aggregate_rl_stats
-from .finetune.sharding import fsdp_requested, is_sharded, set_gradient_sync, shard_model
+from .finetune.sharding import decide_sharding, is_sharded, set_gradient_sync, shard_model
 from .finetune.trace import PhaseTrace
 from . import native_data
 from .devalloc import DEFAULT_SETTINGS, configure_device_allocator
@@ -203,16 +203,32 @@ def run_finetuning_loop(cfg, step_fn: Callable = rl_step, model=None, tokenizer=
     setup_logging(log_dir, ctx.rank)
     update_stream = SingleStreamSpec(exp_path=exp_root, topic=TRAINER_TOPIC)
 
-    sharded = fsdp_requested(cfg, args) and ctx.initialized
+    master = master_weights_requested(cfg)  # fp32 masters + moments: the reference default's optimizer state
+    world = ctx.world if ctx.initialized else 1
+    layout: dict[str, Any] = {}
+
+    def choose_shard_world(m) -> int:
+        """The model state's layout over the DP ranks (finetune/sharding.py decide_sharding)."""
+        shard, reason = decide_sharding(cfg, args, m, ctx.device, world, master)
+        layout.update(shard=shard, reason=reason)
+        if ctx.is_main:
+            logger.info(f"model state layout: {'FSDP' if shard else 'replicas'} ({reason}); "
+                        f"optimizer state: {'fp32 master weights + fp32 AdamW moments' if master else 'bf16'}")
+        return world if shard else 1
+
     snapshot = weight_snapshot_mode(args)
     if model is None:
-        model = load_model(args, args.model_class, current_dir, ctx.device, shard_world=ctx.world if sharded else 1)
+        model = load_model(args, args.model_class, current_dir, ctx.device, shard_world=choose_shard_world,
+                           master_weights=master)
+    else:
+        choose_shard_world(model)
+    sharded = layout["shard"]
     if tokenizer is None:
         tokenizer = load_tokenizer(args.config_name, getattr(getattr(model, "config", None), "eos_token_id", None))
     if sharded:  # before the optimizer: it must see the sharded parameters
         plan = getattr(model, "prl_memory_plan", None)  # load_model's (finetune/recompute.py)
         model = shard_model(model, cfg.get("fsdp"), grad_reduce=args.get("grad_reduce", "mean"),
-                            keep_gathered=plan.gathered_layers if plan is not None else 0)
+                            keep_gathered=plan.gathered_layers if plan is not None else 0, master_weights=master)
     elif args.get("flat_parameters", True):
         # every bf16 parameter into one buffer in the weight broadcast's layout (weight_update.py):
         # in-place broadcasts, the gate / up projections one tensor without a concatenation copy
@@ -220,7 +236,7 @@ def run_finetuning_loop(cfg, step_fn: Callable = rl_step, model=None, tokenizer=
 
         rehome_parameters(model)
     data_stream = SingleStreamSpec(exp_path=exp_root, topic=args.input, instance=0, partition=ctx.rank)
-    optimizer = get_optimizer(args.optim, model, args.learning_rate, args.weight_decay)
+    optimizer = get_optimizer(args.optim, model, args.learning_rate, args.weight_decay, master_weights=master)
     from transformers import get_scheduler
 
     lr_scheduler = get_scheduler(args.lr_scheduler_type, optimizer, args.num_warmup_steps, args.max_train_steps)

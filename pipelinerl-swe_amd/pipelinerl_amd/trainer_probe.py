@@ -119,11 +119,12 @@ class TrainerStep:
                  fused_ops: bool = True, group=None, model=None, step_fn=None, vocab: int | None = None,
                  fsdp: bool = False, kl_coef: float = 0.0, layers: int | None = None, batches: list | None = None,
                  samples_per_step: int | None = None, local: bool = False, flat_params: bool = True,
-                 keep_layers: int = 0):
+                 keep_layers: int = 0, master_weights: bool = True):
         """``batches``: the packed micro-batches to train on (host PipelineBatchEncodings, e.g. from
         workloads.micro_batches), ``samples_per_step`` their global sample count (RLConfig.batch_size);
         default: ``micro_batches`` synthetic batches of ``tokens`` tokens.  ``local``: no gradient
-        all-reduce even under a multi-rank group (the replica's compute alone, for the DP overhead)."""
+        all-reduce even under a multi-rank group (the replica's compute alone, for the DP overhead).
+        ``master_weights``: fp32 master weights + moments, the trainer's default (finetune/optim.py)."""
         from .finetune.grad_sync import GradBuckets
         from .finetune.optim import get_optimizer
         from .finetune.sharding import shard_model
@@ -139,7 +140,7 @@ class TrainerStep:
         if fsdp:  # FSDP2 over the default group (finetune/sharding.py): it reduce-scatters the grads
             if group is not None:
                 raise ValueError("fsdp shards over the default process group")
-            self.model = shard_model(self.model)
+            self.model = shard_model(self.model, master_weights=master_weights)
         elif flat_params:  # as the loop does at load (finetune.flat_parameters, weight_update.py)
             from .weight_update import rehome_parameters
 
@@ -150,7 +151,7 @@ class TrainerStep:
         self._tail_events: list = []
         self._tail_cpu: list[float] = []
         self.step_fn = step_fn if step_fn is not None else rl_step
-        self.opt = get_optimizer("adamw_torch", self.model, 1e-6, 0.01)
+        self.opt = get_optimizer("adamw_torch", self.model, 1e-6, 0.01, master_weights=master_weights)
         self.grads = GradBuckets(list(self.model.parameters()), group=group) \
             if world > 1 and not fsdp and not local else None
         V = vocab or QWEN[name]["vocab_size"]

@@ -163,7 +163,9 @@ def test_deepspeed_grad_scale_convention(tmp_path):
         exp = tmp_path / mode
         exp.mkdir()
         per_step, _ = _setup(exp, world)
-        mp.spawn(_grad_capture_main, args=(world, free_port(), str(exp), 1, per_step, {"grad_scale": mode}),
+        # (master_weights off: the capture wraps torch's clip_grad_norm_, which PrlAdamW's fp32 norm skips)
+        extra = {"grad_scale": mode, "master_weights": False}
+        mp.spawn(_grad_capture_main, args=(world, free_port(), str(exp), 1, per_step, extra),
                  nprocs=world, join=True)
         runs[mode] = torch.load(exp / "grads_r0.pt")
     gas = per_step // world

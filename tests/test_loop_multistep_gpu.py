@@ -3,10 +3,12 @@ with every default on (fused gate/up at these <= 12 288-token micro-batches, nat
 gradient accumulation, deferred statistics, the gc freeze, label-row lm_head) against a plain
 restatement of the reference's step run beside it on the same initial weights and micro-batches:
 HF eager ops on the same bf16 weights (the reference's precision: conf/finetune/base.yaml
-``load_as_bf16: True``, Accelerate's AdamW on them), torch's library attention, the torch
-restatement of rl_step (tests/cpu_rl_step.py, pinned to the oracle by test_configs_gpu.py),
-autograd accumulation, ``clip_grad_norm_(0.3)`` + ``torch.optim.AdamW`` + the cosine schedule
-(finetune_loop.py:700-719).
+``load_as_bf16: True``), torch's library attention, the torch restatement of rl_step
+(tests/cpu_rl_step.py, pinned to the oracle by test_configs_gpu.py), autograd accumulation,
+``clip_grad_norm_(0.3)`` + ``torch.optim.AdamW`` + the cosine schedule (finetune_loop.py:700-719)
+on fp32 master copies of the weights, which the bf16 model weights round from — the optimizer state
+of the reference's default backend (DeepSpeed bf16 ZeRO-3, conf/base.yaml:94-95), which the
+product keeps too (finetune.master_weights auto).
 
 Compared per step: every micro-batch's statistics, the pre-clip gradient norm, EVERY parameter's
 pre-clip gradient on its own against the reference step's gradient AT THE PRODUCT'S OWN PRE-STEP
@@ -96,8 +98,11 @@ def _product_run(tmp_path, init, stale_cache=False):
         assert isinstance(opt, PrlAdamW)  # the clip is deferred: .grad is pre-clip in the pre-hook
         opt.register_step_pre_hook(lambda o, args, kw: grads.append(
             {n: p.grad.detach().float().clone() for n, p in model.named_parameters() if p.grad is not None}))
-        opt.register_step_post_hook(
-            lambda o, args, kw: snaps.append({n: p.detach().float().clone() for n, p in model.named_parameters()}))
+        # the weights the optimizer holds: the fp32 masters (the bf16 weights are their rounding, whose
+        # sub-ulp steps at a small lr would compare rounding noise rather than updates)
+        opt.register_step_post_hook(lambda o, args, kw: snaps.append(
+            {n: (o.state[p]["master"] if "master" in o.state[p] else p.detach().float()).clone()
+             for n, p in model.named_parameters()}))
         return opt
 
     def resolve(self):
@@ -154,7 +159,16 @@ def _reference_run(init, steps):
     try:
         ref = qwen2_model("0.5b", torch.device(DEV), fused_ops=False, layers=LAYERS)
         ref.load_state_dict(init)
-        opt = torch.optim.AdamW(get_grouped_params(ref, 0.01), lr=LR)
+        # the reference default's optimizer state (DeepSpeed bf16 ZeRO-3 / FSDP mixed precision):
+        # fp32 masters + fp32 AdamW, the model's bf16 weights their rounding
+        named = list(ref.named_parameters())
+        masters = {n: torch.nn.Parameter(p.detach().float().clone()) for n, p in named}
+
+        class _Masters(torch.nn.Module):
+            def named_parameters(self, *a, **k):
+                return iter(masters.items())
+
+        opt = torch.optim.AdamW(get_grouped_params(_Masters(), 0.01), lr=LR)
         sched = get_scheduler("cosine", opt, 0, len(steps))
         rlc = workloads.rl_config("c1", PER_STEP)
         snaps = [{n: p.detach().float().clone() for n, p in ref.named_parameters()}]
@@ -167,11 +181,17 @@ def _reference_run(init, steps):
                 loss.backward()
                 stats.append(st)
             grads.append({n: p.grad.detach().float().clone() for n, p in ref.named_parameters() if p.grad is not None})
-            norms.append(float(torch.nn.utils.clip_grad_norm_(ref.parameters(), 0.3)))
+            for n, p in named:
+                masters[n].grad = p.grad.float()
+            norms.append(float(torch.nn.utils.clip_grad_norm_(list(masters.values()), 0.3)))
             opt.step()
+            with torch.no_grad():
+                for n, p in named:
+                    p.copy_(masters[n])
             opt.zero_grad(set_to_none=True)
+            ref.zero_grad(set_to_none=True)
             sched.step()
-            snaps.append({n: p.detach().float().clone() for n, p in ref.named_parameters()})
+            snaps.append({n: m.detach().clone() for n, m in masters.items()})
     finally:
         for k, v in saved.items():
             os.environ.pop(k, None) if v is None else os.environ.__setitem__(k, v)
@@ -294,7 +314,7 @@ def test_c1_three_optimizer_steps_match_the_reference_step(tmp_path):
     # per-tensor pre-clip gradients, step by step, against the reference's gradient at the
     # product's own pre-step weights (step 1: the shared initial weights, == ref_grads[0])
     assert len(grads) == len(ref_grads) == len(steps)
-    ref_at = _reference_grads_at(snaps, steps)
+    ref_at = _reference_grads_at(snaps, steps)  # (loaded as bf16: the masters' rounding, the product's weights)
     g_errs = [_grad_errors(g, r) for g, r in zip(grads, ref_at)]
     drift = [max(v[0] for v in _grad_errors(g, r).values()) for g, r in zip(grads, ref_grads)]
     worst_rel = [max(e.items(), key=lambda kv: kv[1][0]) for e in g_errs]

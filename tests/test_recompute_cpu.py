@@ -39,13 +39,25 @@ def m7b():
 def test_7b_c3_fits_mi355x(m7b):
     from pipelinerl_amd.finetune.recompute import plan_gradient_checkpointing
 
+    from pipelinerl_amd.finetune.recompute import ModelStateTooLarge
+
     p = plan_gradient_checkpointing(_args(), m7b, torch.device("cuda"), device_bytes=288 * GB)
     assert not p.checkpoint, p.as_dict()
-    # 7.6 B bf16 parameters x (weight, grad, 2 moments); activations of 12 000 tokens over 28 layers
-    assert 60 * GB < p.state_bytes < 62 * GB
+    # 7.6 B parameters x (bf16 weight + grad, fp32 master + 2 moments: the reference default's
+    # optimizer state); activations of 12 000 tokens over 28 layers
+    assert 121 * GB < p.state_bytes < 123 * GB
     assert 60 * GB < p.activation_bytes < 75 * GB
-    # the same micro-batch on an 80 GB card recomputes
-    assert plan_gradient_checkpointing(_args(), m7b, torch.device("cuda"), device_bytes=80 * GB).checkpoint
+    # pure bf16 state (finetune.master_weights=false): 8 B per parameter
+    pb = plan_gradient_checkpointing(_args(master_weights=False), m7b, torch.device("cuda"), device_bytes=288 * GB)
+    assert 60 * GB < pb.state_bytes < 62 * GB
+    # the same micro-batch on a 100 GB card recomputes (bf16 state), or cannot hold the fp32 state at
+    # all; an 80 GB card cannot hold even the bf16 state beside one recomputed layer
+    assert plan_gradient_checkpointing(_args(master_weights=False), m7b, torch.device("cuda"),
+                                       device_bytes=100 * GB).checkpoint
+    for dev_gb, master in ((100, True), (80, False)):
+        with pytest.raises(ModelStateTooLarge, match="shard the model"):
+            plan_gradient_checkpointing(_args(master_weights=master), m7b, torch.device("cuda"),
+                                        device_bytes=dev_gb * GB)
 
 
 def test_policy_and_reference_fallbacks(m7b):
@@ -71,10 +83,18 @@ def test_32b_needs_sharding():
     m = _meta_model("32b")
     args = _args(seq_length=4096)
     cuda = torch.device("cuda")
-    # unsharded, the model state alone (262 GB) leaves no room; FSDP over 4 trainer GPUs does
-    assert plan_gradient_checkpointing(args, m, cuda, shard_world=1, device_bytes=288 * GB).checkpoint
+    from pipelinerl_amd.finetune.recompute import ModelStateTooLarge
+
+    # unsharded, the model state (524 GB with fp32 masters; 262 GB in pure bf16, which leaves no room
+    # for even one layer's activations) does not fit: a named error pointing at FSDP, not a
+    # recompute plan that would still run out of memory
+    for master in (True, False):
+        with pytest.raises(ModelStateTooLarge, match="use_fsdp"):
+            plan_gradient_checkpointing(_args(seq_length=4096, master_weights=master), m, cuda, shard_world=1,
+                                        device_bytes=288 * GB)
     p = plan_gradient_checkpointing(args, m, cuda, shard_world=4, device_bytes=288 * GB)
     assert not p.checkpoint, p.as_dict()
+    assert 130 * GB < p.state_bytes < 132 * GB  # 524 GB / 4
 
 
 def test_label_row_chunk_sizes_the_logits(m7b):
@@ -154,8 +174,11 @@ def test_plan_counts_the_allocator_rounding(m7b, monkeypatch):
     assert not plan_gradient_checkpointing(_args(), m7b, cuda, device_bytes=dev).checkpoint
     monkeypatch.setattr(devalloc, "_applied", devalloc.DEFAULT_SETTINGS)
     m32 = _meta_model("32b")
-    p = plan_gradient_checkpointing(_args(), m32, cuda, shard_world=8, device_bytes=288 * 2 ** 30)
+    p = plan_gradient_checkpointing(_args(master_weights=False), m32, cuda, shard_world=8, device_bytes=288 * 2 ** 30)
     assert not p.checkpoint, p.as_dict()
+    # with fp32 masters (65.5 GB of state per rank instead of 32.8) a few layers recompute
+    pm = plan_gradient_checkpointing(_args(), m32, cuda, shard_world=8, device_bytes=288 * 2 ** 30)
+    assert pm.checkpoint and 48 <= pm.keep_layers < 64, pm.as_dict()
 
 
 def test_round_size_follows_the_allocator():
@@ -200,7 +223,7 @@ def test_partial_recompute_keeps_the_layers_that_fit(monkeypatch):
                                        device_bytes=dev)
     assert not allk.checkpoint
     # "always" is the reference's behaviour: every layer recomputes
-    assert plan_gradient_checkpointing(_args(gradient_checkpointing_policy="always"), m32, cuda,
+    assert plan_gradient_checkpointing(_args(gradient_checkpointing_policy="always"), m32, cuda, shard_world=4,
                                        device_bytes=dev).keep_layers == 0
 
 
@@ -268,7 +291,7 @@ def test_fsdp_gathered_layers_spend_the_spare_memory(monkeypatch):
     assert plan_gradient_checkpointing(_args(seq_length=4096, fsdp_keep_gathered_layers=5), m32, cuda,
                                        shard_world=8, device_bytes=dev).gathered_layers == 5
     assert plan_gradient_checkpointing(_args(seq_length=4096), m32, cuda, shard_world=1,
-                                       device_bytes=dev).gathered_layers == 0
+                                       device_bytes=4 * dev).gathered_layers == 0
     assert plan_gradient_checkpointing(_args(gradient_checkpointing_policy="always"), m32, cuda, shard_world=8,
                                        device_bytes=dev).gathered_layers == 0
     for bad in (-1, "all", True):
