@@ -93,10 +93,10 @@ def decide_sharding(cfg, args, model, device, world: int, master_weights: bool,
     state).  Numerically the two layouts give the same update (fp32 masters either way); only the
     summation order of the gradient reduction differs."""
     mode = sharding_mode(cfg, args)
+    if mode == "fsdp":  # (also on one rank: the FSDP code path itself, as the reference's FSDP launch)
+        return True, "sharding requested (use_fsdp / finetune.sharding=fsdp)"
     if world <= 1:
         return False, "one data-parallel rank: nothing to shard"
-    if mode == "fsdp":
-        return True, "sharding requested (use_fsdp / finetune.sharding=fsdp)"
     if mode == "none":
         return False, ("replicas (finetune.sharding=none)" if str(args.get("sharding", "auto")) == "none"
                        else "replicas: the reference's backend here is plain DDP (no DeepSpeed, no FSDP)")

@@ -222,7 +222,7 @@ def run_finetuning_loop(cfg, step_fn: Callable = rl_step, model=None, tokenizer=
                            master_weights=master)
     else:
         choose_shard_world(model)
-    sharded = layout["shard"]
+    sharded = layout["shard"] and ctx.initialized  # FSDP2 needs a process group (one rank included)
     if tokenizer is None:
         tokenizer = load_tokenizer(args.config_name, getattr(getattr(model, "config", None), "eos_token_id", None))
     if sharded:  # before the optimizer: it must see the sharded parameters
@@ -359,8 +359,10 @@ def grad_scale_convention(cfg) -> str:
             logger.warning(
                 f"use_deepspeed is false but the config still names deepspeed_config={cfg.get('deepspeed_config')}: "
                 "the reference's default run uses DeepSpeed's gradient-accumulation scale (every micro-batch loss "
-                "/ GAS); this run sums micro-batch gradients (accelerate). Set finetune.grad_scale=deepspeed to "
-                "keep the reference default's gradients, or finetune.grad_scale=accelerate to silence this warning")
+                "/ GAS) and fp32 master weights; this run sums micro-batch gradients (accelerate) and, unless "
+                "finetune.master_weights=true, trains the bf16 weights directly. Set finetune.grad_scale=deepspeed "
+                "and finetune.master_weights=true to keep the reference default's gradients and optimizer state, or "
+                "finetune.grad_scale=accelerate to silence this warning")
     if mode not in ("accelerate", "deepspeed"):
         raise ValueError(f"finetune.grad_scale must be 'accelerate' or 'deepspeed', got {mode!r}")
     return mode

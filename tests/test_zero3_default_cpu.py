@@ -51,7 +51,8 @@ def test_reference_default_config_selects_the_layout():
     assert decide_sharding(cfg, args_f, _meta("7b"), cuda, 4, True, device_bytes=288 * GB)[0]
     args_n = dict(args, sharding="none")
     assert not decide_sharding(cfg, args_n, _meta("32b"), cuda, 4, True, device_bytes=288 * GB)[0]
-    assert not decide_sharding(cfg, args, _meta("32b"), cuda, 1, True, device_bytes=288 * GB)[0]
+    assert not decide_sharding(cfg, args, _meta("7b"), cuda, 1, True, device_bytes=288 * GB)[0]
+    assert decide_sharding(cfg, args_f, _meta("7b"), cuda, 1, True, device_bytes=288 * GB)[0]  # asked for
     with pytest.raises(ValueError):
         sharding_mode(cfg, dict(args, sharding="zero3"))
 
