@@ -161,9 +161,11 @@ int prl_grpo_forward(const PrlGrpoBatch* batch, const PrlGrpoParams* params,
  * int64, q = b*(L-1) + t, each < B*(L-1)); B and L describe the whole batch, whose token
  * fields are read at those rows.  Per-row outputs land at index row_ids[i] of the
  * B*(L-1)-entry arrays; dlogits (write_grad) is [n, ld] and may alias batch->logits
- * (every row is read before its gradient is stored).  No statistics (out->stats unused)
- * and no value head (values must be NULL).  Replaces the [T, V] slice of the ATen chain
- * rl/__init__.py:199-208 for the rows its mask (:152-153) keeps. */
+ * (every row is read before its gradient is stored).  No statistics (out->stats unused).
+ * A value head's batch->values (every row) enter only through the advantage, reward - value
+ * (rl/__init__.py:239-248); out->dvalues must be given, as for prl_grpo_forward, but the value
+ * loss, its statistics and dvalues are written by prl_grpo_stats.  Replaces the [T, V] slice of
+ * the ATen chain rl/__init__.py:199-208 for the rows its mask (:152-153) keeps. */
 int prl_grpo_forward_rows(const PrlGrpoBatch* batch, const PrlGrpoParams* params,
                           const int64_t* row_ids, int64_t n, const PrlGrpoOutputs* out,
                           void* stream);

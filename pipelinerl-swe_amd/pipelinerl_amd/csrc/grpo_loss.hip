@@ -1526,7 +1526,9 @@ int prl_grpo_forward_rows(const PrlGrpoBatch* batch, const PrlGrpoParams* params
   KArgs a;
   int rc = fill_args(a, batch, params);
   if (rc) return rc;
-  if (batch->values) return PRL_E_UNSUPPORTED;
+  // a value head's values enter the rows only through the advantage (reward - value,
+  // rl/__init__.py:239-248); its loss, statistics and dvalues are prl_grpo_stats' (out->dvalues is
+  // required as there but not written here)
   rc = fill_outputs(a, batch, params, out, false);
   if (rc) return rc;
   if (n < 0 || (n > 0 && !row_ids)) return PRL_E_INVALID;

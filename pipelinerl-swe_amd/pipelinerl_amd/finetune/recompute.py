@@ -121,12 +121,20 @@ def build_buffer_bytes(config, seq: int, chunk: int, shard_world: int, dtype_byt
         heads = int(getattr(config, "num_attention_heads", 1))
         kv = int(getattr(config, "num_key_value_heads", None) or heads) * (H // heads)
         out += (H + 2 * kv) * H * layers * dtype_bytes
-    # lm_head dW: bf16 from one GEMM (one chunk) or an fp32 accumulator (several chunks); an
-    # FSDP-sharded model takes the full-logits loss head (rl_step), its lm_head gradient is the
-    # root unit's unsharded gradient, counted in fsdp_transient_bytes
+    # lm_head dW: bf16 from one GEMM (one chunk) or an fp32 accumulator (several chunks); under
+    # FSDP the one-chunk dW becomes the root unit's unsharded lm_head gradient, counted in
+    # fsdp_transient_bytes
     if shard_world <= 1:
         out += vocab * H * (dtype_bytes if seq <= chunk else 4)
     return out
+
+
+def compute_bytes(model, param_bytes: int) -> int:
+    """Bytes per element of the tensors the model computes with: the parameters' own size, except
+    for a model sharded with fp32 master shards (finetune/sharding.py), whose gathered weights and
+    activations are in the loaded dtype (``_prl_save_dtype``, bf16)."""
+    dt = getattr(model, "_prl_save_dtype", None)
+    return min(param_bytes, torch.empty((), dtype=dt).element_size()) if dt is not None else param_bytes
 
 
 def fsdp_unit_bytes(model) -> tuple[int, int]:
@@ -134,8 +142,8 @@ def fsdp_unit_bytes(model) -> tuple[int, int]:
     model that will be wrapped): the root holds the embedding, lm_head and final norm."""
     from .sharding import decoder_layers
 
-    def nbytes(params) -> int:
-        return sum(p.numel() * p.element_size() for p in params)
+    def nbytes(params) -> int:  # unsharded, in the compute dtype (what an all-gather materialises)
+        return sum(p.numel() * compute_bytes(model, p.element_size()) for p in params)
 
     layers = decoder_layers(model)
     layer = max((nbytes(m.parameters()) for m in layers), default=0)
@@ -145,9 +153,10 @@ def fsdp_unit_bytes(model) -> tuple[int, int]:
 
 def fsdp_transient_bytes(model, shard_world: int, act: int, logits: int, head_grad: int) -> int:
     """FSDP2's unsharded working set beyond the activations (upper bound), the larger of its two
-    peaks in a step: (a) the start of the backward — every activation, the logits' gradient (the
-    full-logits loss head writes it beside the logits), the root unit gathered, the lm_head's
-    unsharded gradient and a decoder layer in use plus the next prefetched; (b) the root's
+    peaks in a step: (a) the start of the backward — every activation, the logits' gradient
+    (``logits``: the full-logits loss head writes it beside the logits; 0 for the label-row head,
+    which writes it in place), the root unit gathered, the lm_head's unsharded gradient and a
+    decoder layer in use plus the next prefetched; (b) the root's
     reduce-scatter at the end of the backward — the root gathered, its unsharded gradients and the
     reduce-scatter input FSDP copies them into (3 x the root).  Returned as that peak minus ``act``
     (the plan adds the activations itself).  0 when not sharded."""
@@ -165,7 +174,7 @@ def gathered_layer_bytes(model) -> int:
     from ..devalloc import round_size
     from .sharding import decoder_layers
 
-    return max((sum(round_size(p.numel() * p.element_size()) for p in m.parameters())
+    return max((sum(round_size(p.numel() * compute_bytes(model, p.element_size())) for p in m.parameters())
                 for m in decoder_layers(model)), default=0)
 
 
@@ -285,10 +294,12 @@ def _plan_recompute(args, model, device: torch.device, shard_world: int, device_
     # weight + gradient + exp_avg + exp_avg_sq in the parameter dtype, or with fp32 masters
     # (PrlAdamW master_weights / FSDP's fp32 shards) 16 B per parameter
     state = state_bytes_per_param(pbytes, master) * n // sw
+    pbytes = compute_bytes(model, pbytes)  # activations, logits and gathered weights: the compute dtype
     act = int(ACT_ALLOWANCE * int(seq) * activation_bytes_per_token(config, pbytes))
     vocab = int(getattr(config, "vocab_size", 0))
     rl = args.get("rl", None) or {}
     chunk = min(int(seq), int(rl.get("lm_head_chunk_rows", 65536) or 65536))  # RLConfig default
+    fused = bool(rl.get("fused_lm_head", True))  # the label-row head writes dlogits in place
     logits = chunk * vocab * pbytes
     head = 0 if getattr(config, "tie_word_embeddings", False) else vocab * int(config.hidden_size) * pbytes
     # the device allocator's size rounding (devalloc.py) at the largest shapes of the micro-batch
@@ -316,7 +327,7 @@ def _plan_recompute(args, model, device: torch.device, shard_world: int, device_
         a = act if keep >= L else keep * act_layer + 2 * act_layer
         a_bytes = int(a * f_act) + (0 if keep >= L else (L - keep) * saved_input)
         buffers = build_buffer_bytes(config, int(seq), chunk, int(shard_world), pbytes, flat) + \
-            fsdp_transient_bytes(model, int(shard_world), a, logits, head)
+            fsdp_transient_bytes(model, int(shard_world), a, 0 if fused else logits, head)
         need = int(state * f_state) + a_bytes + int(logits * f_logits) + \
             int(buffers * max(f_state, f_act, f_logits)) + int(HEADROOM_FRAC * total) + HEADROOM_BYTES
         return need, a_bytes, buffers

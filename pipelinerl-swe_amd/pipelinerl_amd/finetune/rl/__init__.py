@@ -150,12 +150,20 @@ def rl_step(model, batch: PipelineBatchEncoding, current_step: int, max_step: in
         model_inputs["image_grid_thw"] = batch.image_grid_thw
     if getattr(getattr(model, "config", None), "use_cache", None) is not None:
         model_inputs["use_cache"] = False  # training: no KV cache (HF would concatenate k / v per layer)
-    fused_head = config.fused_lm_head and _lm_head_of(model, has_value_head) is not None
+    fused_head = config.fused_lm_head and _lm_head_of(model) is not None
     bad_hidden = None
     if fused_head:
-        hidden = _decoder_of(model)(**model_inputs).last_hidden_state
+        from ..sharding import is_sharded
+
+        if has_value_head or is_sharded(model):
+            # through the root's own forward (FSDP gathers the root unit — embedding, final norm,
+            # lm_head — as it does for the reference's forward; a value head reads the last hidden
+            # state on every row), asking for no logits rows: the label-row head forms them below
+            hidden, values = _hidden_through_root(model, model_inputs, has_value_head)
+        else:
+            hidden = _decoder_of(model)(**model_inputs).last_hidden_state
+            values = None
         logits = hidden
-        values = None
         # The reference asserts every row's new log-probs finite (rl/__init__.py:209), prompt rows
         # included.  Label rows are checked by the kernel; a prompt row's logits h·Wᵀ are finite
         # when its hidden state is (W is finite, or every label row's log-softmax reports it),
@@ -177,8 +185,15 @@ def rl_step(model, batch: PipelineBatchEncoding, current_step: int, max_step: in
         grad_scale=float(grad_scale))
     fields = prepare_fields(batch, logits.device)
     if fused_head:
-        loss, stats_dev, _ = linear_grpo_loss(hidden, _lm_head_of(model, False).weight, fields, params,
-                                              config.lm_head_chunk_rows, getattr(batch, "_label_rows", None))
+        weight = _lm_head_of(model).weight  # (under FSDP: the root unit's gathered weight)
+        from torch.distributed.tensor import DTensor
+
+        if isinstance(weight, DTensor):
+            raise RuntimeError("fused_lm_head: the lm_head weight is still sharded after the root forward "
+                               "(the FSDP root must keep its unit gathered until the backward: "
+                               "finetune/sharding.py shard_model)")
+        loss, stats_dev, _ = linear_grpo_loss(hidden, weight, fields, params, config.lm_head_chunk_rows,
+                                              getattr(batch, "_label_rows", None), values)
     else:
         loss, stats_dev, _ = grpo_loss(logits, fields, params, values)
 
@@ -193,22 +208,41 @@ def _decoder_of(model):
     return dec
 
 
-def _lm_head_of(model, has_value_head: bool):
-    """The plain bias-free lm_head Linear, or None (with a one-time warning) when the model
-    does something else between the decoder and the logits."""
-    head = model.get_output_embeddings() if hasattr(model, "get_output_embeddings") else None
-    from ..sharding import is_sharded
-
-    ok = (isinstance(head, torch.nn.Linear) and head.bias is None and not has_value_head
-          and getattr(getattr(model, "config", None), "final_logit_softcapping", None) is None
-          and not is_sharded(model))  # FSDP: the root's hooks gather lm_head / embeddings
+def _lm_head_of(model):
+    """The language model's plain bias-free lm_head Linear (under a value-head wrapper: its
+    ``pretrained_model``'s), or None (with a one-time warning) when the model does something else
+    between the decoder and the logits."""
+    lm = getattr(model, "pretrained_model", model)
+    head = lm.get_output_embeddings() if hasattr(lm, "get_output_embeddings") else None
+    ok = (isinstance(head, torch.nn.Linear) and head.bias is None
+          and getattr(getattr(lm, "config", None), "final_logit_softcapping", None) is None)
     if not ok:
         if not _warned.get("fused_lm_head"):
             _warned["fused_lm_head"] = True
-            logger.warning("fused_lm_head: model has no plain bias-free lm_head (or has a value head, or "
-                           "is FSDP-sharded); using the full-logits loss head")
+            logger.warning("fused_lm_head: model has no plain bias-free lm_head; using the full-logits loss head")
         return None
     return head
+
+
+def _hidden_through_root(model, model_inputs: dict, has_value_head: bool):
+    """(last hidden state [B, L, H], values [B, L] or None) from ``model``'s own forward with no
+    logits rows (``logits_to_keep=slice(0, 0)``): the decoder's output is caught by a forward hook.
+    Under FSDP the root's pre-forward hook all-gathers the root unit (the embedding, the final norm,
+    the lm_head) and keeps it gathered to the backward; a value-head wrapper (value_model.py) computes
+    its values from the same hidden state (the reference: value_model.py:99-107)."""
+    lm = getattr(model, "pretrained_model", model)
+    dec = _decoder_of(lm)
+    box: dict[str, torch.Tensor] = {}
+
+    def keep(mod, args, out):
+        box["h"] = out.last_hidden_state if hasattr(out, "last_hidden_state") else out[0]
+
+    hook = dec.register_forward_hook(keep)
+    try:
+        out = model(**model_inputs, logits_to_keep=slice(0, 0))
+    finally:
+        hook.remove()
+    return box["h"], (out.value if has_value_head else None)
 
 
 def build_stats(h: np.ndarray, batch, params: GrpoParams, kl_c: float, ent_c: float, num_sequences: int,

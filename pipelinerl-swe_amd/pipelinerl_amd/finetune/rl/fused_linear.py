@@ -31,7 +31,7 @@ import torch
 
 from ... import _native, gemm
 from ..._native import NSTAT, PRL_BF16, PRL_F32
-from .fused import GrpoParams, _relative, _workspace
+from .fused import GrpoParams, _ptr, _relative, _workspace
 
 _ADDMM_F32: dict[str, bool] = {}
 # Parity-test tap (tests/test_configs_gpu.py): when set, called as tap(stage, q_rows, chunk, rows)
@@ -54,12 +54,13 @@ def _accumulate_dw(dw: torch.Tensor, dlg: torch.Tensor, hc: torch.Tensor) -> Non
     dw.add_(torch.mm(dlg.t(), hc).float())
 
 
-def _c_batch(ptr: int, dtype: torch.dtype, B: int, L: int, V: int, ld: int, f: dict) -> _native.PrlGrpoBatch:
+def _c_batch(ptr: int, dtype: torch.dtype, B: int, L: int, V: int, ld: int, f: dict,
+             values: torch.Tensor | None = None) -> _native.PrlGrpoBatch:
     return _native.PrlGrpoBatch(
         ptr, PRL_BF16 if dtype == torch.bfloat16 else PRL_F32, 0, B, L, V, ld,
         f["input_ids"].data_ptr(), f["labels"].data_ptr(), f["rewards"].data_ptr(), f["advantages"].data_ptr(),
         f["ref_logprobs"].data_ptr(), f["old_logprobs"].data_ptr(), f["group_tokens"].data_ptr(),
-        f["num_labels"].data_ptr(), f["overflow"].data_ptr(), None)
+        f["num_labels"].data_ptr(), f["overflow"].data_ptr(), _ptr(values))
 
 
 def _weight_grad(dw: torch.Tensor, g: torch.Tensor, param, w_dtype):
@@ -88,7 +89,7 @@ def _weight_grad(dw: torch.Tensor, g: torch.Tensor, param, w_dtype):
 
 class LinearGrpoLossFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, hidden, weight, fields, params: GrpoParams, chunk_rows: int, label_rows=None):
+    def forward(ctx, hidden, weight, fields, params: GrpoParams, chunk_rows: int, label_rows=None, values=None):
         if hidden.device.type != "cuda":
             raise RuntimeError("the fused lm_head + GRPO loss runs on a HIP device only (no CPU fallback)")
         if hidden.dim() != 3 or weight.dim() != 2 or hidden.shape[-1] != weight.shape[1]:
@@ -111,6 +112,15 @@ class LinearGrpoLossFn(torch.autograd.Function):
         dw = None
         stream = torch.cuda.current_stream(dev).cuda_stream
         cp = params.to_c(write_grad)
+        # a value head (values [B, L], every row): the rows read them for the advantage
+        # (reward - value); the value loss, its statistics and dvalues come from the statistics
+        # pass (rl/__init__.py:239-248, :294-310)
+        vals = dvalues = None
+        if values is not None:
+            if tuple(values.shape) != (B, L):
+                raise ValueError(f"values must be [B, L] = {(B, L)}, got {tuple(values.shape)}")
+            vals = values.detach().to(torch.float32).contiguous()
+            dvalues = torch.empty((B, L), dtype=torch.float32, device=dev)
         if Q > 0:
             if label_rows is not None and label_rows.device == dev:  # counted on the host by the loader
                 qsel = label_rows
@@ -134,8 +144,8 @@ class LinearGrpoLossFn(torch.autograd.Function):
                 # [c, V] contiguous
                 lg = gemm.linear_fwd(hc, w) if use_prl and gemm.solution_for("fwd", hc.shape[0], V, Hd) is not None \
                     else torch.mm(hc, w.t())
-                cb = _c_batch(lg.data_ptr(), lg.dtype, B, L, V, V, fields)
-                co = _native.PrlGrpoOutputs(*[rows[i].data_ptr() for i in range(8)], None,
+                cb = _c_batch(lg.data_ptr(), lg.dtype, B, L, V, V, fields, vals)
+                co = _native.PrlGrpoOutputs(*[rows[i].data_ptr() for i in range(8)], _ptr(dvalues),
                                             lg.data_ptr() if write_grad else None, None)
                 if ROW_TAP is not None:
                     ROW_TAP("logits", qc, lg, rows)
@@ -154,16 +164,17 @@ class LinearGrpoLossFn(torch.autograd.Function):
                     dh.index_copy_(0, idx, torch.mm(lg, w))
                     _accumulate_dw(dw, lg, hc)
                 del lg, hc
-        cb = _c_batch(0, w.dtype, B, L, V, V, fields)
-        co = _native.PrlGrpoOutputs(*[rows[i].data_ptr() for i in range(8)], None, None, stats.data_ptr())
+        cb = _c_batch(0, w.dtype, B, L, V, V, fields, vals)
+        co = _native.PrlGrpoOutputs(*[rows[i].data_ptr() for i in range(8)], _ptr(dvalues), None, stats.data_ptr())
         ws = _workspace(dev)
         _native.check(lib.prl_grpo_stats(ctypes.byref(cb), ctypes.byref(cp), ctypes.byref(co), ws.data_ptr(),
                                          ws.numel(), stream), "prl_grpo_stats")
-        loss = (-stats[0]).to(torch.float32)
+        loss = (-stats[0] + params.value_loss_coef * stats[1]).to(torch.float32) if values is not None \
+            else (-stats[0]).to(torch.float32)
         ctx.mark_non_differentiable(stats, rows)
         if write_grad and dw is None:  # no label rows: zero weight gradient
             dw = torch.zeros((V, Hd), dtype=torch.float32, device=dev)
-        ctx.dh, ctx.dw = dh, dw
+        ctx.dh, ctx.dw, ctx.dvalues = dh, dw, dvalues
         ctx.param = weight  # the Parameter (its .grad: fused accumulation, _weight_grad)
         ctx.shape = (B, L, Hd)
         ctx.h_dtype, ctx.w_dtype = hidden.dtype, weight.dtype
@@ -172,22 +183,26 @@ class LinearGrpoLossFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g_loss, g_stats, g_rows):
-        d_hidden = d_weight = None
-        if g_loss is not None and ctx.dh is not None:
+        d_hidden = d_weight = d_values = None
+        if g_loss is not None:
             g = _relative(g_loss.detach().to(torch.float32), ctx.grad_scale)  # dh / dW formed at grad_scale
-            if ctx.needs_input_grad[0]:
+            if ctx.dh is not None and ctx.needs_input_grad[0]:
                 d_hidden = (ctx.dh.view(ctx.shape) * g.to(ctx.dh.dtype)).to(ctx.h_dtype)
-            if ctx.needs_input_grad[1]:
+            if ctx.dh is not None and ctx.needs_input_grad[1]:
                 d_weight = _weight_grad(ctx.dw, g, ctx.param, ctx.w_dtype)
-        ctx.dh = ctx.dw = None
-        return d_hidden, d_weight, None, None, None, None
+            if ctx.dvalues is not None and ctx.needs_input_grad[6]:
+                d_values = ctx.dvalues * g
+        ctx.dh = ctx.dw = ctx.dvalues = None
+        return d_hidden, d_weight, None, None, None, None, d_values
 
 
 def linear_grpo_loss(hidden: torch.Tensor, weight: torch.Tensor, fields: dict, params: GrpoParams,
-                     chunk_rows: int = 65536, label_rows: torch.Tensor | None = None):
+                     chunk_rows: int = 65536, label_rows: torch.Tensor | None = None,
+                     values: torch.Tensor | None = None):
     """(loss, stats [NSTAT] f64 device, rows [8, B*(L-1)]) of lm_head(hidden) -> GRPO loss head,
     scoring only the label rows.  ``weight``: the lm_head weight [V, H] (no bias).
     ``label_rows``: the rows q = b*(L-1)+t with a label (int64, on the device), if the caller
     counted them on the host (the trainer's loader does); else they are found on the device and
-    their count read back."""
-    return LinearGrpoLossFn.apply(hidden, weight, fields, params, chunk_rows, label_rows)
+    their count read back.  ``values``: a value head's output [B, L] (every row; the loss then adds
+    ``value_loss_coef`` x the value loss and d loss / d values flows back into the head)."""
+    return LinearGrpoLossFn.apply(hidden, weight, fields, params, chunk_rows, label_rows, values)

@@ -173,7 +173,10 @@ def shard_model(model, fsdp_cfg=None, grad_reduce: str = "mean", reshard_after_f
             for name, p in list(mod.named_parameters(recurse=False)):
                 if p.dtype == load and not _is_dtensor(p):
                     p.data = p.data.to(torch.float32)
-    fully_shard(model, mesh=mesh, mp_policy=mp, reshard_after_forward=reshard_after_forward)
+    # the root unit (embedding, final norm, lm_head) stays gathered from its forward to its backward:
+    # the label-row lm_head + loss (finetune/rl/fused_linear.py) runs after the root forward on the
+    # gathered lm_head weight (the backward needs the unit gathered at once anyway)
+    fully_shard(model, mesh=mesh, mp_policy=mp, reshard_after_forward=False)
     if master:
         model._prl_save_dtype = load  # checkpoints keep the loaded dtype (finetune/checkpoints.py)
     for m in [*layers, model]:

@@ -8,10 +8,12 @@ parameters after the forward and gathers them again for the backward.  Each rank
 4 096-token micro-batch (4 rollouts x 1 024, 128-token prompts) through rl_step with the KL term on
 (kl_coef 0.001, ref = old + N(0, 0.05²) on the label tokens).
 
-  1. gradients: the sharded (reduce-scattered, mean over the ranks) gradient of every parameter
-     equals one unsharded model's gradient of the mean of both ranks' losses, per tensor within
-     the bf16 GEMM bar (relative norm 2e-2; the unsharded side runs the label-row lm_head, the
-     sharded side the full-logits loss head).  Each rank compares its own shards with the matching
+  1. gradients: the sharded (reduce-scattered in fp32, mean over the ranks) gradient of every
+     parameter equals one unsharded model's gradient of the mean of both ranks' losses, per tensor
+     within the bf16 GEMM bar (relative norm 2e-2).  Both sides run the label-row lm_head + loss
+     (finetune/rl/fused_linear.py); the sharded side through the FSDP root's own forward, on the
+     root unit's gathered lm_head weight (asserted: every step took that path).  The shards are the
+     fp32 masters of the reference's FSDP mixed precision (finetune/sharding.py master_weights).  Each rank compares its own shards with the matching
      rows of the unsharded gradient (which every rank computes), the test sums the parts: no
      DTensor.full_tensor() gathers (gloo runs those at ~20 MB/s);
   2. weight update: after the optimizer steps, rank 0's WeightUpdateManager snapshot (one FSDP
@@ -91,8 +93,14 @@ def _run(rank: int, port: int, tmp: str):
     # cannot span two ranks on one GPU
     dist.init_process_group("cpu:gloo,cuda:gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=2)
     out: dict = {}
-    model = shard_model(qwen2_model("32b", dev, layers=LAYERS))
-    opt = get_optimizer("adamw_torch", model, 1e-6, 0.01)
+    model = shard_model(qwen2_model("32b", dev, layers=LAYERS), master_weights=True)
+    assert {p.dtype for p in model.parameters()} == {torch.float32}  # the fp32 master shards
+    opt = get_optimizer("adamw_torch", model, 1e-6, 0.01, master_weights=True)
+    from pipelinerl_amd.finetune import rl as rlmod
+
+    fused_calls = []
+    orig_linear = rlmod.linear_grpo_loss
+    rlmod.linear_grpo_loss = lambda *a, **k: (fused_calls.append(1), orig_linear(*a, **k))[1]
     batch = _batch(rank)
     _say(rank, t0, "sharded model built")
 
@@ -126,6 +134,8 @@ def _run(rank: int, port: int, tmp: str):
             "rl": {"lm_head_chunk_rows": 65536}}
     plan = plan_gradient_checkpointing(args, model, dev, shard_world=2)
     out["plan"] = plan.as_dict()
+    rlmod.linear_grpo_loss = orig_linear
+    out["fused_calls"] = len(fused_calls)  # both steps through the label-row head
     out["estimate_bytes"] = plan.state_bytes + plan.activation_bytes + plan.logits_bytes + plan.buffer_bytes
 
     # ---- weight update: rank 0 trains and sends, rank 1 also holds the actor --------------------
@@ -233,6 +243,7 @@ def test_c5_32b_shapes_fsdp_grads_snapshot_and_memory_plan(tmp_path):
     mem = {f"rank{i}": (x["peak_bytes"] / 1e9, x["estimate_bytes"] / 1e9) for i, x in enumerate(r)}
     print(json.dumps({"worst_grad_rel_err": worst, "tensors": len(errs), "peak_vs_estimate_gb": mem,
                       "plan": r[1]["plan"], "actor_tensors_equal": equal}))
+    assert [x["fused_calls"] for x in r] == [2, 2]  # the sharded steps took the label-row head
     assert len(errs) == 3 + LAYERS * 12, len(errs)  # embed, norm, lm_head + 12 per decoder layer
     assert numel["lm_head.weight"] == 152064 * 5120 and numel["model.layers.0.mlp.gate_proj.weight"] == 27648 * 5120
     assert worst[0][1] <= GRAD_REL, worst

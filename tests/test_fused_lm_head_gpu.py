@@ -174,3 +174,104 @@ def test_fp32_label_rows_at_qwen_vocab():
     assert ok, err
     ok, err = rel_close(dw.cpu().numpy(), dw_o, 1e-4, 1e-5 * float(np.abs(dw_o).max()))
     assert ok, err
+
+
+class _Decoder(torch.nn.Module):
+    """Decoder stub: its last hidden state is a fixed tensor (a parameter, so its gradient is read)."""
+
+    def __init__(self, h: torch.Tensor):
+        super().__init__()
+        self.h = torch.nn.Parameter(h)
+
+    def forward(self, **kw):
+        import types
+
+        return types.SimpleNamespace(last_hidden_state=self.h)
+
+
+class _IdentityHeadLM(torch.nn.Module):
+    """A causal LM whose lm_head is the identity [V, V]: its logits ARE the hidden states, so a
+    reference batch's logits can be fed through the label-row lm_head path unchanged (fp32 GEMM
+    with an identity weight is exact)."""
+
+    def __init__(self, logits: torch.Tensor):
+        super().__init__()
+        import types
+
+        V = logits.shape[-1]
+        self.model = _Decoder(logits)
+        self.lm_head = torch.nn.Linear(V, V, bias=False, device=logits.device)
+        with torch.no_grad():
+            self.lm_head.weight.copy_(torch.eye(V, device=logits.device))
+        self.config = types.SimpleNamespace()
+
+    def get_decoder(self):
+        return self.model
+
+    def get_output_embeddings(self):
+        return self.lm_head
+
+    def forward(self, logits_to_keep=0, output_hidden_states=False, **kw):
+        import types
+
+        h = self.model(**kw).last_hidden_state
+        idx = slice(-logits_to_keep, None) if isinstance(logits_to_keep, int) else logits_to_keep
+        return types.SimpleNamespace(logits=self.lm_head(h[:, idx, :]), hidden_states=(h,))
+
+
+class _ValueHeadWrapper(torch.nn.Module):
+    """value_model.py's AutoModelForCausalLMWithValueHead shape: ``pretrained_model`` + a value
+    head; the values are a parameter here (the reference batch's own), their gradient read back."""
+
+    def __init__(self, lm, values: torch.Tensor):
+        super().__init__()
+        self.pretrained_model = lm
+        self.value_head = torch.nn.Parameter(values)
+
+    def forward(self, **kw):
+        import types
+
+        out = self.pretrained_model(output_hidden_states=True, **kw)
+        return types.SimpleNamespace(logits=out.logits, value=self.value_head)
+
+
+def test_f1_value_head_cases_through_the_label_row_head():
+    """The reference's default fine-tune config is actor_critic (a value head, conf/base.yaml:2):
+    every F1 value-head case (generated by the reference's own rl_step, value_loss_coef 0.1) through
+    rl_step's label-row lm_head path — the root forward with no logits rows, the value head on every
+    row, lm_head + loss over the label rows, statistics and dvalues from the statistics pass —
+    against the reference's outputs at the fp32 bar: loss, every statistic, d loss / d values, and
+    d loss / d hidden (= the reference's dlogits through the identity lm_head)."""
+    from conftest import load_f1
+    from pipelinerl_amd.finetune import rl as rlmod
+    from pipelinerl_amd.finetune.rl import RLConfig, rl_step
+
+    batches, out, cases = load_f1()
+    calls = []
+    orig = rlmod.linear_grpo_loss
+    rlmod.linear_grpo_loss = lambda *a, **k: (calls.append(1), orig(*a, **k))[1]
+    n = 0
+    try:
+        for i, c in enumerate(cases):
+            if not c["value_head"]:
+                continue
+            b = batches[c["batch"]]
+            logits = torch.tensor(b["logits"], dtype=torch.float32, device=DEV)
+            model = _ValueHeadWrapper(_IdentityHeadLM(logits), torch.tensor(b["values"], device=DEV))
+            loss, stats = rl_step(model, to_batch(b), c["step"], c["max_step"],
+                                  RLConfig(**c["cfg"], fused_lm_head=True, lm_head_chunk_rows=7))
+            loss.backward()
+            torch.cuda.synchronize()
+            assert abs(float(loss) - c["loss"]) <= 1e-4 * max(1, abs(c["loss"])), (i, float(loss), c["loss"])
+            assert set(stats) == set(c["stats"]), (i, set(stats) ^ set(c["stats"]))
+            for k, v in c["stats"].items():
+                assert abs(stats[k] - v) <= 1e-4 * max(1.0, abs(v)), (i, k, stats[k], v)
+            ok, err = rel_close(model.value_head.grad.cpu().numpy(), out[f"case{i}__dvalues"], 1e-4, 1e-7)
+            assert ok, (i, "dvalues", err)
+            ok, err = rel_close(model.pretrained_model.model.h.grad.cpu().numpy(), out[f"case{i}__dlogits"], 1e-4,
+                                1e-6)
+            assert ok, (i, "dhidden", err)
+            n += 1
+    finally:
+        rlmod.linear_grpo_loss = orig
+    assert n == 17 and len(calls) == n  # every value-head case took the label-row path

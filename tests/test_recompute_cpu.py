@@ -144,8 +144,12 @@ def test_build_buffers_are_counted(m7b, monkeypatch):
     root = (2 * 152064 * 5120 + 5120) * 2
     layer = (2 * 5120 * 5120 + 2 * 1024 * 5120 + 3 * 27648 * 5120 + 5120 + 2 * 1024 + 2 * 5120) * 2
     head = 152064 * 5120 * 2
-    start = p32.logits_bytes + root + head + 2 * layer  # beyond the activations
+    start = root + head + 2 * layer  # beyond the activations (the label-row head: dlogits in place)
     assert p32.buffer_bytes == max(start, 3 * root - p32.activation_bytes) and not p32.checkpoint, p32.as_dict()
+    # the full-logits loss head (rl.fused_lm_head false) also holds the logits' gradient
+    pf = plan_gradient_checkpointing(_args(seq_length=4096, rl={"fused_lm_head": False}), m32, cuda, shard_world=4,
+                                     device_bytes=288 * GB)
+    assert pf.buffer_bytes == max(pf.logits_bytes + start, 3 * root - pf.activation_bytes), pf.as_dict()
 
 
 def test_plan_counts_the_allocator_rounding(m7b, monkeypatch):
