@@ -466,7 +466,10 @@ def main():
         if rehearse:  # gloo for CUDA tensors too (FSDP's device mesh would open RCCL groups)
             dist.init_process_group("cpu:gloo,cuda:gloo")
         else:
-            dist.init_process_group("nccl", device_id=dev)
+            from pipelinerl_amd.torch_utils import collective_options
+
+            # the trainer's DP group (finetune_loop.Dist): collectives on high-priority streams
+            dist.init_process_group("nccl", device_id=dev, pg_options=collective_options("nccl"))
 
     from pipelinerl_amd import _native
     from pipelinerl_amd.finetune.rl.fused import GrpoParams, grpo_loss

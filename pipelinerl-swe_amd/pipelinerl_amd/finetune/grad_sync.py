@@ -61,7 +61,10 @@ class GradBuckets:
         self.armed = False
         dev = params[0].device if params else torch.device("cpu")
         self.on_gpu = dev.type == "cuda"
-        self.stream = torch.cuda.Stream(device=dev) if self.on_gpu else None
+        # high priority: a hardware queue of its own — a normal-priority stream created here shares the
+        # compute stream's queue (GPU_MAX_HW_QUEUES 4; measured, profiles/r06_queue_probe.json), and the
+        # collectives it orders would wait behind the backward's kernels (tools/queue_probe.py)
+        self.stream = torch.cuda.Stream(device=dev, priority=-1) if self.on_gpu else None
         self._avg = self.on_gpu and dist.get_backend(group) == "nccl" and reduce == "mean"
         self._hooks = [p.register_post_accumulate_grad_hook(self._hook) for p in params]
         for p in params:  # model_ops._wgrad may add into .grad in the GEMM while not armed (no hook due)

@@ -64,7 +64,9 @@ logger = logging.getLogger(__name__)
 class Dist:
     """rank / world / device + the CPU control group used for lockstep bookkeeping."""
 
-    def __init__(self, backend: str | None = None):
+    def __init__(self, backend: str | None = None, high_priority_collectives: bool = True):
+        """``high_priority_collectives``: the RCCL data-parallel group runs its collectives on
+        high-priority streams (torch_utils.collective_options), off the compute stream's queue."""
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -72,9 +74,13 @@ class Dist:
         self.device = torch.device("cuda", self.local_rank) if use_gpu else torch.device("cpu")
         if use_gpu:
             torch.cuda.set_device(self.device)
+        self.pg_options = None
         if not dist.is_initialized() and (self.world > 1 or "MASTER_ADDR" in os.environ):
-            dist.init_process_group(backend or ("nccl" if use_gpu else "gloo"),
-                                    device_id=self.device if use_gpu else None)
+            from .torch_utils import collective_options
+
+            be = backend or ("nccl" if use_gpu else "gloo")
+            self.pg_options = collective_options(be, high_priority_collectives)
+            dist.init_process_group(be, device_id=self.device if use_gpu else None, pg_options=self.pg_options)
         self.initialized = dist.is_initialized()
         if self.initialized:
             self.world = dist.get_world_size()
@@ -183,7 +189,8 @@ def run_finetuning_loop(cfg, step_fn: Callable = rl_step, model=None, tokenizer=
     """Trainer process main (finetune_loop.py:290-486).  ``step_fn``/``model`` are injectable
     for tests; production uses rl_step and the HF model named by cfg.finetune.config_name."""
     set_streams_backend(**cfg.streams)
-    ctx = Dist(cfg.finetune.get("dist_backend"))
+    high_prio = str(cfg.finetune.get("collective_stream_priority", "high")) == "high"
+    ctx = Dist(cfg.finetune.get("dist_backend"), high_prio)
     args = cfg.finetune if "finetune" in cfg else cfg
     grad_mode = grad_scale_convention(cfg)
     if args.gradient_accumulation_passes % ctx.world:
@@ -256,9 +263,11 @@ def run_finetuning_loop(cfg, step_fn: Callable = rl_step, model=None, tokenizer=
             actor_group = RcclComm.create(cfg.me.weight_update_group_init_method, 0,
                                           cfg.me.weight_update_group_world_size, ctx.device)
         else:
+            from .torch_utils import collective_options
+
             actor_group = init_extra_process_group(
                 group_name="actor", backend=backend, init_method=cfg.me.weight_update_group_init_method, rank=0,
-                world_size=cfg.me.weight_update_group_world_size)
+                world_size=cfg.me.weight_update_group_world_size, pg_options=collective_options(backend, high_prio))
     ctx.barrier()
 
     metrics = TrainingMetrics()

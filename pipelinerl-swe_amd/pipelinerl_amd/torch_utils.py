@@ -22,6 +22,21 @@ import torch
 import torch.distributed.distributed_c10d as c10d
 
 
+def collective_options(backend: str | None, high_priority: bool = True):
+    """``pg_options`` for an RCCL ("nccl") group: its collectives run on high-priority HIP streams
+    (ProcessGroupNCCL.Options.is_high_priority_stream).  The HIP runtime gives high-priority streams
+    hardware queues of their own (tools/queue_probe.py, profiles/r06_queue_probe.json): a collective
+    then never waits in the compute stream's queue behind the trainer's kernels, which run in order
+    within one queue — with GPU_MAX_HW_QUEUES at its default 4 the normal-priority streams of a rank
+    (compute, GradBuckets', the weight update's, the process groups' own) otherwise share four
+    queues.  None for other backends (gloo runs on host threads)."""
+    if not high_priority or "nccl" not in str(backend or "").lower():
+        return None
+    import torch.distributed as dist
+
+    return dist.ProcessGroupNCCL.Options(is_high_priority_stream=True)
+
+
 def init_extra_process_group(backend: str | None = None, init_method: str | None = None,
                              timeout: timedelta | None = None, world_size: int = -1, rank: int = -1,
                              store: Any = None, group_name: str | None = None, pg_options: Any = None,

@@ -679,8 +679,11 @@ def split_pipeline_probe(actors: int, steps: int = 2, warmup: int = 1, device=No
     n_tr = world - actors
     trainer_ranks = list(range(n_tr))
     # every rank creates every group, in the same order (torch.distributed requirement)
-    dp_group = dist.new_group(trainer_ranks)
-    bc_group = dist.new_group([0] + list(range(n_tr, world)))
+    from .torch_utils import collective_options
+
+    opts = collective_options(dist.get_backend())  # as the trainer creates its DP and actor groups
+    dp_group = dist.new_group(trainer_ranks, pg_options=opts)
+    bc_group = dist.new_group([0] + list(range(n_tr, world)), pg_options=opts)
     is_trainer = rank < n_tr
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
     from .comm_probe import group_census

@@ -399,12 +399,16 @@ class WeightUpdateManager:
 
     def before_optimizer_step(self) -> None:
         """Order the next in-place parameter update after the snapshot: after the staging copy, or
-        (zero-copy) after the broadcast's last read of the parameters.  The zero-copy wait is
-        bounded: the host polls the broadcast's completion (its event on a device, the works of a
-        gloo group) between checks of the watcher's error and the update's deadline, and raises
-        WeightUpdateError instead of blocking past ``timeout_s`` on an actor that never receives.
-        The broadcast started one step earlier, so it is normally complete at the first check; the
-        device-side event wait then orders the optimizer's writes after its reads."""
+        (zero-copy) after the broadcast's last read of the parameters.  On a torch group the
+        zero-copy wait is bounded: the host polls the broadcast's completion (its event on a device,
+        the works of a gloo group) every <= 1 ms between checks of the watcher's error and the
+        update's deadline, and raises WeightUpdateError instead of blocking past ``timeout_s`` on an
+        actor that never receives.  The broadcast started one step earlier, so it is normally
+        complete at the first check and the host goes on at once; the device-side event wait then
+        orders the optimizer's writes after its reads.  On an RcclComm group the broadcasts are
+        stream-ordered with no host handle: the device-side wait alone orders the writes, and the
+        watcher thread bounds it — a failed or timed-out update aborts the communicator
+        (``finish`` below), which ends the in-flight broadcast kernels and so the wait."""
         ev = getattr(self, "_snapshot_done", None)
         self._snapshot_done = None
         works, self._works = self._works, []
@@ -422,7 +426,7 @@ class WeightUpdateManager:
         return isinstance(self.group, comm.RcclComm) or "nccl" in str(_backend_of(self.group))
 
     def _await_reads(self, done: Callable[[], bool]) -> None:
-        delay = 0.0005
+        delay = 0.0002
         while not done():
             self._raise()  # the watcher's error (an actor's HTTP error, its own timeout)
             if self._deadline is not None and time.time() > self._deadline:
@@ -430,7 +434,7 @@ class WeightUpdateManager:
                                         f"{self.timeout_s:.0f} s after its request: the next optimizer step "
                                         "cannot write them (an actor is not receiving)")
             time.sleep(delay)
-            delay = min(delay * 2, 0.02)
+            delay = min(delay * 2, 0.001)  # at most 1 ms late after the broadcast's last read
 
     def wait(self) -> None:
         """Block until the in-flight update (if any) has been received by every actor."""
@@ -457,13 +461,13 @@ class WeightUpdateManager:
 
 
 def side_stream_priority() -> int:
-    """Priority of the broadcast's side stream (torch: lower is higher).  PRL_WU_STREAM_PRIORITY=high
-    puts it on a high-priority HIP stream, which the runtime maps to hardware queues of its own (a
-    normal-priority stream may share a hardware queue with the trainer's compute stream, and kernels
-    in one hardware queue run in order)."""
+    """Priority of the broadcast's side stream (torch: lower is higher): high, so the runtime maps it
+    to a hardware queue of its own (a normal-priority stream may share a hardware queue with the
+    trainer's compute stream, and kernels in one hardware queue run in order;
+    tools/queue_probe.py).  PRL_WU_STREAM_PRIORITY=normal: a pool stream (A/B)."""
     import os
 
-    return -1 if os.environ.get("PRL_WU_STREAM_PRIORITY", "normal") == "high" else 0
+    return 0 if os.environ.get("PRL_WU_STREAM_PRIORITY", "high") == "normal" else -1
 
 
 def flat_home(named, layout: FlatLayout) -> torch.Tensor | None:
