@@ -33,7 +33,11 @@ micro-batches per rank, with the full bucketed 15.23 GB gradient all-reduce at N
 step without the all-reduce, the DP step and the all-reduce alone, its exposed share and overlap,
 and the tokens/s extrapolated to C3's 4096-sample step (one all-reduce per ~hundreds of
 micro-batches).  trainer_step at N > 1 likewise times the replica alone first: dp_efficiency is
-the trainer-step scaling fraction at this N.
+the trainer-step scaling fraction at this N.  At N = 1, c3_dp also times the step with an emulated
+ring all-reduce of the gradients (trainer_probe.EmulatedRingBuckets: the reads a ring over N = 4 / 8
+GPUs makes on each, paced to xGMI link rates, launched from the boundary backward's hooks) and
+projects C3's DP efficiency at that N (dp_scaling.c3_projected_efficiency); "c3_dp_value_head" is
+the same step with a value head (the reference's default actor_critic config).
 
 At N > 1, last, BASELINE.json configs[3] (C4) is measured under "split_pipeline": ranks
 [0, N/2) train Qwen2.5-7B shapes data-parallel while ranks [N/2, N) act as actors; trainer rank 0
@@ -262,6 +266,16 @@ def dp_scaling(world: int, c3: dict | None, trainer: dict | None) -> dict | None
     if ex.get("allreduce_share") is not None:
         out["c3_extrapolated_efficiency"] = round(1.0 - ex["allreduce_share"], 5)
         out["c3_extrapolated_tokens_per_s"] = round(ex["tokens_per_s_per_gpu"] * world, 1)
+    emu = c3.get("allreduce_emulated")
+    if emu:
+        # N = 1 bound on the scaling claim: the emulated ring all-reduce's exposed time per arm, and
+        # C3's efficiency at that arm's N projected from it and the lockstep protocol's model
+        out["allreduce_exposed_ms_emulated"] = {k: v["exposed_ms"] for k, v in emu.items()}
+        out["c3_projected_efficiency"] = {k: v["projection"]["projected_efficiency"] for k, v in emu.items()
+                                          if "projection" in v}
+        out["c3_projected_efficiency_basis"] = (
+            "lockstep model (workloads.LOCKSTEP_EFFICIENCY, the loop's order on C3's packing) x (1 - emulated "
+            "all-reduce exposed ms / C3's 4096-sample step); arms: ranks, xGMI GB/s, channel workgroups in c3_dp")
     if trainer and trainer.get("dp_efficiency") is not None:
         out["trainer_step_1.5b_efficiency"] = trainer["dp_efficiency"]
     return out
@@ -583,10 +597,21 @@ def main():
         # bucketed 15.23 GB gradient all-reduce at N > 1 (local / DP / all-reduce-alone timings);
         # at N = 1 also the same step with the weight-update snapshot (staging copy / in place) in
         # flight (at N > 1 the split_pipeline probe prices the whole broadcast with real actors)
+        from pipelinerl_amd.trainer_probe import RING_ARMS, dp_step_probe
+
+        # at N = 1 also the same step with emulated ring all-reduces of the gradients (N = 4 / 8 at one
+        # xGMI link's rate, N = 8 over seven) launched from the boundary backward's hooks
+        c3 = optional("c3_dp", lambda: dp_step_probe("c3", micro_batches=4, steps=2, warmup=1, device=dev,
+                                                      layers=4 if rehearse else None, snapshot=world == 1,
+                                                      emulate=RING_ARMS if world == 1 else None))
+    c3_vh = None
+    if world == 1 and not args.no_c3:
+        # the reference's default fine-tune config is actor_critic (conf/base.yaml:2): the same C3 step
+        # with a value head, through the label-row lm_head as the GRPO step
         from pipelinerl_amd.trainer_probe import dp_step_probe
 
-        c3 = optional("c3_dp", lambda: dp_step_probe("c3", micro_batches=4, steps=2, warmup=1, device=dev,
-                                                      layers=4 if rehearse else None, snapshot=world == 1))
+        c3_vh = optional("c3_dp_value_head", lambda: dp_step_probe("c3", micro_batches=4, steps=2, warmup=1,
+                                                                    device=dev, value_head=True))
     trainer = None
     if not args.no_trainer_step:
         # the whole optimizer step the loss head sits in
@@ -711,7 +736,12 @@ def main():
             # the trainer-side half of "weight broadcast fully overlapped": C3's 7B step with and
             # without WeightUpdateManager's snapshot in flight on its side stream
             out["snapshot_overlap"] = dict(c3.pop("snapshot_overlap"), step="c3_dp (Qwen2.5-7B, 4 micro-batches)")
-        for key, res in (("communicators", census), ("c3_dp", c3), ("trainer_step", trainer),
+        if isinstance(c3_vh, dict):  # beside the GRPO step: its rate, step time and roofline only
+            c3_vh = {k: c3_vh[k] for k in ("config", "value_head", "ms_per_step_local", "tokens_per_s_per_gpu",
+                                           "optimizer_tail_ms", "peak_mem_gb", "roofline", "extrapolated")
+                     if k in c3_vh}
+        for key, res in (("communicators", census), ("c3_dp", c3), ("c3_dp_value_head", c3_vh),
+                         ("trainer_step", trainer),
                          ("loss_head_fp32", fp32), ("fsdp_32b", fsdp),
                          ("split_pipeline", split), ("exchange", comm), ("fsdp_32b_kept_gathered", fsdp_kept)):
             if res is not None:

@@ -32,11 +32,14 @@ class _Bucket:
 
 
 class GradBuckets:
-    def __init__(self, params, group=None, bucket_bytes: int = 256 << 20, reduce: str = "mean"):
+    def __init__(self, params, group=None, bucket_bytes: int = 256 << 20, reduce: str = "mean",
+                 world: int | None = None):
+        """``world``: the group's size when no process group exists (measurement subclasses that
+        replace the collective, trainer_probe.EmulatedRingBuckets); else the group's own."""
         if reduce not in ("mean", "sum"):
             raise ValueError("reduce must be 'mean' or 'sum'")
         self.group = group
-        self.world = dist.get_world_size(group)
+        self.world = int(world) if world is not None else dist.get_world_size(group)
         self.reduce = reduce
         params = [p for p in params if p.requires_grad]
         self.buckets: list[_Bucket] = []
@@ -65,7 +68,7 @@ class GradBuckets:
         # compute stream's queue (GPU_MAX_HW_QUEUES 4; measured, profiles/r06_queue_probe.json), and the
         # collectives it orders would wait behind the backward's kernels (tools/queue_probe.py)
         self.stream = torch.cuda.Stream(device=dev, priority=-1) if self.on_gpu else None
-        self._avg = self.on_gpu and dist.get_backend(group) == "nccl" and reduce == "mean"
+        self._avg = self.on_gpu and world is None and dist.get_backend(group) == "nccl" and reduce == "mean"
         self._hooks = [p.register_post_accumulate_grad_hook(self._hook) for p in params]
         for p in params:  # model_ops._wgrad may add into .grad in the GEMM while not armed (no hook due)
             p._prl_grad_buckets = self

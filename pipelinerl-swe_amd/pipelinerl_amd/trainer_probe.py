@@ -119,12 +119,14 @@ class TrainerStep:
                  fused_ops: bool = True, group=None, model=None, step_fn=None, vocab: int | None = None,
                  fsdp: bool = False, kl_coef: float = 0.0, layers: int | None = None, batches: list | None = None,
                  samples_per_step: int | None = None, local: bool = False, flat_params: bool = True,
-                 keep_layers: int = 0, master_weights: bool = True):
+                 keep_layers: int = 0, master_weights: bool = True, value_head: bool = False):
         """``batches``: the packed micro-batches to train on (host PipelineBatchEncodings, e.g. from
         workloads.micro_batches), ``samples_per_step`` their global sample count (RLConfig.batch_size);
         default: ``micro_batches`` synthetic batches of ``tokens`` tokens.  ``local``: no gradient
         all-reduce even under a multi-rank group (the replica's compute alone, for the DP overhead).
-        ``master_weights``: fp32 master weights + moments, the trainer's default (finetune/optim.py)."""
+        ``master_weights``: fp32 master weights + moments, the trainer's default (finetune/optim.py).
+        ``value_head``: the model wrapped with a value head (finetune/value_model.py; the reference's
+        default actor_critic fine-tune config), value_loss_coef 0.1 (conf/finetune/actor_critic.yaml)."""
         from .finetune.grad_sync import GradBuckets
         from .finetune.optim import get_optimizer
         from .finetune.sharding import shard_model
@@ -136,6 +138,10 @@ class TrainerStep:
         self.world, self.tokens, self.micro_batches = world, tokens, micro_batches
         self.model = model if model is not None else qwen2_model(name, self.device, grad_ckpt, fused_ops, layers,
                                                                  keep_layers)
+        if value_head:
+            from .finetune.value_model import AutoModelForCausalLMWithValueHead
+
+            self.model = AutoModelForCausalLMWithValueHead(self.model).to(self.device)
         self.fsdp = fsdp
         if fsdp:  # FSDP2 over the default group (finetune/sharding.py): it reduce-scatters the grads
             if group is not None:
@@ -169,6 +175,8 @@ class TrainerStep:
             self.batches = [packed_batch(tokens, seq, prompt, V, self.device, seed=rank * 97 + i,
                                          ref_noise=kl_coef > 0) for i in range(micro_batches)]
             self.cfg = rl_config(micro_batches * (tokens // seq) * world, fused_head, kl_coef)
+        if value_head:
+            self.cfg.value_loss_coef = 0.1
         from .hostgc import freeze_setup_heap
 
         freeze_setup_heap()  # as the loop does before its first step
@@ -254,16 +262,18 @@ class TrainerStep:
             dist.all_reduce(dt, op=dist.ReduceOp.MAX, group=self.group)
         return float(dt)
 
-    def allreduce_alone(self, iters: int = 3) -> float:
+    def allreduce_alone(self, iters: int = 3, group_sync: bool = True) -> float:
         """Seconds of the bucketed gradient all-reduce over the model's real buckets with no
-        backward to hide behind (max over the group's ranks)."""
+        backward to hide behind (max over the group's ranks; ``group_sync`` False: this rank alone,
+        an emulated all-reduce at N = 1)."""
         if self.grads is None:
             return 0.0
         params = [p for p in self.model.parameters() if p.requires_grad]
         times = []
         for it in range(iters + 1):
             _sync(self.device)
-            dist.barrier(self.group)
+            if group_sync:
+                dist.barrier(self.group)
             t0 = time.perf_counter()
             self.grads.arm()
             for p in reversed(params):  # the order backward produces gradients
@@ -274,7 +284,8 @@ class TrainerStep:
                 times.append(time.perf_counter() - t0)
         self.grads.zero_()
         dt = torch.tensor([sum(times) / len(times)], dtype=torch.float64, device=self.device)
-        dist.all_reduce(dt, op=dist.ReduceOp.MAX, group=self.group)
+        if group_sync:
+            dist.all_reduce(dt, op=dist.ReduceOp.MAX, group=self.group)
         return float(dt)
 
     def close(self) -> None:
@@ -521,10 +532,73 @@ def snapshot_overlap(ts: "TrainerStep", t_ref: float, steps: int, warmup: int, f
             "steps_per_arm": steps, "rounds": rounds}
 
 
+class EmulatedRingBuckets:
+    """GradBuckets whose bucket all-reduce, at N = 1, makes the HBM reads and holds the CUs a ring
+    all-reduce over ``ranks`` GPUs would on this one (a ring moves 2(N−1)/N x S bytes
+    per GPU, per-link bound at ~153 GB/s per xGMI link): ``prl_paced_read`` over each bucket,
+    2(N−1)/N x its bytes, paced to ``gbps`` with ``channels`` workgroups, launched from the same
+    post-accumulate-grad hooks on GradBuckets' own stream the moment the bucket's last gradient lands
+    in the boundary micro-batch's backward.  What it prices: the all-reduce's contention with the
+    backward (CUs, HBM) and the tail no backward is left to hide (the embedding's gradient lands
+    last).  What it does not: the links' own latency and the peers' skew."""
+
+    def __new__(cls, params, ranks: int, gbps: float, channels: int, bucket_bytes: int = 256 << 20):
+        import ctypes
+
+        from . import _native
+        from .finetune.grad_sync import GradBuckets
+
+        lib = _native.load()
+
+        class _Done:
+            def wait(self):
+                return None
+
+        class _Emulated(GradBuckets):
+            def _launch(self, b):
+                b.launched = True
+                self.stream.wait_stream(torch.cuda.current_stream(b.flat.device))
+                nbytes = b.flat.numel() * b.flat.element_size() // 16 * 16
+                todo = int(2 * (ranks - 1) / ranks * nbytes) // 16 * 16
+                with torch.cuda.stream(self.stream):
+                    while todo > 0:  # the ring's 2(N-1)/N passes over the bucket
+                        n = min(todo, nbytes)
+                        _native.check(lib.prl_paced_read(ctypes.c_void_p(b.flat.data_ptr()), n, float(gbps),
+                                                         int(channels), ctypes.c_void_p(self._sink.data_ptr()),
+                                                         self.stream.cuda_stream), "prl_paced_read")
+                        todo -= n
+                b.work = _Done()
+
+        inst = _Emulated(params, bucket_bytes=bucket_bytes, world=1)
+        inst._sink = torch.zeros(max(1, int(channels)), dtype=torch.int32, device=inst.buckets[0].flat.device)
+        inst.bytes_per_gpu = int(2 * (ranks - 1) / ranks * sum(b.flat.numel() * b.flat.element_size()
+                                                               for b in inst.buckets))
+        return inst
+
+
+# emulated ring all-reduce arms at N = 1 (dp_step_probe ``emulate``): ranks, GB/s, channel workgroups.
+# One ring over one 153 GB/s xGMI link (SURVEY.md §5, the conservative case) at the SCALE run's N = 4
+# and 8; and N = 8 over the 7 direct links at once.
+RING_ARMS = {"n4_1link": (4, 153.0, 16), "n8_1link": (8, 153.0, 16), "n8_7links": (8, 7 * 153.0, 32)}
+
+
+def projected_dp_efficiency(lockstep_eff: float, exposed_ms: float, ms_per_micro_batch: float,
+                            micro_batches_per_rank: float, tail_ms: float) -> dict:
+    """C3's data-parallel efficiency at N from its two losses: the lockstep protocol's
+    (workloads.LOCKSTEP_EFFICIENCY: sentinel passes and the per-pass coupling of the ranks, the
+    loop's order) and the all-reduce's exposed time in one optimizer step, ``exposed_ms`` against
+    the step it ends (``micro_batches_per_rank`` x ``ms_per_micro_batch`` + the optimizer tail +
+    itself)."""
+    step = micro_batches_per_rank * ms_per_micro_batch + tail_ms + exposed_ms
+    ar = 1.0 - exposed_ms / step if step > 0 else 1.0
+    return {"lockstep_efficiency": round(lockstep_eff, 4), "allreduce_efficiency": round(ar, 6),
+            "projected_efficiency": round(lockstep_eff * ar, 4), "step_ms": round(step, 1)}
+
+
 def dp_step_probe(config: str = "c3", micro_batches: int = 4, steps: int = 2, warmup: int = 1, device=None,
                   samples_per_step: int = 4096, layers: int | None = None, batches: list | None = None,
                   model=None, step_fn=None, snapshot: bool = False, grad_ckpt: bool = False,
-                  keep_layers: int = 0) -> dict:
+                  keep_layers: int = 0, emulate: dict | None = None, value_head: bool = False) -> dict:
     """BASELINE.json configs[2] (C3) data-parallel trainer step on this rank's GPU: the config's
     model shapes (Qwen2.5-7B), ``micro_batches`` packed micro-batches per rank from the config's
     rollout distribution (workloads.py: prompt U{64..512} + completion U{256..8192}, packing cap
@@ -541,7 +615,11 @@ def dp_step_probe(config: str = "c3", micro_batches: int = 4, steps: int = 2, wa
     optimizer tail (clip + AdamW + zeroing, timed with device events: ``optimizer_tail_ms``).
     Collective over the default group (every rank calls it).  ``batches`` / ``model`` /
     ``step_fn`` are injectable (gloo tests on CPU).  ``snapshot``: also time the same step with the
-    weight-update snapshot in flight (``snapshot_overlap``, HIP devices only)."""
+    weight-update snapshot in flight (``snapshot_overlap``, HIP devices only).  ``emulate`` (N = 1,
+    HIP): {name: (ranks, GB/s, channels)} — the same step with each emulated ring all-reduce
+    (EmulatedRingBuckets) launched from the boundary backward's hooks: ``allreduce_emulated``, each
+    arm's exposed time and its projection to C3's real step at its N.  ``value_head``: the model
+    wrapped with a value head (the reference's default actor_critic config, value_loss_coef 0.1)."""
     from . import workloads
 
     device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
@@ -558,10 +636,22 @@ def dp_step_probe(config: str = "c3", micro_batches: int = 4, steps: int = 2, wa
         torch.cuda.reset_peak_memory_stats(device)
     ts = TrainerStep(spec.model, device=device, fused_head=True, kl_coef=spec.kl_coef, layers=layers,
                      batches=batches, samples_per_step=samples_per_step, local=True, model=model, step_fn=step_fn,
-                     grad_ckpt=grad_ckpt, keep_layers=keep_layers)
+                     grad_ckpt=grad_ckpt, keep_layers=keep_layers, value_head=value_head)
     t_local = ts.timed(steps, warmup)
     t_tail = ts.optimizer_tail()
     t_dp, t_ar = t_local, 0.0
+    emulated = {}
+    if emulate and world == 1 and on_gpu:
+        for name, (ranks, gbps, channels) in emulate.items():
+            ts.grads = EmulatedRingBuckets(list(ts.model.parameters()), ranks, gbps, channels)
+            t_e = ts.timed(steps, warmup)
+            t_alone = ts.allreduce_alone(group_sync=False)  # the reads alone, no backward to hide behind
+            emulated[name] = {"ranks": ranks, "link_GBps": gbps, "channel_workgroups": channels,
+                              "bytes_per_gpu": ts.grads.bytes_per_gpu, "ms_per_step": round(t_e * 1e3, 2),
+                              "alone_ms": round(t_alone * 1e3, 2),
+                              "exposed_ms": round(max(0.0, t_e - t_local) * 1e3, 2)}
+            ts.grads.remove()
+            ts.grads = None
     if world > 1:
         from .finetune.grad_sync import GradBuckets
 
@@ -592,6 +682,12 @@ def dp_step_probe(config: str = "c3", micro_batches: int = 4, steps: int = 2, wa
     per_mb = (t_local_max - t_tail) / micro_batches
     tok_per_mb = tok_all / (micro_batches * world)
     t_real = (mb_real / world) * per_mb + t_tail + exposed
+    from .workloads import LOCKSTEP_EFFICIENCY
+
+    for arm in emulated.values():  # projected to C3's real step at the arm's N
+        n = arm["ranks"]
+        arm["projection"] = projected_dp_efficiency(LOCKSTEP_EFFICIENCY[config][n], arm["exposed_ms"], per_mb * 1e3,
+                                                    mb_real / n, t_tail * 1e3)
     return {"config": f"C3: Qwen2.5-{spec.model} shapes{f' ({layers} layers)' if layers else ''} (random init, bf16), "
                       f"math rollouts packed at {spec.seq_length}, label-row lm_head",
             "micro_batches_per_rank": micro_batches, "tokens_per_rank_step": round(tok_all / world, 1),
@@ -610,6 +706,8 @@ def dp_step_probe(config: str = "c3", micro_batches: int = 4, steps: int = 2, wa
                              "allreduce_share": round(exposed / t_real, 5)},
             "peak_mem_gb": round(peak, 2), "steps": steps, "warmup": warmup, "world": world,
             **({"roofline": roof} if roof is not None else {}),
+            **({"allreduce_emulated": emulated} if emulated else {}),
+            **({"value_head": True} if value_head else {}),
             **({"snapshot_overlap": snap} if snap is not None else {})}
 
 

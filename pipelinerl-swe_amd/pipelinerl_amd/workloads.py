@@ -120,6 +120,12 @@ def rl_config(config: str, samples_per_step: int):
                     clamp_log_ratio_ref_new_value=5, divide_advantage_by_std=False, batch_size=samples_per_step)
 
 
+# lockstep_cost(config, N, 4096 // N)["efficiency"]["loop"]: the protocol's efficiency of one C3
+# optimizer step (4096 samples) at N data-parallel ranks, on the preprocessor's packing of C3's
+# rollouts (seed 7).  Minutes of CPU per N, so tabled: regenerate with tools/lockstep_table.py.
+LOCKSTEP_EFFICIENCY = {"c3": {1: 1.0, 2: 0.9786, 4: 0.9669, 8: 0.949}}
+
+
 def lockstep_cost(config: str, ranks: int, samples_per_rank: int, seed: int = 7, seq_length: int | None = None,
                   ms_fixed: float = 30.0, ms_per_token: float = (350.0 - 30.0) / 11425,
                   forward_share: float = 1 / 3) -> dict:
