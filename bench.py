@@ -93,8 +93,8 @@ def fp32_loss_head_probe(T: int, V: int, device, iters: int = 8, warmup: int = 2
     finetune_loop.py:381-385): the fused loss head's forward + gradient, HIP events on its stream;
     algorithmic bytes = logits read once + dlogits written once + side data.
     At Qwen2.5 vocabularies the product kernel is grpo_fwd_pair_f32<19> (each row fully resident
-    over a pair of CUs); the round-4 part-resident grpo_fwd_hybrid_f32<19, 9> (PRL_F32_PAIR=0) is
-    timed in alternation beside it, same process and buffers."""
+    over a pair of CUs); the round-4 part-resident grpo_fwd_hybrid_f32<19, 9> (PrlGrpoParams.f32_rows
+    = 1) is timed in alternation beside it, same process and buffers."""
     from pipelinerl_amd.finetune.rl.fused import GrpoParams, grpo_loss
 
     lb, fields = make_workload(T, V, seq=2048, prompt=256, seed=4321, device=device)
@@ -104,41 +104,38 @@ def fp32_loss_head_probe(T: int, V: int, device, iters: int = 8, warmup: int = 2
     params = GrpoParams(policy_loss="ppo", epsilon=4.0, kl_coef=0.0, entropy_coef=0.0, clamp_log_ratio=5.0,
                         temperature=1.0, batch_size=4096.0)
     times: dict[str, list[float]] = {"pair": [], "hybrid": []}
-    prev = os.environ.get("PRL_F32_PAIR")
     import ctypes
+    import dataclasses
 
     from pipelinerl_amd import _native
+    from pipelinerl_amd.finetune.rl.fused import _workspace
 
     def fallbacks() -> int:  # row halves that computed their partner's partial themselves (read + reset)
         n = ctypes.c_uint64(0)
-        _native.check(_native.load().prl_grpo_pair_fallbacks(device.index or 0, torch.cuda.current_stream(device).cuda_stream,
+        ws = _workspace(device)
+        _native.check(_native.load().prl_grpo_pair_fallbacks(ws.data_ptr(), ws.numel(),
+                                                             torch.cuda.current_stream(device).cuda_stream,
                                                              ctypes.byref(n)), "prl_grpo_pair_fallbacks")
         return int(n.value)
 
     fallbacks()
     fb, pair_launches = 0, 0
-    try:
-        for _ in range(rounds):
-            for arm in ("pair", "hybrid"):
-                os.environ["PRL_F32_PAIR"] = "1" if arm == "pair" else "0"  # read per launch
-                for i in range(warmup + iters):
-                    logits.grad = None
-                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                    e0.record()
-                    loss, stats, _ = grpo_loss(logits, fields, params)
-                    e1.record()
-                    loss.backward()
-                    stats.cpu()
-                    if i >= warmup:
-                        times[arm].append(e0.elapsed_time(e1))
-                if arm == "pair":
-                    fb += fallbacks()
-                    pair_launches += warmup + iters
-    finally:
-        if prev is None:
-            os.environ.pop("PRL_F32_PAIR", None)
-        else:
-            os.environ["PRL_F32_PAIR"] = prev
+    arm_params = {"pair": params, "hybrid": dataclasses.replace(params, f32_rows=1)}
+    for _ in range(rounds):
+        for arm in ("pair", "hybrid"):
+            for i in range(warmup + iters):
+                logits.grad = None
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                loss, stats, _ = grpo_loss(logits, fields, arm_params[arm])
+                e1.record()
+                loss.backward()
+                stats.cpu()
+                if i >= warmup:
+                    times[arm].append(e0.elapsed_time(e1))
+            if arm == "pair":
+                fb += fallbacks()
+                pair_launches += warmup + iters
     ms = float(np.median(times["pair"]))
     ms_h = float(np.median(times["hybrid"]))
     alg = 2.0 * T * V * 4 + SIDE_BYTES_PER_TOKEN * T
@@ -164,7 +161,7 @@ def fp32_loss_head_probe(T: int, V: int, device, iters: int = 8, warmup: int = 2
             "tokens_per_s": round(T / ms * 1e3, 1), "iters": iters * rounds,
             "pair_fallbacks_per_launch": round(fb / max(1, pair_launches), 3),
             "pair_row_halves_per_launch": 2 * T,
-            "hybrid": {"kernel": "grpo_fwd_hybrid_f32<19, 9> (PRL_F32_PAIR=0, alternated)", "kernel_ms": round(ms_h, 4),
+            "hybrid": {"kernel": "grpo_fwd_hybrid_f32<19, 9> (f32_rows=1, alternated)", "kernel_ms": round(ms_h, 4),
                        "frac": round(alg / ms_h / 1e6 / HBM_PEAK_GBS, 4),
                        "traffic_over_algorithmic": round(traffic_h / alg, 4) if traffic_h else None}}
 

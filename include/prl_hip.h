@@ -2,8 +2,16 @@
  *
  * Plain C: device pointers, sizes and a hipStream_t (passed as void*).  No torch types.
  * Every entry point returns 0 on success or a PRL_E* / hipError_t-derived code; nothing
- * throws across the ABI.  All buffers are caller-owned device memory.  The library keeps no
- * global state besides a per-device property cache.
+ * throws across the ABI.  All buffers are caller-owned device memory, scratch included (the
+ * workspaces and counters below); nothing is allocated on a launch path.  The library keeps no
+ * global state besides a per-device property cache.  A workspace or counter serves one stream at
+ * a time (launches on two streams in flight at once need two).
+ *
+ * ABI history: 2 -> 3 (round 6): prl_grpo_forward_rows takes the loss-head workspace;
+ * prl_grpo_pair_fallbacks reads the workspace's counter (not a per-stream library buffer);
+ * PrlGrpoParams gains pair_spin_ticks and f32_rows (replacing the PRL_PAIR_SPIN_TICKS /
+ * PRL_F32_PAIR environment reads); the phased SwiGLU entry points take their chunk counter;
+ * prl_grad_sqnorm requires its workspace (since round 5; PRL_E_WORKSPACE without one).
  *
  * Reference interfaces replaced (paths under the reference repo, ServiceNow/PipelineRL-SWE):
  *   prl_grpo_forward   <- rl_step loss head + stats + autograd backward
@@ -29,7 +37,7 @@
 extern "C" {
 #endif
 
-#define PRL_ABI_VERSION 2
+#define PRL_ABI_VERSION 3
 
 /* error codes (besides hipError_t values, which are < 1000) */
 #define PRL_OK 0
@@ -125,6 +133,11 @@ typedef struct PrlGrpoParams {
   float batch_size;            /* token weight = 1 / batch_size unless group-normalised */
   float value_loss_coef;
   float grad_scale;            /* upstream d(final_loss) assumed for dlogits / dvalues (> 0, finite) */
+  int32_t pair_spin_ticks;     /* fp32 pair kernel: realtime ticks (100 MHz) a row half waits for its
+                                  partner's partial before computing it from HBM itself (the same bits);
+                                  0 = the default (20000, 200 us), < 0 = never waits */
+  int32_t f32_rows;            /* fp32 logits: 0 = the pair kernel where the row fits two CUs (default),
+                                  1 = the part-resident kernel */
 } PrlGrpoParams;
 
 /* Outputs.  Per-token arrays have B*(L-1) entries (row q = b*(L-1) + t). */
@@ -145,7 +158,9 @@ typedef struct PrlGrpoOutputs {
 int prl_abi_version(void);
 const char* prl_error_string(int code);
 
-/* Bytes of device workspace prl_grpo_forward needs on `device` (per-block partial sums). */
+/* Bytes of the loss head's device workspace on `device`: the statistics' per-block partial sums
+ * and the row kernels' scratch (row counter, fp32 pair hand-off slots, pair fallback counter).
+ * Zero-fill it once when allocated (the fallback counter accumulates across launches). */
 int prl_grpo_workspace_bytes(int device, size_t* bytes);
 
 /* Fused loss head: log-softmax + gather + entropy over V, importance ratio x advantage
@@ -168,7 +183,7 @@ int prl_grpo_forward(const PrlGrpoBatch* batch, const PrlGrpoParams* params,
  * the ATen chain rl/__init__.py:199-208 for the rows its mask (:152-153) keeps. */
 int prl_grpo_forward_rows(const PrlGrpoBatch* batch, const PrlGrpoParams* params,
                           const int64_t* row_ids, int64_t n, const PrlGrpoOutputs* out,
-                          void* stream);
+                          void* workspace, size_t workspace_bytes, void* stream);
 
 /* Statistics (rl/__init__.py:315-375) and dvalues from the per-row new_logprobs / entropy
  * arrays over all B*(L-1) rows (batch->logits may be NULL).  Rows never scored must hold
@@ -193,10 +208,10 @@ int prl_grpo_backward(const PrlGrpoBatch* batch, const PrlGrpoParams* params,
 int prl_grpo_nstat(void);
 
 /* Observability of the pair kernels (fp32 rows, each split over two workgroups): how many row halves
- * on (device, stream) computed their partner's partial themselves because the partner had not
- * published it in time (PRL_PAIR_SPIN_TICKS) since the last call; reads and resets the counter,
- * synchronising the stream.  0 when no pair launch ran there. */
-int prl_grpo_pair_fallbacks(int device, void* stream, uint64_t* count);
+ * of launches with this workspace computed their partner's partial themselves because the partner
+ * had not published it in time (PrlGrpoParams.pair_spin_ticks) since the last call; reads and
+ * resets the workspace's counter, synchronising the stream. */
+int prl_grpo_pair_fallbacks(void* workspace, size_t workspace_bytes, void* stream, uint64_t* count);
 
 /* Weight broadcast staging: copy n tensors (f32 or bf16, contiguous) into one bf16 buffer
  * at the given element offsets (dst_offsets[i], bf16 elements; 8-element aligned for the
@@ -285,10 +300,12 @@ int prl_add_rmsnorm_forward(const void* residual, const void* x, const void* w, 
 int prl_add_rmsnorm_backward(const void* dy, const void* dh, const void* h, const void* w,
                              const float* rstd, void* dx, void* dw, void* workspace,
                              size_t workspace_bytes, int64_t rows, int64_t H, void* stream);
-/* out = bf16(bf16(silu(gate)) * up) over n elements; backward gives dgate, dup. */
-int prl_swiglu_forward(const void* gate, const void* up, void* out, int64_t n, void* stream);
+/* out = bf16(bf16(silu(gate)) * up) over n elements; backward gives dgate, dup.  counter: a
+ * caller-owned device uint32 the kernel's workgroups claim chunks from (zeroed by the call,
+ * stream-ordered); NULL = a static chunk stride (the same bits). */
+int prl_swiglu_forward(const void* gate, const void* up, void* out, int64_t n, uint32_t* counter, void* stream);
 int prl_swiglu_backward(const void* dout, const void* gate, const void* up, void* dgate, void* dup,
-                        int64_t n, void* stream);
+                        int64_t n, uint32_t* counter, void* stream);
 /* The same over [rows, cols] matrices with row strides (elements; cols and strides multiples of 8,
  * pointers 16-B aligned): gate / up as the column halves of one fused gate_up GEMM output, the
  * backward writing dgate / dup into the halves of one [rows, 2 cols] buffer.  Bit-identical to

@@ -1,6 +1,8 @@
 """ctypes binding of libprl_hip.so (C ABI in include/prl_hip.h).
 
 There is no CPU fallback: if the HIP library cannot be loaded, every entry point raises.
+Device scratch the kernels need (the loss head's workspace, the SwiGLU chunk counter) is allocated
+here, per (device, stream), as torch tensors the library is handed: the library holds none.
 """
 
 from __future__ import annotations
@@ -15,7 +17,7 @@ _PKG = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ["PRL_LIB"]) if os.environ.get("PRL_LIB") else _PKG / "libprl_hip.so"
 HEADER_PATH = _PKG.parents[1] / "include" / "prl_hip.h"
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 PRL_F32, PRL_BF16 = 0, 1
 PRL_PPO, PRL_REINFORCE = 0, 1
 
@@ -49,7 +51,7 @@ class PrlGrpoParams(ctypes.Structure):
         ("group_normalization", c_int32), ("overlong_filtering", c_int32), ("write_grad", c_int32),
         ("epsilon", c_float), ("kl_coef", c_float), ("entropy_coef", c_float),
         ("clamp_log_ratio", c_float), ("temperature", c_float), ("batch_size", c_float),
-        ("value_loss_coef", c_float), ("grad_scale", c_float),
+        ("value_loss_coef", c_float), ("grad_scale", c_float), ("pair_spin_ticks", c_int32), ("f32_rows", c_int32),
     ]
 
 
@@ -71,7 +73,7 @@ _SIGNATURES = {
     "prl_grpo_backward": (c_int, [POINTER(PrlGrpoBatch), POINTER(PrlGrpoParams), c_void_p, c_void_p,
                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "prl_grpo_forward_rows": (c_int, [POINTER(PrlGrpoBatch), POINTER(PrlGrpoParams), c_void_p, c_int64,
-                                      POINTER(PrlGrpoOutputs), c_void_p]),
+                                      POINTER(PrlGrpoOutputs), c_void_p, c_size_t, c_void_p]),
     "prl_grpo_stats": (c_int, [POINTER(PrlGrpoBatch), POINTER(PrlGrpoParams), POINTER(PrlGrpoOutputs),
                                c_void_p, c_size_t, c_void_p]),
     "prl_grpo_nstat": (c_int, []),
@@ -81,7 +83,7 @@ _SIGNATURES = {
                                    POINTER(c_int64), c_int32, c_void_p]),
     "prl_grad_scale_bf16": (c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_int64, c_int32, c_void_p]),
     "prl_paced_read": (c_int, [c_void_p, c_int64, c_double, c_int32, c_void_p, c_void_p]),
-    "prl_grpo_pair_fallbacks": (c_int, [c_int, c_void_p, POINTER(ctypes.c_uint64)]),
+    "prl_grpo_pair_fallbacks": (c_int, [c_void_p, c_size_t, c_void_p, POINTER(ctypes.c_uint64)]),
     "prl_adamw_step": (c_int, [c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32,
                                c_double, c_double, c_double, c_double, c_double, c_void_p, c_void_p]),
     "prl_adamw_master_step": (c_int, [c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -97,8 +99,8 @@ _SIGNATURES = {
                                         c_float, c_void_p]),
     "prl_add_rmsnorm_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                          c_void_p, c_size_t, c_int64, c_int64, c_void_p]),
-    "prl_swiglu_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
-    "prl_swiglu_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
+    "prl_swiglu_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
+    "prl_swiglu_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     "prl_swiglu_forward_rows": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64,
                                         c_void_p]),
     "prl_swiglu_backward_rows": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64,
@@ -123,6 +125,23 @@ _SIGNATURES = {
 }
 
 _lib = None
+_SCRATCH: dict[tuple, object] = {}
+
+
+def stream_scratch(kind: str, nbytes: int, device, stream: int):
+    """A zero-filled uint8 device tensor of ``nbytes`` for ``kind`` on (device, stream): the caller-owned
+    scratch of include/prl_hip.h (one stream at a time per workspace).  Cached: torch draws its
+    streams from fixed pools, so the keys stay few."""
+    import torch
+
+    dev = torch.device(device)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    key = (kind, idx, int(stream or 0))
+    t = _SCRATCH.get(key)
+    if t is None or t.numel() < nbytes:
+        t = torch.zeros(max(1, nbytes), dtype=torch.uint8, device=torch.device("cuda", idx))
+        _SCRATCH[key] = t
+    return t
 
 
 class PrlError(RuntimeError):

@@ -120,6 +120,12 @@ class WorkerExtension:
             t = resolve(name, tuple(shape))
             if (t is None or t.dtype != torch.bfloat16 or not t.is_contiguous() or t.device != self.device
                     or t.data_ptr() % 16):
+                if not getattr(self, "_warned_per_name", False):  # a slower path: say so, once
+                    self._warned_per_name = True
+                    why = ("no destination" if t is None else f"dtype {t.dtype}, contiguous {t.is_contiguous()}, "
+                           f"device {t.device} (this worker: {self.device}), 16-B aligned {t.data_ptr() % 16 == 0}")
+                    logger.warning(f"weight updates load per name (load_weights), not by one HIP unflatten: "
+                                   f"{name} {tuple(shape)}: {why}")
                 return None
             out.append(t)  # views share the parameter's version counter: the unflatten moves it
         return out

@@ -5,7 +5,7 @@
 // its autograd backward.  Kernels:
 //   grpo_fwd_resident<NV>  bf16 logits, V % 8 == 0 (Qwen2.5: V = 151936 / 152064).
 //       Persistent grid, one 1024-thread workgroup per CU, one vocab row per iteration; rows after
-//       a workgroup's first are claimed from a per-stream counter (KArgs.row_ctr).
+//       a workgroup's first are claimed from a counter in the caller's workspace (KArgs.row_ctr).
 //       The whole row (V*2 B = 297 KiB) is held in VGPRs (NV x 16 B per lane), so the
 //       gradient pass re-reads nothing.  Read / write phases: the row's dlogits stores retire,
 //       then the whole next row (~300 KiB per CU) is loaded at once, so a CU never mixes HBM
@@ -21,9 +21,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <cstdlib>
-#include <map>
-#include <mutex>
 #include <type_traits>
 #include <utility>
 
@@ -857,7 +854,10 @@ __global__ __launch_bounds__(1024) void grpo_fwd_hybrid_f32(KArgs a) {
 // within PairArgs::spin_ticks of the realtime clock (100 MHz) computes the partner's partial itself
 // from HBM (the same loads and arithmetic in the same order: the same bits), so a launch that shares
 // the chip with other kernels still completes.  Slots are zeroed by the host before each launch
-// (tag = the pair's row iteration + 1).
+// (tag = the pair's row iteration + 1).  A half waits at most once per launch: after a timeout it
+// only looks (one load) for the rest of the launch, and it never waits for a partner whose tag is
+// already past this row's (two or more rows ahead, it has overwritten the row's parity slot) — so
+// halves that drift apart cost one spin, not one per row.
 struct PairArgs {
   uint32_t* slots;      // [pairs][2 halves][2 parities] x 4 words {m, s, w, tag}
   int64_t slot_bytes;   // bytes of the slot array (its buffer descriptor's range)
@@ -872,20 +872,29 @@ constexpr int kSc1 = 16;  // aux bit of buffer_load / buffer_store: sc1 (bypass 
 
 // One lane of each half: publish this half's partial as one 16-B sc1 granule {m, s, w, tag} (a
 // single vector store: never torn, written through to memory), then poll the partner's granule with
-// sc1 loads until it carries this row's tag or spin_ticks of the realtime clock have passed; the
-// partner's words and whether they arrived go to `out` (LDS) for the whole workgroup.
+// sc1 loads until it carries this row's tag or spin_ticks of the realtime clock have passed (no wait
+// when spin_ticks is 0, or when the partner's tag is already past this row's); the partner's words
+// and whether they arrived go to `out` (LDS) for the whole workgroup.  The realtime clock is read
+// once per 8 polls (a tight clock loop delays other kernels' starts; flat_pack.hip paced_read_kernel),
+// s_sleep between polls.
 __device__ __forceinline__ void pair_exchange(__amdgpu_buffer_rsrc_t slots, int mine_off, int partner_off, uint32_t tag,
                                               Lse mine, int64_t spin_ticks, uint32_t* out) {
   const u32x4 g = {__float_as_uint(mine.m), __float_as_uint(mine.s), __float_as_uint(mine.w), tag};
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, g), slots,
                                          mine_off, 0, kSc1);
   u32x4 v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(slots, partner_off, 0, kSc1));
-  if (v[3] != tag) {
+  if (v[3] != tag && spin_ticks > 0) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (v[3] != tag && (int64_t)(__builtin_amdgcn_s_memrealtime() - t0) < spin_ticks) {
-      __builtin_amdgcn_s_sleep(1);
-      asm volatile("" ::: "memory");  // a fresh load every turn
-      v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(slots, partner_off, 0, kSc1));
+    bool more = true;
+    while (more) {
+#pragma unroll 1
+      for (int k = 0; k < 8 && v[3] != tag && (int32_t)(v[3] - tag) < 0; ++k) {
+        __builtin_amdgcn_s_sleep(2);
+        asm volatile("" ::: "memory");  // a fresh load every turn
+        v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(slots, partner_off, 0, kSc1));
+      }
+      more = v[3] != tag && (int32_t)(v[3] - tag) < 0 &&
+             (int64_t)(__builtin_amdgcn_s_memrealtime() - t0) < spin_ticks;
     }
   }
   out[0] = v[0];
@@ -978,6 +987,7 @@ __global__ __launch_bounds__(1024) void grpo_fwd_pair_f32(KArgs a, PairArgs pa) 
       buf[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, k * VSTRIDE, kLoadAux));
   }
   uint32_t it = 0;
+  int64_t spin = pa.spin_ticks;  // lane 0's wait budget: one spin per launch (see above)
   for (; i < nrows; i += npairs, ++it) {
     const int par = (int)(it & 1);
     const uint32_t tag = it + 1;
@@ -993,7 +1003,10 @@ __global__ __launch_bounds__(1024) void grpo_fwd_pair_f32(KArgs a, PairArgs pa) 
 
     // ---- pass 1: this half's state from registers, published for the partner
     const Lse mine = half_state<NV, true>(buf, slots, voff, last_ok, c, red[par], lane, wid);  // (rsrc unused)
-    if (tid == 0) pair_exchange(slots, my_slot + par * 16, partner_slot + par * 16, tag, mine, pa.spin_ticks, xch[par]);
+    if (tid == 0) {
+      pair_exchange(slots, my_slot + par * 16, partner_slot + par * 16, tag, mine, spin, xch[par]);
+      if (!xch[par][3]) spin = 0;  // the partner was late once: only look from now on
+    }
     __syncthreads();
     Lse part;
     if (xch[par][3]) {
@@ -1295,42 +1308,39 @@ static hipError_t launch_resident_nv(int nv, const KArgs& a, int grid, hipStream
   return launch_resident_table(nv, a, grid, s, std::make_integer_sequence<int, kMaxNV>{});
 }
 
-// the fp32 pair kernel: one zeroed slot array per (device, stream), so launches on different streams
-// never share hand-off slots; [pairs][2][2] granules of 16 B for up to 1024 CUs
+// The caller's workspace (prl_grpo_workspace_bytes): the statistics' per-block partials, then the
+// row kernels' scratch — the fp32 pair kernel's hand-off slots ([pairs][2][2] granules of 16 B for up
+// to 1024 CUs, zeroed before each pair launch), its fallback counter (accumulated over launches;
+// prl_grpo_pair_fallbacks reads and resets it) and the resident kernel's row counter (zeroed before
+// each launch).  No library-held device memory: a workspace serves one stream at a time.
 constexpr int kPairMaxCUs = 1024;
+constexpr size_t kPartialsBytes = sizeof(double) * (size_t)kMaxGrid * PRL_NSTAT;
 constexpr size_t kPairSlotBytes = (size_t)(kPairMaxCUs / 2) * 2 * 2 * 16;
-// after the slots: the fallback counter (not cleared per launch; prl_grpo_pair_fallbacks reads and resets it),
-// then the resident kernel's row counter (zeroed before every launch)
 constexpr size_t kPairCounterBytes = 16;
 constexpr size_t kRowCounterBytes = 16;
-static std::mutex g_slot_mu;
-static std::map<std::pair<int, hipStream_t>, void*> g_pair_slots;
+constexpr size_t kWorkspaceBytes = kPartialsBytes + kPairSlotBytes + kPairCounterBytes + kRowCounterBytes;
 
-static hipError_t pair_slots(int dev, hipStream_t s, void** out) {
-  std::lock_guard<std::mutex> lk(g_slot_mu);
-  auto key = std::make_pair(dev, s);
-  auto it = g_pair_slots.find(key);
-  if (it == g_pair_slots.end()) {
-    void* p = nullptr;
-    hipError_t e = hipMalloc(&p, kPairSlotBytes + kPairCounterBytes + kRowCounterBytes);
-    if (e != hipSuccess) return e;
-    e = hipMemset(static_cast<char*>(p) + kPairSlotBytes, 0, kPairCounterBytes + kRowCounterBytes);
-    if (e != hipSuccess) return e;
-    it = g_pair_slots.emplace(key, p).first;
-  }
-  *out = it->second;
-  return hipSuccess;
+struct Scratch {
+  uint32_t* slots;      // pair hand-off slots
+  uint32_t* fallbacks;  // pair fallback counter
+  uint32_t* row_ctr;    // resident kernel's row counter
+};
+static Scratch scratch_of(void* ws) {
+  char* p = static_cast<char*>(ws) + kPartialsBytes;
+  return Scratch{reinterpret_cast<uint32_t*>(p), reinterpret_cast<uint32_t*>(p + kPairSlotBytes),
+                 reinterpret_cast<uint32_t*>(p + kPairSlotBytes + kPairCounterBytes)};
 }
 
-// PRL_F32_PAIR=0 keeps the part-resident kernel for fp32 rows (A/B); PRL_PAIR_SPIN_TICKS sets the
-// partner wait (tests force the from-HBM partial with 0)
-static bool pair_f32_enabled() {
-  const char* e = getenv("PRL_F32_PAIR");  // read per launch: tests run both kernels in one process
-  return !(e && e[0] == '0');
+// the device a stream belongs to (the null stream: the current device)
+static int stream_device(hipStream_t s) {
+  int dev = 0;
+  if (s == nullptr || hipStreamGetDevice(s, &dev) != hipSuccess) (void)hipGetDevice(&dev);
+  return dev;
 }
-static int64_t pair_spin_ticks() {
-  const char* e = getenv("PRL_PAIR_SPIN_TICKS");  // read per launch: tests switch it
-  return e ? atoll(e) : (int64_t)PRL_PAIR_SPIN_TICKS;
+
+// the fp32 pair kernel's partner wait (PrlGrpoParams.pair_spin_ticks: 0 = the default, < 0 = none)
+static int64_t pair_spin_ticks(const PrlGrpoParams* p) {
+  return p->pair_spin_ticks == 0 ? (int64_t)PRL_PAIR_SPIN_TICKS : (p->pair_spin_ticks < 0 ? 0 : p->pair_spin_ticks);
 }
 
 template <int NV>
@@ -1353,7 +1363,8 @@ static int pair_nv(int64_t V) {
   const int64_t nv = (half + 1023) / 1024;
   return (nv >= kPairMinNV && nv <= kPairMaxNV) ? (int)nv : 0;
 }
-static hipError_t launch_pair_rows(const KArgs& a, int nv, int64_t nrows, int cus, int dev, hipStream_t s) {
+static hipError_t launch_pair_rows(const KArgs& a, int nv, int64_t nrows, int cus, const Scratch& sc,
+                                   int64_t spin_ticks, hipStream_t s) {
   int grid = cus < kPairMaxCUs ? cus : kPairMaxCUs;
   const int64_t need = 2 * nrows;
   if (need < grid) grid = (int)need;
@@ -1361,34 +1372,20 @@ static hipError_t launch_pair_rows(const KArgs& a, int nv, int64_t nrows, int cu
   if (grid > cus) grid = cus / 16 * 16;
   if (grid < 16) grid = 16;
   PairArgs pa{};
-  void* slots = nullptr;
-  hipError_t e = pair_slots(dev, s, &slots);
-  if (e != hipSuccess) return e;
-  pa.slots = static_cast<uint32_t*>(slots);
+  pa.slots = sc.slots;
   pa.slot_bytes = (int64_t)kPairSlotBytes;
-  pa.spin_ticks = pair_spin_ticks();
-  pa.fallbacks = reinterpret_cast<uint32_t*>(static_cast<char*>(slots) + kPairSlotBytes);
-  e = hipMemsetAsync(slots, 0, (size_t)(grid / 2) * 2 * 2 * 16, s);  // tags restart at 1 every launch
+  pa.spin_ticks = spin_ticks;
+  pa.fallbacks = sc.fallbacks;
+  const hipError_t e = hipMemsetAsync(sc.slots, 0, (size_t)(grid / 2) * 2 * 2 * 16, s);  // tags restart at 1
   if (e != hipSuccess) return e;
   return launch_pair_table(nv, a, pa, grid, s, std::make_integer_sequence<int, kPairMaxNV - kPairMinNV + 1>{});
 }
 
-// PRL_ROW_CLAIM=0: the resident kernel's static row stride (A/B); read per launch
-static bool row_claim_enabled() {
-  const char* e = getenv("PRL_ROW_CLAIM");
-  return !(e && e[0] == '0');
-}
-
-static hipError_t launch_resident_rows(KArgs a, int nv, int grid, int dev, hipStream_t s) {
-  a.row_ctr = nullptr;
-  if (row_claim_enabled()) {
-    void* scratch = nullptr;
-    hipError_t e = pair_slots(dev, s, &scratch);
-    if (e != hipSuccess) return e;
-    a.row_ctr = reinterpret_cast<uint32_t*>(static_cast<char*>(scratch) + kPairSlotBytes + kPairCounterBytes);
-    e = hipMemsetAsync(a.row_ctr, 0, sizeof(uint32_t), s);
-    if (e != hipSuccess) return e;
-  }
+// the resident kernel's rows claimed from the workspace's counter (zeroed here, stream-ordered)
+static hipError_t launch_resident_rows(KArgs a, int nv, int grid, const Scratch& sc, hipStream_t s) {
+  a.row_ctr = sc.row_ctr;
+  const hipError_t e = hipMemsetAsync(a.row_ctr, 0, sizeof(uint32_t), s);
+  if (e != hipSuccess) return e;
   return launch_resident_nv(nv, a, grid, s);
 }
 
@@ -1416,16 +1413,14 @@ static int fill_outputs(KArgs& a, const PrlGrpoBatch* b, const PrlGrpoParams* p,
 // the vocab pass over `nrows` logits rows: register-resident kernel when a bf16 row fits,
 // streaming kernels otherwise
 static hipError_t launch_rows(const KArgs& a, const PrlGrpoBatch* b, const PrlGrpoParams* p,
-                              const PrlGrpoOutputs* out, int64_t nrows, hipStream_t s) {
+                              const PrlGrpoOutputs* out, int64_t nrows, const Scratch& sc, hipStream_t s) {
   if (nrows <= 0) return hipSuccess;
-  int dev = 0;
-  hipGetDevice(&dev);
-  const int cus = device_cus(dev);
+  const int cus = device_cus(stream_device(s));
   const bool bf16 = b->logits_dtype == PRL_BF16;
   const bool vec_ok_bf = bf16 && b->V % 8 == 0 && b->ld % 8 == 0 && aligned16(b->logits) &&
                          (!p->write_grad || aligned16(out->dlogits));
   const int nv = vec_ok_bf ? resident_nv(b->V / 8) : 0;  // row <= 24*16 KiB
-  if (nv > 0) return launch_resident_rows(a, nv, (int)(nrows < cus ? nrows : cus), dev, s);
+  if (nv > 0) return launch_resident_rows(a, nv, (int)(nrows < cus ? nrows : cus), sc, s);
   const int64_t want = (int64_t)cus * 4;
   int grid = (int)(nrows < want ? nrows : want);
   if (grid > kMaxGrid) grid = kMaxGrid;
@@ -1435,8 +1430,8 @@ static hipError_t launch_rows(const KArgs& a, const PrlGrpoBatch* b, const PrlGr
     hipLaunchKernelGGL((grpo_fwd_stream<uint16_t, 1>), dim3(grid), dim3(256), 0, s, a);
   } else if (b->V % 4 == 0 && b->ld % 4 == 0 && aligned16(b->logits) &&
              (!p->write_grad || aligned16(out->dlogits))) {
-    const int pnv = pair_f32_enabled() ? pair_nv(b->V) : 0;
-    if (pnv > 0) return launch_pair_rows(a, pnv, nrows, cus, dev, s);  // the row fully resident over two CUs
+    const int pnv = p->f32_rows == 0 ? pair_nv(b->V) : 0;  // PrlGrpoParams.f32_rows 1: the part-resident kernel
+    if (pnv > 0) return launch_pair_rows(a, pnv, nrows, cus, sc, pair_spin_ticks(p), s);  // resident over two CUs
     if (PRL_HYB_NL >= 0 && b->V / 4 >= (int64_t)(kHybNR + kHybNL) * 1024) {  // a tail to stream: the row part-resident
       const int g1 = (int)(nrows < cus ? nrows : cus);  // one workgroup per CU (the LDS slab)
       hipLaunchKernelGGL((grpo_fwd_hybrid_f32<kHybNR, kHybNL>), dim3(g1), dim3(1024), 0, s, a);
@@ -1488,7 +1483,7 @@ const char* prl_error_string(int code) {
 int prl_grpo_workspace_bytes(int device, size_t* bytes) {
   (void)device;
   if (!bytes) return PRL_E_INVALID;
-  *bytes = sizeof(double) * (size_t)kMaxGrid * PRL_NSTAT;
+  *bytes = kWorkspaceBytes;
   return PRL_OK;
 }
 
@@ -1500,7 +1495,7 @@ int prl_grpo_forward(const PrlGrpoBatch* batch, const PrlGrpoParams* params,
   if (rc) return rc;
   rc = fill_outputs(a, batch, params, out, true);
   if (rc) return rc;
-  if (!workspace || workspace_bytes < sizeof(double) * (size_t)kMaxGrid * PRL_NSTAT) return PRL_E_WORKSPACE;
+  if (!workspace || workspace_bytes < kWorkspaceBytes) return PRL_E_WORKSPACE;
   hipStream_t s = static_cast<hipStream_t>(stream);
   a.partials = static_cast<double*>(workspace);
   const size_t es = batch->logits_dtype == PRL_BF16 ? 2 : 4;
@@ -1516,13 +1511,14 @@ int prl_grpo_forward(const PrlGrpoBatch* batch, const PrlGrpoParams* params,
     if (e != hipSuccess) return (int)e;
   }
   const int64_t nrows = batch->B * (batch->L - 1);
-  e = launch_rows(a, batch, params, out, nrows, s);
+  e = launch_rows(a, batch, params, out, nrows, scratch_of(workspace), s);
   if (e != hipSuccess) return (int)e;
   return (int)launch_stats(a, nrows, out->stats, s);
 }
 
 int prl_grpo_forward_rows(const PrlGrpoBatch* batch, const PrlGrpoParams* params, const int64_t* row_ids,
-                          int64_t n, const PrlGrpoOutputs* out, void* stream) {
+                          int64_t n, const PrlGrpoOutputs* out, void* workspace, size_t workspace_bytes,
+                          void* stream) {
   KArgs a;
   int rc = fill_args(a, batch, params);
   if (rc) return rc;
@@ -1532,10 +1528,11 @@ int prl_grpo_forward_rows(const PrlGrpoBatch* batch, const PrlGrpoParams* params
   rc = fill_outputs(a, batch, params, out, false);
   if (rc) return rc;
   if (n < 0 || (n > 0 && !row_ids)) return PRL_E_INVALID;
+  if (!workspace || workspace_bytes < kWorkspaceBytes) return PRL_E_WORKSPACE;
   if (n == 0) return PRL_OK;
   a.row_ids = row_ids;
   a.nsel = n;
-  return (int)launch_rows(a, batch, params, out, n, static_cast<hipStream_t>(stream));
+  return (int)launch_rows(a, batch, params, out, n, scratch_of(workspace), static_cast<hipStream_t>(stream));
 }
 
 int prl_grpo_stats(const PrlGrpoBatch* batch, const PrlGrpoParams* params, const PrlGrpoOutputs* out,
@@ -1545,7 +1542,7 @@ int prl_grpo_stats(const PrlGrpoBatch* batch, const PrlGrpoParams* params, const
   if (rc) return rc;
   if (!out || !out->new_logprobs || !out->entropy || !out->stats) return PRL_E_INVALID;
   if (batch->values && !out->dvalues) return PRL_E_INVALID;
-  if (!workspace || workspace_bytes < sizeof(double) * (size_t)kMaxGrid * PRL_NSTAT) return PRL_E_WORKSPACE;
+  if (!workspace || workspace_bytes < kWorkspaceBytes) return PRL_E_WORKSPACE;
   a.o_lp = out->new_logprobs;
   a.o_ent = out->entropy;
   a.o_dv = out->dvalues;
@@ -1577,9 +1574,7 @@ int prl_grpo_backward(const PrlGrpoBatch* batch, const PrlGrpoParams* params, co
   }
   const int64_t nrows = batch->B * (batch->L - 1);
   if (nrows == 0) return PRL_OK;
-  int dev = 0;
-  hipGetDevice(&dev);
-  const int64_t want = (int64_t)device_cus(dev) * 8;
+  const int64_t want = (int64_t)device_cus(stream_device(s)) * 8;
   const int grid = (int)(nrows < want ? nrows : want);
   const bool bf16 = batch->logits_dtype == PRL_BF16;
   if (bf16 && batch->V % 8 == 0 && batch->ld % 8 == 0 && aligned16(batch->logits) && aligned16(dlogits)) {
@@ -1596,18 +1591,12 @@ int prl_grpo_backward(const PrlGrpoBatch* batch, const PrlGrpoParams* params, co
 
 int prl_grpo_nstat(void) { return PRL_NSTAT; }
 
-int prl_grpo_pair_fallbacks(int device, void* stream, uint64_t* count) {
+int prl_grpo_pair_fallbacks(void* workspace, size_t workspace_bytes, void* stream, uint64_t* count) {
   if (!count) return PRL_E_INVALID;
   *count = 0;
-  void* slots = nullptr;
-  {
-    std::lock_guard<std::mutex> lk(g_slot_mu);
-    auto it = g_pair_slots.find(std::make_pair(device, static_cast<hipStream_t>(stream)));
-    if (it == g_pair_slots.end()) return PRL_OK;  // no pair launch on this stream yet
-    slots = it->second;
-  }
+  if (!workspace || workspace_bytes < kWorkspaceBytes) return PRL_E_WORKSPACE;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  uint32_t* ctr = reinterpret_cast<uint32_t*>(static_cast<char*>(slots) + kPairSlotBytes);
+  uint32_t* ctr = scratch_of(workspace).fallbacks;
   uint32_t host = 0;
   hipError_t e = hipMemcpyAsync(&host, ctr, sizeof(host), hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipMemsetAsync(ctr, 0, sizeof(uint32_t), s);

@@ -14,9 +14,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <cstdlib>
-#include <map>
-#include <mutex>
 #include <utility>
 
 #include "prl_hip.h"
@@ -887,40 +884,24 @@ bool a8(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7u) == 0; }
 #ifndef PRL_SWIGLU_PHASED_WG
 #define PRL_SWIGLU_PHASED_WG 1
 #endif
-// the phased SwiGLU kernels' chunk counter: one per (device, stream), zeroed before each launch
-// (PRL_CHUNK_CLAIM=0: the static stride, A/B; read per launch)
-static std::mutex g_ctr_mu;
-static std::map<std::pair<int, hipStream_t>, uint32_t*> g_ctrs;
-static hipError_t chunk_counter(hipStream_t s, uint32_t** out) {
-  *out = nullptr;
-  const char* env = getenv("PRL_CHUNK_CLAIM");
-  if (env && env[0] == '0') return hipSuccess;
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) return e;
-  {
-    std::lock_guard<std::mutex> lk(g_ctr_mu);
-    auto key = std::make_pair(dev, s);
-    auto it = g_ctrs.find(key);
-    if (it == g_ctrs.end()) {
-      void* p = nullptr;
-      e = hipMalloc(&p, 16);
-      if (e != hipSuccess) return e;
-      it = g_ctrs.emplace(key, static_cast<uint32_t*>(p)).first;
-    }
-    *out = it->second;
-  }
-  return hipMemsetAsync(*out, 0, sizeof(uint32_t), s);
+// the phased SwiGLU kernels claim chunks from the caller's counter (zeroed here, stream-ordered);
+// without one they take the static stride
+static hipError_t reset_counter(uint32_t* ctr, hipStream_t s) {
+  return ctr ? hipMemsetAsync(ctr, 0, sizeof(uint32_t), s) : hipSuccess;
 }
 
-static int phased_grid() {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-      cus = 256;
+// one workgroup per CU of the stream's device (cached per device)
+static int phased_grid(hipStream_t s) {
+  static int cus[64] = {};
+  int dev = 0;
+  if (s == nullptr || hipStreamGetDevice(s, &dev) != hipSuccess) (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 64) return 256 * PRL_SWIGLU_PHASED_WG;
+  if (!cus[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cus[dev] = n;
   }
-  return cus * PRL_SWIGLU_PHASED_WG;
+  return cus[dev] * PRL_SWIGLU_PHASED_WG;
 }
 int ew_grid(int64_t n8) {
   const int64_t g = (n8 + 255) / 256;
@@ -1016,19 +997,19 @@ int prl_add_rmsnorm_backward(const void* dy, const void* dh, const void* h, cons
   return norm_backward(dy, h, w, rstd, dx, dw, workspace, workspace_bytes, rows, H, stream, dh);
 }
 
-int prl_swiglu_forward(const void* gate, const void* up, void* out, int64_t n, void* stream) {
+int prl_swiglu_forward(const void* gate, const void* up, void* out, int64_t n, uint32_t* counter, void* stream) {
   if (!gate || !up || !out || n < 0) return PRL_E_INVALID;
   if (n % 8 || !a16(gate) || !a16(up) || !a16(out)) return PRL_E_UNSUPPORTED;
   if (n == 0) return PRL_OK;
   const int64_t n8 = n / 8;
   if (PRL_SWIGLU_PHASED) {
+    const hipStream_t s = static_cast<hipStream_t>(stream);
     const int64_t chunks = (n8 + 1024 * kPhFwdU - 1) / (1024 * kPhFwdU);
-    const int grid = (int)(chunks < phased_grid() ? chunks : phased_grid());
-    uint32_t* ctr = nullptr;
-    const hipError_t e = chunk_counter(static_cast<hipStream_t>(stream), &ctr);
+    const int grid = (int)(chunks < phased_grid(s) ? chunks : phased_grid(s));
+    const hipError_t e = reset_counter(counter, s);
     if (e != hipSuccess) return (int)e;
-    hipLaunchKernelGGL(swiglu_fwd_phased, dim3(grid), dim3(1024), 0, static_cast<hipStream_t>(stream),
-                       (const u32x4*)gate, (const u32x4*)up, (u32x4*)out, n8, ctr);
+    hipLaunchKernelGGL(swiglu_fwd_phased, dim3(grid), dim3(1024), 0, s,
+                       (const u32x4*)gate, (const u32x4*)up, (u32x4*)out, n8, counter);
     return (int)hipGetLastError();
   }
   hipLaunchKernelGGL(swiglu_fwd, dim3(ew_grid(n8)), dim3(256), 0, static_cast<hipStream_t>(stream),
@@ -1037,19 +1018,19 @@ int prl_swiglu_forward(const void* gate, const void* up, void* out, int64_t n, v
 }
 
 int prl_swiglu_backward(const void* dout, const void* gate, const void* up, void* dgate, void* dup, int64_t n,
-                        void* stream) {
+                        uint32_t* counter, void* stream) {
   if (!dout || !gate || !up || !dgate || !dup || n < 0) return PRL_E_INVALID;
   if (n % 8 || !a16(dout) || !a16(gate) || !a16(up) || !a16(dgate) || !a16(dup)) return PRL_E_UNSUPPORTED;
   if (n == 0) return PRL_OK;
   const int64_t n8 = n / 8;
   if (PRL_SWIGLU_PHASED) {
+    const hipStream_t s = static_cast<hipStream_t>(stream);
     const int64_t chunks = (n8 + 1024 * kPhBwdU - 1) / (1024 * kPhBwdU);
-    const int grid = (int)(chunks < phased_grid() ? chunks : phased_grid());
-    uint32_t* ctr = nullptr;
-    const hipError_t e = chunk_counter(static_cast<hipStream_t>(stream), &ctr);
+    const int grid = (int)(chunks < phased_grid(s) ? chunks : phased_grid(s));
+    const hipError_t e = reset_counter(counter, s);
     if (e != hipSuccess) return (int)e;
-    hipLaunchKernelGGL(swiglu_bwd_phased, dim3(grid), dim3(1024), 0, static_cast<hipStream_t>(stream),
-                       (const u32x4*)dout, (const u32x4*)gate, (const u32x4*)up, (u32x4*)dgate, (u32x4*)dup, n8, ctr);
+    hipLaunchKernelGGL(swiglu_bwd_phased, dim3(grid), dim3(1024), 0, s,
+                       (const u32x4*)dout, (const u32x4*)gate, (const u32x4*)up, (u32x4*)dgate, (u32x4*)dup, n8, counter);
     return (int)hipGetLastError();
   }
   hipLaunchKernelGGL(swiglu_bwd, dim3(ew_grid(n8)), dim3(256), 0, static_cast<hipStream_t>(stream),
@@ -1069,7 +1050,8 @@ int prl_swiglu_forward_rows(const void* gate, const void* up, void* out, int64_t
   if (rows == 0 || cols == 0) return PRL_OK;
   if (PRL_SWIGLU_ROWS_PHASED) {
     const int64_t chunks = (rows * (cols / 8) + 1024 * kPhFwdU - 1) / (1024 * kPhFwdU);
-    const int grid = (int)(chunks < phased_grid() ? chunks : phased_grid());
+    const int grid = (int)(chunks < phased_grid(static_cast<hipStream_t>(stream)) ? chunks
+                                                                               : phased_grid(static_cast<hipStream_t>(stream)));
     hipLaunchKernelGGL(swiglu_fwd_rows_phased, dim3(grid), dim3(1024), 0, static_cast<hipStream_t>(stream),
                        (const u32x4*)gate, (const u32x4*)up, (u32x4*)out, rows, (int)(cols / 8), ld_gate / 8,
                        ld_up / 8, ld_out / 8);
@@ -1093,7 +1075,8 @@ int prl_swiglu_backward_rows(const void* dout, const void* gate, const void* up,
   if (rows == 0 || cols == 0) return PRL_OK;
   if (PRL_SWIGLU_ROWS_PHASED) {
     const int64_t chunks = (rows * (cols / 8) + 1024 * kPhBwdU - 1) / (1024 * kPhBwdU);
-    const int grid = (int)(chunks < phased_grid() ? chunks : phased_grid());
+    const int grid = (int)(chunks < phased_grid(static_cast<hipStream_t>(stream)) ? chunks
+                                                                               : phased_grid(static_cast<hipStream_t>(stream)));
     hipLaunchKernelGGL(swiglu_bwd_rows_phased, dim3(grid), dim3(1024), 0, static_cast<hipStream_t>(stream),
                        (const u32x4*)dout, (const u32x4*)gate, (const u32x4*)up, (u32x4*)dgate, (u32x4*)dup, rows,
                        (int)(cols / 8), ld_dout / 8, ld_gate / 8, ld_up / 8, ld_dgate / 8, ld_dup / 8);

@@ -128,12 +128,18 @@ class AddRMSNormFn(torch.autograd.Function):
         return dx, dx, dw, None
 
 
+def _chunk_counter(t: torch.Tensor) -> int:
+    """The phased SwiGLU kernels' chunk counter for ``t``'s device and current stream (caller-owned
+    scratch, include/prl_hip.h: the library zeroes it per launch)."""
+    return _native.stream_scratch("swiglu_ctr", 16, t.device, _stream(t)).data_ptr()
+
+
 class SwiGLUFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, g, u):
         h = torch.empty_like(g)
         _native.check(_native.load().prl_swiglu_forward(g.data_ptr(), u.data_ptr(), h.data_ptr(), g.numel(),
-                                                        _stream(g)), "prl_swiglu_forward")
+                                                        _chunk_counter(g), _stream(g)), "prl_swiglu_forward")
         ctx.save_for_backward(g, u)
         return h
 
@@ -143,7 +149,8 @@ class SwiGLUFn(torch.autograd.Function):
         dh = dh.contiguous()
         dg, du = torch.empty_like(g), torch.empty_like(u)
         _native.check(_native.load().prl_swiglu_backward(dh.data_ptr(), g.data_ptr(), u.data_ptr(), dg.data_ptr(),
-                                                         du.data_ptr(), g.numel(), _stream(g)), "prl_swiglu_backward")
+                                                         du.data_ptr(), g.numel(), _chunk_counter(g), _stream(g)),
+                      "prl_swiglu_backward")
         return dg, du
 
 

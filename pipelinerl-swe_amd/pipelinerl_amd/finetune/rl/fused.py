@@ -24,19 +24,14 @@ import torch
 from ... import _native
 from ..._native import PRL_BF16, PRL_F32, PRL_PPO, PRL_REINFORCE, NSTAT
 
-_WORKSPACE: dict[int, torch.Tensor] = {}
-
-
 def _workspace(device: torch.device) -> torch.Tensor:
+    """The loss head's workspace (statistics partials + row-kernel scratch, include/prl_hip.h) for the
+    current stream of ``device``: zero-filled once, one per (device, stream)."""
     idx = device.index if device.index is not None else torch.cuda.current_device()
-    ws = _WORKSPACE.get(idx)
-    if ws is None:
-        lib = _native.load()
-        nbytes = ctypes.c_size_t(0)
-        _native.check(lib.prl_grpo_workspace_bytes(idx, ctypes.byref(nbytes)), "prl_grpo_workspace_bytes")
-        ws = torch.empty(nbytes.value, dtype=torch.uint8, device=device)
-        _WORKSPACE[idx] = ws
-    return ws
+    lib = _native.load()
+    nbytes = ctypes.c_size_t(0)
+    _native.check(lib.prl_grpo_workspace_bytes(idx, ctypes.byref(nbytes)), "prl_grpo_workspace_bytes")
+    return _native.stream_scratch("grpo", nbytes.value, device, torch.cuda.current_stream(device).cuda_stream)
 
 
 @dataclass
@@ -56,6 +51,10 @@ class GrpoParams:
     value_loss_coef: float = 0.0
     # the upstream gradient the forward writes dlogits / dvalues for (the caller's loss scale)
     grad_scale: float = 1.0
+    # fp32 logits: the pair kernel's partner wait (0 default, < 0 none) and the part-resident kernel
+    # instead of the pair kernel (f32_rows 1) — measurement and test controls (include/prl_hip.h)
+    pair_spin_ticks: int = 0
+    f32_rows: int = 0
 
     def to_c(self, write_grad: bool) -> _native.PrlGrpoParams:
         if self.policy_loss == "ppo":
@@ -68,7 +67,7 @@ class GrpoParams:
             kind, int(self.use_advantages), int(self.relu_log_p_weights), int(self.group_normalization),
             int(self.overlong_filtering), int(write_grad), self.epsilon, self.kl_coef, self.entropy_coef,
             self.clamp_log_ratio, self.temperature, float(self.batch_size), self.value_loss_coef,
-            float(self.grad_scale))
+            float(self.grad_scale), int(self.pair_spin_ticks), int(self.f32_rows))
 
 
 FIELDS = ("input_ids", "labels", "rewards", "advantages", "ref_logprobs", "old_logprobs", "group_tokens",

@@ -149,9 +149,10 @@ class LinearGrpoLossFn(torch.autograd.Function):
                                             lg.data_ptr() if write_grad else None, None)
                 if ROW_TAP is not None:
                     ROW_TAP("logits", qc, lg, rows)
+                ws = _workspace(dev)
                 _native.check(lib.prl_grpo_forward_rows(ctypes.byref(cb), ctypes.byref(cp), qc.data_ptr(),
-                                                        qc.numel(), ctypes.byref(co), stream),
-                              "prl_grpo_forward_rows")
+                                                        qc.numel(), ctypes.byref(co), ws.data_ptr(), ws.numel(),
+                                                        stream), "prl_grpo_forward_rows")
                 if ROW_TAP is not None:
                     ROW_TAP("dlogits", qc, lg, rows)
                 if write_grad and use_prl:  # ROCm hipBLASLt (include/prl_gemm.h)

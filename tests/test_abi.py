@@ -17,7 +17,7 @@ def test_library_exports_header_symbols():
     assert len(declared) >= 9
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.prl_abi_version() == _native.ABI_VERSION == 2
+    assert lib.prl_abi_version() == _native.ABI_VERSION == 3
     assert lib.prl_grpo_nstat() == _native.NSTAT
     assert lib.prl_error_string(1001).decode() == "invalid argument"
     nbytes = ctypes.c_size_t(0)
@@ -37,7 +37,7 @@ def test_struct_layouts():
     from pipelinerl_amd import _native
 
     assert ctypes.sizeof(_native.PrlGrpoBatch) == 8 + 4 + 4 + 4 * 8 + 10 * 8
-    assert ctypes.sizeof(_native.PrlGrpoParams) == 6 * 4 + 8 * 4
+    assert ctypes.sizeof(_native.PrlGrpoParams) == 6 * 4 + 8 * 4 + 2 * 4  # + pair_spin_ticks, f32_rows (ABI 3)
     assert ctypes.sizeof(_native.PrlGrpoOutputs) == 11 * 8
 
 
@@ -51,7 +51,9 @@ def test_invalid_arguments_rejected_without_gpu():
     # null pointers / zero shapes are rejected before any device call
     assert lib.prl_grpo_forward(ctypes.byref(b), ctypes.byref(p), ctypes.byref(o), None, 0, None) == 1001
     assert lib.prl_flatten_bf16(None, None, None, None, -1, None, None) == 1001
-    assert lib.prl_grpo_pair_fallbacks(0, None, None) == 1001
+    assert lib.prl_grpo_pair_fallbacks(None, 0, None, None) == 1001
+    n = ctypes.c_uint64(7)
+    assert lib.prl_grpo_pair_fallbacks(None, 0, None, ctypes.byref(n)) == 1003 and n.value == 0  # no workspace
     assert lib.prl_paced_read(None, 1 << 20, 153.0, 16, None, None) == 1001
     assert lib.prl_paced_read(16, 1 << 20, 0.0, 16, 16, None) == 1001  # a rate must be given
     assert lib.prl_paced_read(16, 1 << 20, 153.0, 0, 16, None) == 1001

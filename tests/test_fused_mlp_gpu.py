@@ -26,14 +26,15 @@ def test_swiglu_rows_bit_exact_to_contiguous():
     dh = torch.randn((rows, I), generator=g, device=DEV).to(torch.bfloat16)
     gate, up = gu[:, :I].contiguous(), gu[:, I:].contiguous()
     h_ref = torch.empty_like(gate)
-    _native.check(lib.prl_swiglu_forward(gate.data_ptr(), up.data_ptr(), h_ref.data_ptr(), gate.numel(), st), "fwd")
+    _native.check(lib.prl_swiglu_forward(gate.data_ptr(), up.data_ptr(), h_ref.data_ptr(), gate.numel(), None, st),
+                  "fwd")
     h = torch.empty_like(gate)
     _native.check(lib.prl_swiglu_forward_rows(gu.data_ptr(), gu.data_ptr() + 2 * I, h.data_ptr(), rows, I, 2 * I,
                                               2 * I, I, st), "fwd rows")
     assert torch.equal(_bits(h), _bits(h_ref))
     dg_ref, du_ref = torch.empty_like(gate), torch.empty_like(up)
     _native.check(lib.prl_swiglu_backward(dh.data_ptr(), gate.data_ptr(), up.data_ptr(), dg_ref.data_ptr(),
-                                          du_ref.data_ptr(), gate.numel(), st), "bwd")
+                                          du_ref.data_ptr(), gate.numel(), None, st), "bwd")
     dgu = torch.empty_like(gu)
     _native.check(lib.prl_swiglu_backward_rows(dh.data_ptr(), gu.data_ptr(), gu.data_ptr() + 2 * I, dgu.data_ptr(),
                                                dgu.data_ptr() + 2 * I, rows, I, I, 2 * I, 2 * I, 2 * I, 2 * I, st),

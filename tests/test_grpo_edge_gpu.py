@@ -167,25 +167,17 @@ def test_unpacked_bf16_value_head_ragged():
 
 def test_multi_row_per_workgroup():
     """Qwen2.5's vocab (the resident kernel's NV = 19, read / write phased schedule) with ~2.3 rows
-    per workgroup of the persistent grid, so rows with and without a next row are both taken: every
-    row's dlogits and every statistic against the oracle, two runs bitwise identical, and the static
-    row stride (PRL_ROW_CLAIM=0) bitwise identical to the claimed rows."""
-    import os
-
+    per workgroup of the persistent grid, so rows with and without a next row are both taken (rows
+    claimed from the workspace's counter): every row's dlogits and every statistic against the
+    oracle, two runs bitwise identical."""
     V = 151936
     lens = [150, 200, 251]
     T = sum(lens)
     b = _batch(T, V, seed=9, lens=lens, prompts=[20, 30, 40])
     lg = synth.to_bf16(np.random.default_rng(9).normal(0, 2.5, (1, T, V))).astype(np.float32)
     stats1, d1 = _cmp(lg, b)
-    _, _, d2 = _run(lg, b)
-    assert np.array_equal(d1, d2)
-    os.environ["PRL_ROW_CLAIM"] = "0"
-    try:
-        loss3, stats3, d3 = _run(lg, b)
-    finally:
-        del os.environ["PRL_ROW_CLAIM"]
-    assert np.array_equal(d1, d3) and stats3 == stats1
+    _, stats2, d2 = _run(lg, b)
+    assert np.array_equal(d1, d2) and stats2 == stats1
 
 
 @pytest.mark.parametrize("V", [151936, 152064])
@@ -240,19 +232,34 @@ def test_target_columns_at_vector_edges(ent):
 
 # fp32 logits at a Qwen2.5 vocabulary take the pair kernel (grpo_fwd_pair_f32<19>: the row split
 # over two workgroups, columns [0, 75 968) and [75 968, 151 936), each half in registers, 19 vectors
-# per lane, the last one partial) or, with PRL_F32_PAIR=0, the part-resident one
+# per lane, the last one partial) or, with PrlGrpoParams.f32_rows = 1, the part-resident one
 # (grpo_fwd_hybrid_f32<19, 9>: columns [0, 77 824) in registers, [77 824, 114 688) in LDS, the rest
-# streamed and re-read).  PRL_PAIR_SPIN_TICKS=0: a half never waits for its partner's partial and
+# streamed and re-read).  pair_spin_ticks < 0: a half never waits for its partner's partial and
 # computes it from HBM whenever it has not arrived yet (the bounded-spin path).
 HYB_EDGES = [0, 3, 4, 77823, 77824, 77827, 114687, 114688, 114691, 151935]
 PAIR_EDGES = [0, 3, 4, 73723, 73727, 73728, 75967, 75968, 75971, 75972, 149503, 149504, 151935]
-F32_KERNELS = {"pair": {}, "pair_nowait": {"PRL_PAIR_SPIN_TICKS": "0"}, "hybrid": {"PRL_F32_PAIR": "0"}}
+F32_KERNELS = {"pair": {}, "pair_nowait": {"pair_spin_ticks": -1}, "hybrid": {"f32_rows": 1}}
+
+
+def _controls(monkeypatch, **fields):
+    """The loss head's kernel controls (PrlGrpoParams.pair_spin_ticks / f32_rows) for every launch
+    rl_step makes while ``monkeypatch`` is active."""
+    from pipelinerl_amd.finetune.rl.fused import GrpoParams
+
+    orig = GrpoParams.to_c
+
+    def to_c(self, write_grad):
+        c = orig(self, write_grad)
+        for k, v in fields.items():
+            setattr(c, k, v)
+        return c
+
+    monkeypatch.setattr(GrpoParams, "to_c", to_c)
 
 
 @pytest.fixture(params=list(F32_KERNELS))
 def f32_kernel(request, monkeypatch):
-    for k, v in F32_KERNELS[request.param].items():
-        monkeypatch.setenv(k, v)
+    _controls(monkeypatch, **F32_KERNELS[request.param])
     return request.param
 
 
@@ -276,7 +283,7 @@ def test_fp32_resident_targets_at_region_edges(ent, f32_kernel):
             assert rel_close(d[0, r, col], o["dlogits"][0, r, col], 1e-4, 1e-7)[0], col
 
 
-def test_fp32_resident_many_rows_per_workgroup_and_non_finite(f32_kernel):
+def test_fp32_resident_many_rows_per_workgroup_and_non_finite(f32_kernel, monkeypatch):
     """~2.3 rows per workgroup pair (hybrid: per workgroup) — rows with and without a successor,
     slots / the LDS slab reused row after row —, a -inf in each half of one row each; two runs
     bitwise identical (for the pair kernel also against the run that never waits: the partner's
@@ -300,13 +307,9 @@ def test_fp32_resident_many_rows_per_workgroup_and_non_finite(f32_kernel):
     _, _, d2 = _run(lg, b, dtype=torch.float32)
     assert np.array_equal(d1, d2)
     if f32_kernel == "pair":
-        import os
-
-        os.environ["PRL_PAIR_SPIN_TICKS"] = "0"
-        try:
+        with monkeypatch.context() as m:
+            _controls(m, pair_spin_ticks=-1)
             loss3, stats3, d3 = _run(lg, b, dtype=torch.float32)
-        finally:
-            del os.environ["PRL_PAIR_SPIN_TICKS"]
         assert np.array_equal(d1, d3) and loss3 == loss and stats3 == stats
 
 
@@ -375,19 +378,12 @@ def test_pair_kernels_beside_a_kernel_holding_cus(dtype, env, monkeypatch):
     assert rel_close(d0, o["dlogits"], *tol)[0]
 
     lib = _native.load()
-
-    def fallbacks() -> int:  # read and reset this stream's counter
-        n = ctypes.c_uint64(0)
-        assert lib.prl_grpo_pair_fallbacks(torch.cuda.current_device(),
-                                           ctypes.c_void_p(torch.cuda.current_stream().cuda_stream),
-                                           ctypes.byref(n)) == 0
-        return int(n.value)
-
+    fallbacks = _fallbacks_reader(lib)
     fallbacks()
     hog = torch.empty(1 << 30, dtype=torch.uint8, device=DEV)
     sink = torch.zeros(256, dtype=torch.int32, device=DEV)
     side = torch.cuda.Stream()
-    monkeypatch.setenv("PRL_PAIR_SPIN_TICKS", "2000")  # 20 us
+    _controls(monkeypatch, pair_spin_ticks=2000)  # 20 us
     model = LogitsModel(torch.tensor(lg, dtype=torch.float32).to(dtype).to(DEV))
     torch.cuda.synchronize()
     with torch.cuda.stream(side):  # ~50 ms of 128 workgroups reading 1 GiB at 20 GB/s
@@ -404,9 +400,89 @@ def test_pair_kernels_beside_a_kernel_holding_cus(dtype, env, monkeypatch):
     # test_*_many_rows_* take the from-HBM partial on every row); it must be readable and bounded
     assert 0 <= fallbacks() <= 2 * (T - 1)
     # the counter counts: the never-wait arm falls back on (almost) every row half
-    monkeypatch.setenv("PRL_PAIR_SPIN_TICKS", "0")
+    _controls(monkeypatch, pair_spin_ticks=-1)
     _run(lg, b, dtype=dtype)
     assert fallbacks() > 0
+
+
+def _fallbacks_reader(lib):
+    """prl_grpo_pair_fallbacks on the current stream's workspace (fused._workspace): read and reset."""
+    import ctypes
+
+    from pipelinerl_amd.finetune.rl.fused import _workspace
+
+    def fallbacks() -> int:
+        ws = _workspace(torch.device(DEV))
+        n = ctypes.c_uint64(0)
+        assert lib.prl_grpo_pair_fallbacks(ctypes.c_void_p(ws.data_ptr()), ws.numel(),
+                                           ctypes.c_void_p(torch.cuda.current_stream().cuda_stream),
+                                           ctypes.byref(n)) == 0
+        return int(n.value)
+
+    return fallbacks
+
+
+def test_pair_halves_far_apart_wait_once_not_every_row():
+    """The fp32 pair kernel's waits are bounded per launch, not per row (halves that
+    drift two or more rows apart used to wait the full 200 us spin on every remaining row, 64 rows x
+    200 us = 12.8 ms per half here).  8 192 rows (64 per pair) run beside a long GEMM on a side stream
+    that competes for the CUs: the launch costs about the GEMM's hold plus the rows, results
+    bit-identical to the uncontended launch (measured on MI355X: 2.15 ms alone, 3.89 ms beside a
+    2.34 ms GEMM, no fallback — the GEMM's tiles delay both halves of a pair alike).  Then a 10 ns
+    spin bound (pair_spin_ticks 1): halves time out on their first late partner, then only look for
+    the rest of the launch (the sticky no-wait path), computing partner partials from HBM — the same
+    bits."""
+    import dataclasses
+
+    from pipelinerl_amd import _native
+    from pipelinerl_amd.finetune.rl.fused import GrpoParams, grpo_loss, prepare_fields
+
+    lib = _native.load()
+    V, T = 151936, 8193
+    b = _batch(T, V, seed=23, lens=[4097, 4096], prompts=[1, 1])
+    lg = torch.randn((1, T, V), generator=torch.Generator(device=DEV).manual_seed(23), device=DEV) * 2
+    fields = prepare_fields(to_batch(b), DEV)
+    params = GrpoParams(policy_loss="ppo", epsilon=0.2, kl_coef=0.05, entropy_coef=0.0, clamp_log_ratio=5.0,
+                        temperature=1.0, batch_size=4.0)
+    fallbacks = _fallbacks_reader(lib)
+
+    def launch():
+        x = lg.detach().requires_grad_(True)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        loss, stats, rows = grpo_loss(x, fields, params)
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1), rows.clone(), stats.clone()
+
+    launch()
+    t0, rows0, stats0 = launch()
+    fallbacks()
+    ga = torch.randn((2048, 131072), device=DEV, dtype=torch.bfloat16)
+    gb = torch.randn((131072, 4096), device=DEV, dtype=torch.bfloat16)
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        torch.mm(ga, gb)  # warm the GEMM's kernel selection
+    torch.cuda.synchronize()
+    es0, es1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(side):
+        es0.record(side)
+        torch.mm(ga, gb)
+        es1.record(side)
+    t1, rows1, stats1 = launch()
+    torch.cuda.synchronize()
+    hold = es0.elapsed_time(es1)
+    fb = fallbacks()
+    print(f"uncontended {t0:.2f} ms, beside the {hold:.2f} ms hold {t1:.2f} ms, fallbacks {fb}")
+    assert torch.equal(rows0, rows1) and torch.equal(stats0, stats1)
+    assert t1 <= hold + 3 * t0 + 2.0, (t0, t1, hold, fb)
+    params1 = dataclasses.replace(params, pair_spin_ticks=1)
+    x = lg.detach().requires_grad_(True)
+    loss2, stats2, rows2 = grpo_loss(x, fields, params1)
+    torch.cuda.synchronize()
+    fb2 = fallbacks()
+    print(f"spin bound 10 ns: fallbacks {fb2} of {2 * (T - 1)} row halves")
+    assert torch.equal(rows0, rows2) and torch.equal(stats0, stats2)
 
 
 def test_claimed_rows_on_concurrent_streams():

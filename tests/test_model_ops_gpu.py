@@ -73,10 +73,9 @@ def test_swiglu(shape):
 
 def test_swiglu_phased_chunks_claimed_and_static():
     """The phased kernels at a size with many chunks per workgroup (4096 x 8960: 4480 forward chunks
-    for a 256-workgroup grid): claimed chunks (default) and the static stride (PRL_CHUNK_CLAIM=0)
-    give bit-identical outputs, equal to the eager forward."""
-    import os
-
+    for a 256-workgroup grid): chunks claimed from the caller's counter (the default) and the static
+    stride (no counter) give bit-identical outputs, equal to the eager forward."""
+    from pipelinerl_amd.finetune import model_ops
     from pipelinerl_amd.finetune.model_ops import SwiGLUFn
 
     g0 = torch.Generator(device=DEV).manual_seed(2)
@@ -84,16 +83,17 @@ def test_swiglu_phased_chunks_claimed_and_static():
     up = torch.randn((4096, 8960), generator=g0, device=DEV).to(torch.bfloat16)
     dh = torch.randn((4096, 8960), generator=g0, device=DEV).to(torch.bfloat16)
     outs = {}
+    orig = model_ops._chunk_counter
     for arm in ("claim", "static"):
         if arm == "static":
-            os.environ["PRL_CHUNK_CLAIM"] = "0"
+            model_ops._chunk_counter = lambda t: None
         try:
             gb, ub = gate.clone().requires_grad_(), up.clone().requires_grad_()
             hb = SwiGLUFn.apply(gb, ub)
             hb.backward(dh)
             torch.cuda.synchronize()
         finally:
-            os.environ.pop("PRL_CHUNK_CLAIM", None)
+            model_ops._chunk_counter = orig
         outs[arm] = (hb.detach(), gb.grad, ub.grad)
     for a, b in zip(outs["claim"], outs["static"]):
         assert torch.equal(a, b)

@@ -17,7 +17,6 @@ from __future__ import annotations
 import argparse
 import ctypes
 import json
-import os
 import sys
 from pathlib import Path
 
@@ -80,29 +79,22 @@ def main():
     lg.requires_grad_(True)
     sg, su = (torch.randn((65536, 8960), generator=g, device=dev).to(torch.bfloat16) for _ in range(2))
     sh, sdg, sdu = torch.empty_like(sg), torch.empty_like(sg), torch.empty_like(sg)
+    ctr = torch.zeros(4, dtype=torch.int32, device=dev)  # the SwiGLU chunk counter (caller-owned)
+    st = lambda: torch.cuda.current_stream().cuda_stream  # noqa: E731
     kernels = {
         "loss_head_fwd_8192_rows": lambda: grpo_loss(lg, fields, params),
-        # the same with the static row stride (PRL_ROW_CLAIM=0, read per launch)
-        "loss_head_fwd_8192_rows_static": lambda: (os.environ.__setitem__("PRL_ROW_CLAIM", "0"),
-                                                   grpo_loss(lg, fields, params),
-                                                   os.environ.pop("PRL_ROW_CLAIM")),
         # the phased SwiGLU kernels (one 1024-thread workgroup per CU) at the 1.5B step's C2 shape,
-        # chunks claimed and with the static stride (PRL_CHUNK_CLAIM=0, read per launch)
+        # chunks claimed from the counter and with the static stride (no counter)
         "swiglu_fwd_65536x8960": lambda: lib.prl_swiglu_forward(sg.data_ptr(), su.data_ptr(), sh.data_ptr(),
-                                                                sg.numel(), torch.cuda.current_stream().cuda_stream),
-        "swiglu_fwd_65536x8960_static": lambda: (os.environ.__setitem__("PRL_CHUNK_CLAIM", "0"),
-                                                 lib.prl_swiglu_forward(sg.data_ptr(), su.data_ptr(), sh.data_ptr(),
-                                                                        sg.numel(),
-                                                                        torch.cuda.current_stream().cuda_stream),
-                                                 os.environ.pop("PRL_CHUNK_CLAIM")),
+                                                                sg.numel(), ctr.data_ptr(), st()),
+        "swiglu_fwd_65536x8960_static": lambda: lib.prl_swiglu_forward(sg.data_ptr(), su.data_ptr(), sh.data_ptr(),
+                                                                       sg.numel(), None, st()),
         "swiglu_bwd_65536x8960": lambda: lib.prl_swiglu_backward(sh.data_ptr(), sg.data_ptr(), su.data_ptr(),
                                                                  sdg.data_ptr(), sdu.data_ptr(), sg.numel(),
-                                                                 torch.cuda.current_stream().cuda_stream),
-        "swiglu_bwd_65536x8960_static": lambda: (os.environ.__setitem__("PRL_CHUNK_CLAIM", "0"),
-                                                 lib.prl_swiglu_backward(sh.data_ptr(), sg.data_ptr(), su.data_ptr(),
-                                                                         sdg.data_ptr(), sdu.data_ptr(), sg.numel(),
-                                                                         torch.cuda.current_stream().cuda_stream),
-                                                 os.environ.pop("PRL_CHUNK_CLAIM")),
+                                                                 ctr.data_ptr(), st()),
+        "swiglu_bwd_65536x8960_static": lambda: lib.prl_swiglu_backward(sh.data_ptr(), sg.data_ptr(), su.data_ptr(),
+                                                                        sdg.data_ptr(), sdu.data_ptr(), sg.numel(),
+                                                                        None, st()),
         "gemm_fwd_gate_up": lambda: prl_gemm.linear_fwd(x, wgu),
         "gemm_dgrad_gate_up": lambda: prl_gemm.linear_dgrad(dy, wgu),
         "gemm_wgrad_gate_up": lambda: prl_gemm.linear_wgrad(dy, x),
