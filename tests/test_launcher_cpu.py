@@ -75,3 +75,48 @@ def test_reference_launcher_command_runs_the_entry_by_path(tmp_path):
     assert [ln["step"] for ln in lines] == [1, 2] and "rl/loss" in lines[-1]
     # both ranks ran (each logs to its own file)
     assert (fin / "logs" / "info_0.log").exists() and (fin / "logs" / "info_1.log").exists()
+
+
+def test_reference_default_deepspeed_config_unchanged_through_torchrun(tmp_path):
+    """The reference's DEFAULT exp_config — use_deepspeed true, deepspeed_config deepspeed_stage3_bf16,
+    bf16 weights (conf/base.yaml:94-96) — left unchanged, launched one process per rank (torchrun:
+    the launcher's accelerate --use_deepspeed needs DeepSpeed installed for accelerate itself, the
+    trainer never imports it).  The trainer honours it: DeepSpeed's gradient scale, fp32 master
+    weights and moments, and the ZeRO-3 layout decision logged (replicas here: a tiny model fits)."""
+    exp = tmp_path / "exp"
+    exp.mkdir()
+    world = 2
+    per_step, _ = _setup(exp, world)
+    raw = yaml.safe_load((GOLDEN / "exp_config_math_grpo.yaml").read_text())
+    assert raw["use_deepspeed"] is True and raw["deepspeed_config"] == "deepspeed_stage3_bf16"
+    raw["model_path"] = str(exp / "tiny_qwen2")
+    raw["streams"] = {"backend": "files"}
+    raw["finetune"].update(seq_length=28, train_batch_size=1, gradient_accumulation_passes=per_step,
+                           max_train_steps=2, learning_rate=1e-3, gradient_checkpointing=False,
+                           save_checkpoint_steps=100, log_each_n_steps=1, data_timeout_s=120)
+    (exp / "conf").mkdir()
+    (exp / "conf" / "exp_config.yaml").write_text(yaml.safe_dump(raw))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), str(ENTRY),
+           "--config-dir", f"{exp}/conf", "--config-name", "exp_config", f"output_dir={exp}",
+           f"hydra.run.dir={exp}/finetune", f"+me.weight_update_group_init_method=tcp://127.0.0.1:{free_port()}",
+           "+me.weight_update_group_world_size=2", "+me.llm_urls=http://127.0.0.1:1+http://127.0.0.1:2",
+           "finetune.send_weight_updates=False"]
+    env = dict(os.environ, PRL_TEST_CPU_STEP="1", OMP_NUM_THREADS="1", CUDA_VISIBLE_DEVICES="",
+               HIP_VISIBLE_DEVICES="",
+               PYTHONPATH=os.pathsep.join([str(ROOT / "tests" / "launcher_site"), os.environ.get("PYTHONPATH", "")]))
+    r = subprocess.run(cmd, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-6000:])
+    fin = exp / "finetune"
+    assert json.loads((fin / "summary.json").read_text())["completed_steps"] == 2
+    log = (fin / "logs" / "info_0.log").read_text()
+    assert "model state layout: replicas (DeepSpeed ZeRO-3 config" in log, log[-2000:]
+    assert "fp32 master weights + fp32 AdamW moments" in log
+    import torch
+
+    st = torch.load(fin / "training_state" / "training_state.pt", weights_only=True)
+    s0 = st["optimizer_state"]["state"][0]
+    assert s0["master"].dtype == torch.float32 and s0["exp_avg"].dtype == torch.float32
+    from safetensors.torch import load_file
+
+    assert {t.dtype for t in load_file(str(fin / "current" / "model.safetensors")).values()} == {torch.bfloat16}
