@@ -136,13 +136,41 @@ def fp32_loss_head_probe(T: int, V: int, device, iters: int = 8, warmup: int = 2
             if arm == "pair":
                 fb += fallbacks()
                 pair_launches += warmup + iters
+    # beside 16 resident side workgroups reading at one xGMI link's rate (an RCCL collective's
+    # channels beside the loss head): the pair kernel's time, and its extra HBM reads — every row
+    # half that computed its partner's partial itself re-read that half row (V/2 x 4 B); PMC counting
+    # serialises kernels, so the extra traffic comes from the kernel's own fallback counter
+    side = torch.cuda.Stream(device=device)
+    src = torch.empty(4 << 30, dtype=torch.uint8, device=device)
+    sink = torch.zeros(16, dtype=torch.int32, device=device)
+    lib = _native.load()
+    fallbacks()
+    side_ms: list[float] = []
+    for i in range(warmup + iters):
+        logits.grad = None
+        side.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(side):  # ~26 ms of reads at 153 GB/s: covers the launch
+            _native.check(lib.prl_paced_read(ctypes.c_void_p(src.data_ptr()), 4 << 30, 153.0, 16,
+                                             ctypes.c_void_p(sink.data_ptr()), side.cuda_stream), "prl_paced_read")
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        loss, stats, _ = grpo_loss(logits, fields, params)
+        e1.record()
+        loss.backward()
+        stats.cpu()
+        torch.cuda.synchronize(device)
+        if i >= warmup:
+            side_ms.append(e0.elapsed_time(e1))
+    fb_side = fallbacks() / (warmup + iters)
+    del src
     ms = float(np.median(times["pair"]))
     ms_h = float(np.median(times["hybrid"]))
     alg = 2.0 * T * V * 4 + SIDE_BYTES_PER_TOKEN * T
     del logits, fields
     torch.cuda.empty_cache()
     traffic = traffic_h = None  # HBM bytes per launch from the committed PMC passes (tools/profile_bench.sh)
-    src = "r05_fp32_pmc.json"
+    pmcs = sorted((ROOT / "profiles").glob("r*_fp32_pmc.json"))  # the newest round's passes
+    src = pmcs[-1].name if pmcs else "r05_fp32_pmc.json"
     try:
         pmc = json.loads((ROOT / "profiles" / src).read_text())["per_launch_median"]
         if T == 65536 and V == 151936:
@@ -161,6 +189,12 @@ def fp32_loss_head_probe(T: int, V: int, device, iters: int = 8, warmup: int = 2
             "tokens_per_s": round(T / ms * 1e3, 1), "iters": iters * rounds,
             "pair_fallbacks_per_launch": round(fb / max(1, pair_launches), 3),
             "pair_row_halves_per_launch": 2 * T,
+            "beside_16_side_workgroups": {
+                "side": "prl_paced_read, 16 workgroups at 153 GB/s on another stream, launched with each call",
+                "kernel_ms": round(float(np.median(side_ms)), 4),
+                "fallbacks_per_launch": round(fb_side, 2),
+                "traffic_over_algorithmic": (round((traffic + fb_side * (V // 2) * 4) / alg, 4) if traffic else None),
+                "traffic_basis": "PMC per-launch traffic (serialised) + fallback half rows x V/2 x 4 B re-read"},
             "hybrid": {"kernel": "grpo_fwd_hybrid_f32<19, 9> (f32_rows=1, alternated)", "kernel_ms": round(ms_h, 4),
                        "frac": round(alg / ms_h / 1e6 / HBM_PEAK_GBS, 4),
                        "traffic_over_algorithmic": round(traffic_h / alg, 4) if traffic_h else None}}
