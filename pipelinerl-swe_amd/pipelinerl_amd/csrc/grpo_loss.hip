@@ -694,12 +694,14 @@ __global__ __launch_bounds__(BLOCK) void grpo_fwd_stream(KArgs a) {
 constexpr int kHybNR = PRL_HYB_NR, kHybNL = PRL_HYB_NL;
 typedef __attribute__((address_space(3))) void lds_void_t;
 // d = p (alpha + beta t) (+ gadd at the target column) of one fp32 vector, stored at voff + soff of
-// the dlogits row.  ``rel`` = target column - the vector's first column (in [0, 4) for the one lane
-// that owns it).  The offsets come as one per-lane VGPR plus a wave-uniform SGPR and the target as
-// a uniform difference: per-vector lane addresses would be hoisted out of the row loop as
-// loop invariants (3 VGPRs per resident vector: what spilled the first version).  The store is
-// store_row_b128 (fenced: SGPR soffset, see its comment).
-__device__ __forceinline__ void hyb_store(__amdgpu_buffer_rsrc_t ws, int voff, int soff, int rel, f32x4 x,
+// the dlogits row.  ``hit``: this lane's vector holds the target, at element ``jt`` (uniform).  The
+// offsets come as one per-lane VGPR plus a wave-uniform SGPR, and the target test as a row-uniform
+// vector index against a per-row lane flag (target_lane): per-vector lane addresses — or a
+// per-vector ``lane column + k * 4096`` to compare the target with — are loop invariants the
+// compiler hoists out of the row loop, one VGPR per resident vector (what spilled the first version,
+// and, as 18 reloads per row from scratch, the round-5 pair kernel: ~9 GB of extra reads per C2
+// launch).  The store is store_row_b128 (fenced: SGPR soffset, see its comment).
+__device__ __forceinline__ void hyb_store(__amdgpu_buffer_rsrc_t ws, int voff, int soff, bool hit, int jt, f32x4 x,
                                          bool zero_row, float c, float M, float l2s, float alpha, float beta,
                                          float gadd) {
   f32x4 d = {0.f, 0.f, 0.f, 0.f};
@@ -708,10 +710,24 @@ __device__ __forceinline__ void hyb_store(__amdgpu_buffer_rsrc_t ws, int voff, i
     for (int j = 0; j < 4; ++j) {
       const float t = __builtin_fmaf(x[j] - M, c, -l2s);
       d[j] = fexp2(t) * __builtin_fmaf(beta, t, alpha);
-      if (j == rel) d[j] += gadd;
+      if (hit && j == jt) d[j] += gadd;
     }
   }
   store_row_b128(__builtin_bit_cast(u32x4, d), ws, voff, soff);
+}
+// A row's target relative to a resident block's first column, trel (uniform; < 0: none): it sits in
+// the block's vector trel >> 12 (1024 lanes x 4 columns), lane (trel >> 2) & 1023, element trel & 3.
+struct TargetPos {
+  int kt;     // vector index (negative: none)
+  int jt;     // element
+  bool lane;  // this lane owns it
+};
+__device__ __forceinline__ TargetPos target_pos(int trel, int tid) {
+  TargetPos t;
+  t.kt = trel < 0 ? -1 : (trel >> 12);
+  t.jt = trel & 3;
+  t.lane = ((trel >> 2) & 1023) == tid;
+  return t;
 }
 template <int NR, int NL>
 __global__ __launch_bounds__(1024) void grpo_fwd_hybrid_f32(KArgs a) {
@@ -812,14 +828,15 @@ __global__ __launch_bounds__(1024) void grpo_fwd_hybrid_f32(KArgs a) {
       const float beta = -core.g_h * kLn2 * inv_t;
       const float gadd = core.g_lp * inv_t;
       const bool zero_row = (core.g_lp == 0.f && core.g_h == 0.f);
-      const int lcol = tid * 4;
+      const TargetPos tp = target_pos(tgt, tid);
 #pragma unroll
       for (int k = 0; k < NR; ++k)
-        hyb_store(ws, voff, k * VSTRIDE, (tgt - k * BLOCK * 4) - lcol, buf[k], zero_row, c, M, l2s, alpha, beta, gadd);
+        hyb_store(ws, voff, k * VSTRIDE, tp.lane && k == tp.kt, tp.jt, buf[k], zero_row, c, M, l2s, alpha, beta, gadd);
 #pragma unroll
       for (int k = 0; k < NL; ++k)
-        hyb_store(ws, voff, (NR + k) * VSTRIDE, (tgt - (NR + k) * BLOCK * 4) - lcol, slab[k][tid], zero_row, c, M, l2s,
+        hyb_store(ws, voff, (NR + k) * VSTRIDE, tp.lane && NR + k == tp.kt, tp.jt, slab[k][tid], zero_row, c, M, l2s,
                   alpha, beta, gadd);
+      const int vt = tgt < 0 ? -1 : (tgt >> 2);  // the target's vector (tail: per-lane compare)
       int g2 = kTail0 + tid;
       for (; g2 + (U - 1) * BLOCK < nvec; g2 += U * BLOCK) {
         f32x4 x[U];
@@ -828,12 +845,12 @@ __global__ __launch_bounds__(1024) void grpo_fwd_hybrid_f32(KArgs a) {
           x[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, g2 * 16, u * VSTRIDE, kLoadAux));
 #pragma unroll
         for (int u = 0; u < U; ++u)
-          hyb_store(ws, g2 * 16, u * VSTRIDE, (tgt - u * BLOCK * 4) - g2 * 4, x[u], zero_row, c, M, l2s, alpha, beta,
+          hyb_store(ws, g2 * 16, u * VSTRIDE, g2 + u * BLOCK == vt, tp.jt, x[u], zero_row, c, M, l2s, alpha, beta,
                     gadd);
       }
       for (; g2 < nvec; g2 += BLOCK) {
         const f32x4 x = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, g2 * 16, 0, kLoadAux));
-        hyb_store(ws, g2 * 16, 0, tgt - g2 * 4, x, zero_row, c, M, l2s, alpha, beta, gadd);
+        hyb_store(ws, g2 * 16, 0, g2 == vt, tp.jt, x, zero_row, c, M, l2s, alpha, beta, gadd);
       }
     }
     // the next row's DMA overwrites this lane's slab slots only after its own reads above (same
@@ -850,62 +867,83 @@ __global__ __launch_bounds__(1024) void grpo_fwd_hybrid_f32(KArgs a) {
 // store of {m, s, w, tag} by one lane, sc1 polls by the partner's lane 0 (the data-tagged hand-off
 // of MI355X_MICROARCH.md's price list, handoff-1to1) — and both combine the two partials in half
 // order, so both hold bit-identical row statistics.  Pairs are blocks b and b ^ 8 (one XCD under the
-// round-robin placement: speed only).  Every spin is bounded: a half whose partner has not published
-// within PairArgs::spin_ticks of the realtime clock (100 MHz) computes the partner's partial itself
-// from HBM (the same loads and arithmetic in the same order: the same bits), so a launch that shares
-// the chip with other kernels still completes.  Slots are zeroed by the host before each launch
-// (tag = the pair's row iteration + 1).  A half waits at most once per launch: after a timeout it
-// only looks (one load) for the rest of the launch, and it never waits for a partner whose tag is
-// already past this row's (two or more rows ahead, it has overwritten the row's parity slot) — so
-// halves that drift apart cost one spin, not one per row.
+// round-robin placement: speed only).
+//
+// Rows are claimed (round 6), so a pair whose CUs are held by another queue's kernel (an RCCL
+// channel, a side-stream kernel) takes fewer rows instead of finishing a static share after everyone
+// else: the LEADER (half 0) claims the pair's next row from a counter at the top of each row (its
+// latency hides behind the row's loads) and publishes it in the pair's claim granule {row, 0, tag}
+// right before its partial; the PARTNER loads that granule after the exchange and uses it after its
+// gradient pass (by then it has landed), so the claim costs the pair no wait.  Every wait is
+// bounded: a half whose partner has not published within PairArgs::spin_ticks of the realtime clock
+// (100 MHz) goes SOLO for the rest of the launch — it computes the partner's partial from HBM (the
+// same loads and arithmetic in the same order: the same bits), writes the partner half's gradient
+// streamed from HBM too, claims its own rows, and marks its own partial slots with kSoloTag so a
+// partner that arrives later goes SOLO at its next exchange instead of waiting.  A row two halves
+// both finish is written twice with the same bits.  A pair that starts after the rows are claimed
+// exits at its first claim.  Slots and the counter are zeroed by the host before each launch.
 struct PairArgs {
-  uint32_t* slots;      // [pairs][2 halves][2 parities] x 4 words {m, s, w, tag}
+  uint32_t* slots;      // [pairs] x kPairSlotStride: partials {m, s, w, tag} [2 halves][2 parities], claims {row lo, row hi, 0, tag} [2 parities]
+  uint32_t* row_ctr;    // rows claimed so far
   int64_t slot_bytes;   // bytes of the slot array (its buffer descriptor's range)
-  int64_t spin_ticks;   // realtime ticks a half waits for its partner before computing its partial
-  uint32_t* fallbacks;  // rows whose partner partial a half computed itself (one vector atomic each)
+  int64_t spin_ticks;   // realtime ticks a half waits for its partner before going SOLO
+  uint32_t* fallbacks;  // rows whose other half a SOLO half streamed (one vector atomic each)
 };
 #ifndef PRL_PAIR_SPIN_TICKS
 #define PRL_PAIR_SPIN_TICKS 20000  // 200 us
 #endif
 constexpr int kPairMinNV = 8, kPairMaxNV = 19;  // above 19 the registers spill (hybrid kernel there)
 constexpr int kSc1 = 16;  // aux bit of buffer_load / buffer_store: sc1 (bypass the CU's L1; write through)
+constexpr int kPairSlotStride = 96;
+#ifndef PRL_PAIR_PERMUTE
+#define PRL_PAIR_PERMUTE 0
+#endif
+// The pair kernel visits rows in claim order: perm_row's 64-bit modulo kept two loop invariants
+// (the row count as floats) and a loop-carried value in registers the kernel does not have, so
+// they went to scratch and back every row (2.7 % extra writes, more reads: profiles/r06_fp32_calibration.json)
+__device__ __forceinline__ int64_t pair_row(int64_t i, int64_t n) {
+#if PRL_PAIR_PERMUTE
+  return perm_row(i, n);
+#else
+  (void)n;
+  return i;
+#endif
+}
+constexpr uint32_t kSoloTag = 0xFFFFFFFFu;  // a partial slot's tag once its half went SOLO
 
-// One lane of each half: publish this half's partial as one 16-B sc1 granule {m, s, w, tag} (a
-// single vector store: never torn, written through to memory), then poll the partner's granule with
-// sc1 loads until it carries this row's tag or spin_ticks of the realtime clock have passed (no wait
-// when spin_ticks is 0, or when the partner's tag is already past this row's); the partner's words
-// and whether they arrived go to `out` (LDS) for the whole workgroup.  The realtime clock is read
-// once per 8 polls (a tight clock loop delays other kernels' starts; flat_pack.hip paced_read_kernel),
-// s_sleep between polls.
-__device__ __forceinline__ void pair_exchange(__amdgpu_buffer_rsrc_t slots, int mine_off, int partner_off, uint32_t tag,
-                                              Lse mine, int64_t spin_ticks, uint32_t* out) {
-  const u32x4 g = {__float_as_uint(mine.m), __float_as_uint(mine.s), __float_as_uint(mine.w), tag};
+__device__ __forceinline__ u32x4 load_slot(__amdgpu_buffer_rsrc_t slots, int off) {
+  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(slots, off, 0, kSc1));
+}
+__device__ __forceinline__ void store_slot(__amdgpu_buffer_rsrc_t slots, int off, u32x4 g) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, g), slots,
-                                         mine_off, 0, kSc1);
-  u32x4 v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(slots, partner_off, 0, kSc1));
-  if (v[3] != tag && spin_ticks > 0) {
+                                         off, 0, kSc1);
+}
+// One lane: poll the granule at `off` (first look already in v) with sc1 loads until it carries
+// `tag`, or kSoloTag, or a tag past `tag` (its writer is ahead), or spin_ticks of the realtime clock
+// have passed (no wait when spin_ticks is 0).  The clock is read once per 8 polls (a tight clock loop
+// delays other kernels' starts; flat_pack.hip paced_read_kernel), s_sleep between polls.
+__device__ __forceinline__ u32x4 poll_slot(__amdgpu_buffer_rsrc_t slots, int off, uint32_t tag, int64_t spin_ticks,
+                                           u32x4 v) {
+  auto waiting = [&](const u32x4& x) { return x[3] != tag && x[3] != kSoloTag && (int32_t)(x[3] - tag) < 0; };
+  if (waiting(v) && spin_ticks > 0) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     bool more = true;
     while (more) {
 #pragma unroll 1
-      for (int k = 0; k < 8 && v[3] != tag && (int32_t)(v[3] - tag) < 0; ++k) {
+      for (int k = 0; k < 8 && waiting(v); ++k) {
         __builtin_amdgcn_s_sleep(2);
         asm volatile("" ::: "memory");  // a fresh load every turn
-        v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(slots, partner_off, 0, kSc1));
+        v = load_slot(slots, off);
       }
-      more = v[3] != tag && (int32_t)(v[3] - tag) < 0 &&
-             (int64_t)(__builtin_amdgcn_s_memrealtime() - t0) < spin_ticks;
+      more = waiting(v) && (int64_t)(__builtin_amdgcn_s_memrealtime() - t0) < spin_ticks;
     }
   }
-  out[0] = v[0];
-  out[1] = v[1];
-  out[2] = v[2];
-  out[3] = v[3] == tag ? 1u : 0u;
+  return v;
 }
 
 // the (m, s, w) state of a half row: its NV vectors per lane from registers (FROM_REGS) or streamed
 // from HBM in the same order, then the wave and block reductions.  The same code computes both, so a
-// half's own partial and the one its partner computes for it on a timeout are the same bits.
+// half's own partial and the one a SOLO half computes for its partner are the same bits.
 template <int NV, bool FROM_REGS>
 __device__ __forceinline__ Lse half_state(const f32x4 (&buf)[NV], __amdgpu_buffer_rsrc_t rs, int voff, bool last_ok,
                                           float c, float (*red)[3], int lane, int wid) {
@@ -947,23 +985,51 @@ __device__ __forceinline__ Lse half_state(const f32x4 (&buf)[NV], __amdgpu_buffe
   return block_combine<NW>(red, c);
 }
 
+// the same from the lane's byte offset voff = 16 x its thread index
+__device__ __forceinline__ TargetPos target_pos_v(int trel, int voff) {
+  TargetPos t;
+  t.kt = trel < 0 ? -1 : (trel >> 12);
+  t.jt = trel & 3;
+  t.lane = ((trel << 2) & (1023 << 4)) == voff;
+  return t;
+}
+// a SOLO half's gradient pass over the OTHER half of its row, streamed from HBM (rare path)
+template <int NV>
+__device__ __forceinline__ void half_grad_stream(__amdgpu_buffer_rsrc_t rs, __amdgpu_buffer_rsrc_t ws, int voff,
+                                                 TargetPos tp, bool zero_row, float c, float M, float l2s, float alpha, float beta,
+                                                 float gadd) {
+  constexpr int BLOCK = 1024, VSTRIDE = BLOCK * 16, U = 2;
+#pragma unroll
+  for (int k0 = 0; k0 < NV; k0 += U) {
+    f32x4 t[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (k0 + u < NV) t[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, (k0 + u) * VSTRIDE, kLoadAux));
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (k0 + u < NV) hyb_store(ws, voff, (k0 + u) * VSTRIDE, tp.lane && k0 + u == tp.kt, tp.jt, t[u], zero_row, c, M, l2s,
+                                 alpha, beta, gadd);
+  }
+}
+
 template <int NV>
 __global__ __launch_bounds__(1024) void grpo_fwd_pair_f32(KArgs a, PairArgs pa) {
   constexpr int BLOCK = 1024, NW = BLOCK / 64, VSTRIDE = BLOCK * 16;
   __shared__ float red[2][NW][3];
-  __shared__ float red2[NW][3];   // the partner partial, when this half computes it
+  __shared__ float red2[NW][3];   // the other half's partial, when this half computes it
   __shared__ uint32_t xch[2][4];  // the partner's published partial and whether it arrived
+  __shared__ int64_t next_row[2]; // the row after this one (by parity)
+  __shared__ int solo_sh;         // this half went SOLO
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int b = blockIdx.x;
-  const int h = (b >> 3) & 1;                          // which half of the row
-  const int64_t npairs = gridDim.x >> 1;               // the host launches a multiple of 16 blocks
-  const int64_t p = (int64_t)(b >> 4) * 8 + (b & 7);   // pair: blocks b and b ^ 8
+  const int h = (b >> 3) & 1;                          // which half of the row (0: the leader)
+  const int64_t p = (int64_t)(b >> 4) * 8 + (b & 7);   // pair: blocks b and b ^ 8 (the host launches a multiple of 16)
   const int64_t nrows = fwd_rows(a);
   const int nvec = (int)(a.V >> 2);
   const int n0 = (nvec + 1) >> 1;                      // half 0: vectors [0, n0), half 1: [n0, nvec)
   const int nmine = h ? nvec - n0 : n0, npart = h ? n0 : nvec - n0;
   const int64_t off_mine = h ? (int64_t)n0 * 16 : 0, off_part = h ? 0 : (int64_t)n0 * 16;
-  const int col0 = h ? n0 * 4 : 0;                     // first column of this half
+  const int col0 = h ? n0 * 4 : 0, col0_part = h ? 0 : n0 * 4;  // first column of each half
   const float c = kLog2e / a.temperature;
   const float inv_t = 1.0f / a.temperature;
   const float* lg = static_cast<const float*>(a.logits);
@@ -972,27 +1038,71 @@ __global__ __launch_bounds__(1024) void grpo_fwd_pair_f32(KArgs a, PairArgs pa) 
   const bool last_ok = (NV - 1) * BLOCK + tid < nmine;  // only vector NV-1 can be partial
   const bool last_ok_part = (NV - 1) * BLOCK + tid < npart;
   const auto slots = __builtin_amdgcn_make_buffer_rsrc(pa.slots, 0, (int)pa.slot_bytes, 0x00020000);
-  const int my_slot = (int)((p * 2 + h) * 2) * 16, partner_slot = (int)((p * 2 + (h ^ 1)) * 2) * 16;
+  const int pbase = (int)p * kPairSlotStride;
+  auto part_off = [&](int half, int par) { return pbase + (half * 2 + par) * 16; };
+  auto claim_off = [&](int par) { return pbase + 64 + par * 16; };
   f32x4 buf[NV];
   auto half_rsrc = [&](int64_t lrow, int64_t off, int n) {
     return row_rsrc(reinterpret_cast<const char*>(lg + lrow * a.ld) + off, (int64_t)n * 16);
   };
-  int64_t i = p;
-  if (i < nrows) {
+  auto load_half = [&](int64_t row) {
     int64_t lrow, tok, qo;
-    map_row(a, perm_row(i, nrows), lrow, tok, qo);
+    map_row<RowLd>(a, pair_row(row, nrows), lrow, tok, qo);
     const auto rs = half_rsrc(lrow, off_mine, nmine);
 #pragma unroll
     for (int k = 0; k < NV; ++k)
       buf[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, k * VSTRIDE, kLoadAux));
+  };
+  // lane 0 of a half going SOLO: mark both of its partial slots so the partner stops waiting on it
+  auto mark_solo = [&]() {
+    const u32x4 g = {0u, 0u, 0u, kSoloTag};
+    store_slot(slots, part_off(h, 0), g);
+    store_slot(slots, part_off(h, 1), g);
+  };
+  auto uniform64 = [](int64_t v) {
+    return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
+                     (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)v));
+  };
+
+  // ---- the first row: the leader claims it, the partner follows (or goes SOLO after spin_ticks)
+  if (tid == 0) {
+    int solo = 0;
+    int64_t r;
+    if (h == 0) {
+      r = (int64_t)atomicAdd(pa.row_ctr, 1u);
+      store_slot(slots, claim_off(0), u32x4{(uint32_t)r, (uint32_t)(r >> 32), 0u, 1u});
+    } else {
+      const u32x4 v = poll_slot(slots, claim_off(0), 1u, pa.spin_ticks, load_slot(slots, claim_off(0)));
+      if (v[3] == 1u) {
+        r = (int64_t)(((uint64_t)v[1] << 32) | v[0]);
+      } else {
+        solo = 1;
+        mark_solo();
+        r = (int64_t)atomicAdd(pa.row_ctr, 1u);
+      }
+    }
+    next_row[1] = r;
+    solo_sh = solo;
   }
-  uint32_t it = 0;
-  int64_t spin = pa.spin_ticks;  // lane 0's wait budget: one spin per launch (see above)
-  for (; i < nrows; i += npairs, ++it) {
+  __syncthreads();
+  int64_t i = uniform64(next_row[1]);
+  bool solo = __builtin_amdgcn_readfirstlane(solo_sh) != 0;
+  if (i < nrows) load_half(i);
+  for (uint32_t it = 0; i < nrows; ++it) {
     const int par = (int)(it & 1);
     const uint32_t tag = it + 1;
+    // this lane's identity, opaque per row: what derives from it (wave, lane, lane-0 flag, the
+    // target test) is recomputed here instead of hoisted out of the loop into registers the kernel
+    // does not have (they went to scratch and back every row)
+    int vo = voff;
+    asm volatile("" : "+v"(vo));
+    const int lane_r = (vo >> 4) & 63, wid_r = vo >> 10;
+    const bool t0 = vo == 0;
+    // the next row's claim (leader or SOLO): one vector atomic, its latency behind the row's loads
+    uint32_t claim = 0;
+    if (t0 && (h == 0 || solo)) claim = atomicAdd(pa.row_ctr, 1u);
     int64_t lrow, tok, qo;
-    map_row<RowLd>(a, perm_row(i, nrows), lrow, tok, qo);
+    map_row<RowLd>(a, pair_row(i, nrows), lrow, tok, qo);
     const int64_t tid_raw = RowLd::ld(a.input_ids, tok);
     TokIn tin = tok_in<RowLd>(a, tok);
     const bool bad_id = (uint64_t)tid_raw >= (uint64_t)a.V;
@@ -1001,19 +1111,33 @@ __global__ __launch_bounds__(1024) void grpo_fwd_pair_f32(KArgs a, PairArgs pa) 
     pin_sgpr(tin, xr);
     const float xt = bad_id ? __builtin_nanf("") : xr;
 
-    // ---- pass 1: this half's state from registers, published for the partner
-    const Lse mine = half_state<NV, true>(buf, slots, voff, last_ok, c, red[par], lane, wid);  // (rsrc unused)
-    if (tid == 0) {
-      pair_exchange(slots, my_slot + par * 16, partner_slot + par * 16, tag, mine, spin, xch[par]);
-      if (!xch[par][3]) spin = 0;  // the partner was late once: only look from now on
+    // ---- pass 1: this half's state from registers, published for the partner (with the claim)
+    const Lse mine = half_state<NV, true>(buf, slots, voff, last_ok, c, red[par], lane_r, wid_r);  // (rsrc unused)
+    if (t0) {
+      int arrived = 0;
+      if (!solo) {
+        if (h == 0) store_slot(slots, claim_off(par ^ 1), u32x4{claim, 0u, 0u, tag + 1});
+        store_slot(slots, part_off(h, par), u32x4{__float_as_uint(mine.m), __float_as_uint(mine.s), __float_as_uint(mine.w), tag});
+        const u32x4 v = poll_slot(slots, part_off(h ^ 1, par), tag, pa.spin_ticks, load_slot(slots, part_off(h ^ 1, par)));
+        arrived = v[3] == tag;
+        xch[par][0] = v[0];
+        xch[par][1] = v[1];
+        xch[par][2] = v[2];
+        if (!arrived) mark_solo();  // the partner is late or SOLO: this half goes SOLO
+      }
+      xch[par][3] = (uint32_t)arrived;
+      if (h == 0 || solo) next_row[par] = (int64_t)claim;  // (a partner that just went SOLO claims after pass 2)
     }
     __syncthreads();
+    const bool paired = __builtin_amdgcn_readfirstlane((int)xch[par][3]) != 0;
+    const bool was_solo = solo;
+    solo = !paired;
     Lse part;
-    if (xch[par][3]) {
+    if (paired) {
       part = Lse{__uint_as_float(xch[par][0]), __uint_as_float(xch[par][1]), __uint_as_float(xch[par][2])};
-    } else {  // the partner is late (not resident, or behind): its partial from HBM (block-uniform branch)
-      part = half_state<NV, false>(buf, half_rsrc(lrow, off_part, npart), voff, last_ok_part, c, red2, lane, wid);
-      if (tid == 0) atomicAdd(pa.fallbacks, 1u);
+    } else {  // SOLO: the other half's partial from HBM (block-uniform branch)
+      part = half_state<NV, false>(buf, half_rsrc(lrow, off_part, npart), voff, last_ok_part, c, red2, lane_r, wid_r);
+      if (t0) atomicAdd(pa.fallbacks, 1u);
     }
     const Lse tot = h == 0 ? lse_combine(mine, part, c) : lse_combine(part, mine, c);
     const float l2s = log2f(tot.s);
@@ -1021,33 +1145,52 @@ __global__ __launch_bounds__(1024) void grpo_fwd_pair_f32(KArgs a, PairArgs pa) 
     const float lse = M * inv_t + kLn2 * l2s;
     const float H = kLn2 * (l2s - tot.w / tot.s);
     const float lp = (xt - M) * inv_t - kLn2 * l2s;
-    const TokGrad core = row_epilogue(a, qo, tin, lp, H, lse, M, l2s, h == 0 && tid == 0);
+    const TokGrad core = row_epilogue(a, qo, tin, lp, H, lse, M, l2s, (h == 0 || solo) && t0);
 #pragma unroll
     for (int k = 0; k < NV; ++k) asm volatile("" : "+v"(buf[k]));
 
-    // ---- pass 2: this half's gradient from registers, then (stores retired) the next half-row
-    const int64_t in = i + npairs;
-    const bool has_next = in < nrows;
+    // ---- pass 2: this half's gradient from registers (SOLO: the other half's streamed), then the
+    // next row (stores retired) — the partner learns it from the claim granule, loaded behind its
+    // stores (the load's latency hides in their drain; nothing holds it through the pass)
     if (a.write_grad) {
       const auto ws = row_rsrc(reinterpret_cast<char*>(dl + lrow * a.ld) + off_mine, (int64_t)nmine * 16);
       const float alpha = -(core.g_lp + core.g_h * H) * inv_t;
       const float beta = -core.g_h * kLn2 * inv_t;
       const float gadd = core.g_lp * inv_t;
       const bool zero_row = (core.g_lp == 0.f && core.g_h == 0.f);
-      const int rel0 = (int)(tgt < 0 ? -(1 << 30) : tgt - col0) - tid * 4;  // target - this lane's first column
+      const TargetPos tp = target_pos_v((int)(tgt < 0 ? -1 : tgt - col0), vo);  // (other half: trel < 0)
 #pragma unroll
       for (int k = 0; k < NV; ++k)
-        hyb_store(ws, voff, k * VSTRIDE, rel0 - k * BLOCK * 4, buf[k], zero_row, c, M, l2s, alpha, beta, gadd);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        hyb_store(ws, voff, k * VSTRIDE, tp.lane && k == tp.kt, tp.jt, buf[k], zero_row, c, M, l2s, alpha, beta, gadd);
+      if (solo) {
+        const auto wo = row_rsrc(reinterpret_cast<char*>(dl + lrow * a.ld) + off_part, (int64_t)npart * 16);
+        const TargetPos tq = target_pos_v((int)(tgt < 0 ? -1 : tgt - col0_part), vo);
+        half_grad_stream<NV>(half_rsrc(lrow, off_part, npart), wo, voff, tq, zero_row, c, M, l2s, alpha, beta, gadd);
+      }
     }
-    if (has_next) {
-      int64_t nl, nt, nq;
-      map_row<RowLd>(a, perm_row(in, nrows), nl, nt, nq);
-      const auto rn = half_rsrc(nl, off_mine, nmine);
-#pragma unroll
-      for (int k = 0; k < NV; ++k)
-        buf[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rn, voff, k * VSTRIDE, kLoadAux));
+    const bool follow = h == 1 && !was_solo;  // the partner (block-uniform): its next row from the claim granule
+    u32x4 cv = {0u, 0u, 0u, 0u};
+    if (follow && !solo && t0) cv = load_slot(slots, claim_off(par ^ 1));
+    if (a.write_grad) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (follow) {
+      if (t0) {
+        int64_t r;
+        const u32x4 v = solo ? cv : poll_slot(slots, claim_off(par ^ 1), tag + 1, pa.spin_ticks, cv);
+        if (!solo && v[3] == tag + 1) {
+          r = (int64_t)(((uint64_t)v[1] << 32) | v[0]);
+        } else {
+          if (!solo) mark_solo();
+          solo_sh = 1;
+          r = (int64_t)atomicAdd(pa.row_ctr, 1u);
+        }
+        next_row[par] = r;
+        if (solo) solo_sh = 1;
+      }
+      __syncthreads();
+      solo = solo || __builtin_amdgcn_readfirstlane(solo_sh) != 0;
     }
+    i = uniform64(next_row[par]);
+    if (i < nrows) load_half(i);
   }
 }
 
@@ -1309,13 +1452,14 @@ static hipError_t launch_resident_nv(int nv, const KArgs& a, int grid, hipStream
 }
 
 // The caller's workspace (prl_grpo_workspace_bytes): the statistics' per-block partials, then the
-// row kernels' scratch — the fp32 pair kernel's hand-off slots ([pairs][2][2] granules of 16 B for up
-// to 1024 CUs, zeroed before each pair launch), its fallback counter (accumulated over launches;
+// row kernels' scratch — the fp32 pair kernel's row counter (16 B) and hand-off slots
+// (kPairSlotStride bytes per pair for up to 1024 CUs; both zeroed before each pair launch), its
+// fallback counter (accumulated over launches;
 // prl_grpo_pair_fallbacks reads and resets it) and the resident kernel's row counter (zeroed before
 // each launch).  No library-held device memory: a workspace serves one stream at a time.
 constexpr int kPairMaxCUs = 1024;
 constexpr size_t kPartialsBytes = sizeof(double) * (size_t)kMaxGrid * PRL_NSTAT;
-constexpr size_t kPairSlotBytes = (size_t)(kPairMaxCUs / 2) * 2 * 2 * 16;
+constexpr size_t kPairSlotBytes = 16 + (size_t)(kPairMaxCUs / 2) * kPairSlotStride;
 constexpr size_t kPairCounterBytes = 16;
 constexpr size_t kRowCounterBytes = 16;
 constexpr size_t kWorkspaceBytes = kPartialsBytes + kPairSlotBytes + kPairCounterBytes + kRowCounterBytes;
@@ -1372,11 +1516,13 @@ static hipError_t launch_pair_rows(const KArgs& a, int nv, int64_t nrows, int cu
   if (grid > cus) grid = cus / 16 * 16;
   if (grid < 16) grid = 16;
   PairArgs pa{};
-  pa.slots = sc.slots;
-  pa.slot_bytes = (int64_t)kPairSlotBytes;
+  pa.row_ctr = sc.slots;
+  pa.slots = sc.slots + 4;
+  pa.slot_bytes = (int64_t)(kPairSlotBytes - 16);
   pa.spin_ticks = spin_ticks;
   pa.fallbacks = sc.fallbacks;
-  const hipError_t e = hipMemsetAsync(sc.slots, 0, (size_t)(grid / 2) * 2 * 2 * 16, s);  // tags restart at 1
+  // the counter and the launch's pairs' slots (tags restart at 1)
+  const hipError_t e = hipMemsetAsync(sc.slots, 0, 16 + (size_t)(grid / 2) * kPairSlotStride, s);
   if (e != hipSuccess) return e;
   return launch_pair_table(nv, a, pa, grid, s, std::make_integer_sequence<int, kPairMaxNV - kPairMinNV + 1>{});
 }
@@ -1431,7 +1577,7 @@ static hipError_t launch_rows(const KArgs& a, const PrlGrpoBatch* b, const PrlGr
   } else if (b->V % 4 == 0 && b->ld % 4 == 0 && aligned16(b->logits) &&
              (!p->write_grad || aligned16(out->dlogits))) {
     const int pnv = p->f32_rows == 0 ? pair_nv(b->V) : 0;  // PrlGrpoParams.f32_rows 1: the part-resident kernel
-    if (pnv > 0) return launch_pair_rows(a, pnv, nrows, cus, sc, pair_spin_ticks(p), s);  // resident over two CUs
+    if (pnv > 0 && nrows < ((int64_t)1 << 31)) return launch_pair_rows(a, pnv, nrows, cus, sc, pair_spin_ticks(p), s);  // resident over two CUs
     if (PRL_HYB_NL >= 0 && b->V / 4 >= (int64_t)(kHybNR + kHybNL) * 1024) {  // a tail to stream: the row part-resident
       const int g1 = (int)(nrows < cus ? nrows : cus);  // one workgroup per CU (the LDS slab)
       hipLaunchKernelGGL((grpo_fwd_hybrid_f32<kHybNR, kHybNL>), dim3(g1), dim3(1024), 0, s, a);

@@ -234,8 +234,9 @@ def test_target_columns_at_vector_edges(ent):
 # over two workgroups, columns [0, 75 968) and [75 968, 151 936), each half in registers, 19 vectors
 # per lane, the last one partial) or, with PrlGrpoParams.f32_rows = 1, the part-resident one
 # (grpo_fwd_hybrid_f32<19, 9>: columns [0, 77 824) in registers, [77 824, 114 688) in LDS, the rest
-# streamed and re-read).  pair_spin_ticks < 0: a half never waits for its partner's partial and
-# computes it from HBM whenever it has not arrived yet (the bounded-spin path).
+# streamed and re-read).  pair_spin_ticks < 0: a half never waits for its partner — a partner whose
+# claim or partial has not arrived yet at the first look sends the half SOLO (its own rows claimed,
+# the other half's partial and gradient streamed from HBM: the bounded-spin path).
 HYB_EDGES = [0, 3, 4, 77823, 77824, 77827, 114687, 114688, 114691, 151935]
 PAIR_EDGES = [0, 3, 4, 73723, 73727, 73728, 75967, 75968, 75971, 75972, 149503, 149504, 151935]
 F32_KERNELS = {"pair": {}, "pair_nowait": {"pair_spin_ticks": -1}, "hybrid": {"f32_rows": 1}}
@@ -397,9 +398,10 @@ def test_pair_kernels_beside_a_kernel_holding_cus(dtype, env, monkeypatch):
     assert float(loss.detach()) == loss0 and stats == stats0
     # pairs are blocks b, b ^ 8 of 16-block groups: dispatched in order onto the free CUs, both halves
     # of a pair mostly start together, so the counter is usually 0 here (the never-wait runs of
-    # test_*_many_rows_* take the from-HBM partial on every row); it must be readable and bounded
+    # test_*_many_rows_* go SOLO); it must be readable and bounded (a row is finished SOLO at most
+    # once by each half)
     assert 0 <= fallbacks() <= 2 * (T - 1)
-    # the counter counts: the never-wait arm falls back on (almost) every row half
+    # the counter counts: in the never-wait arm partners go SOLO at their first look
     _controls(monkeypatch, pair_spin_ticks=-1)
     _run(lg, b, dtype=dtype)
     assert fallbacks() > 0
@@ -429,9 +431,9 @@ def test_pair_halves_far_apart_wait_once_not_every_row():
     that competes for the CUs: the launch costs about the GEMM's hold plus the rows, results
     bit-identical to the uncontended launch (measured on MI355X: 2.15 ms alone, 3.89 ms beside a
     2.34 ms GEMM, no fallback — the GEMM's tiles delay both halves of a pair alike).  Then a 10 ns
-    spin bound (pair_spin_ticks 1): halves time out on their first late partner, then only look for
-    the rest of the launch (the sticky no-wait path), computing partner partials from HBM — the same
-    bits."""
+    spin bound (pair_spin_ticks 1): halves time out on their first late partner and go SOLO for the
+    rest of the launch (their own rows claimed, the other half's partial and gradient from HBM) —
+    the same bits."""
     import dataclasses
 
     from pipelinerl_amd import _native
@@ -483,6 +485,59 @@ def test_pair_halves_far_apart_wait_once_not_every_row():
     fb2 = fallbacks()
     print(f"spin bound 10 ns: fallbacks {fb2} of {2 * (T - 1)} row halves")
     assert torch.equal(rows0, rows2) and torch.equal(stats0, stats2)
+
+
+def test_pair_claimed_rows_beside_side_workgroups():
+    """The fp32 pair kernel claims its rows (round 6): beside 16 long-running side workgroups (an
+    RCCL collective's channels: prl_paced_read, 1 GiB at 20 GB/s, ~50 ms) the pairs on the CUs they
+    share take fewer rows instead of a static share, so the launch stays near its uncontended time
+    (static rows: 13.2 -> 23.0 ms per C2 launch beside 16 side workgroups, claimed: 12.6 -> 13.7 ms,
+    bench.py loss_head_fp32.beside_16_side_workgroups) — with the same bits and no SOLO rows."""
+    import ctypes
+
+    from pipelinerl_amd import _native
+    from pipelinerl_amd.finetune.rl.fused import GrpoParams, grpo_loss, prepare_fields
+
+    lib = _native.load()
+    V, T = 151936, 16385
+    b = _batch(T, V, seed=29, lens=[8193, 8192], prompts=[1, 1])
+    lg = torch.randn((1, T, V), generator=torch.Generator(device=DEV).manual_seed(29), device=DEV) * 2
+    fields = prepare_fields(to_batch(b), DEV)
+    params = GrpoParams(policy_loss="ppo", epsilon=0.2, kl_coef=0.05, entropy_coef=0.0, clamp_log_ratio=5.0,
+                        temperature=1.0, batch_size=4.0)
+    fallbacks = _fallbacks_reader(lib)
+    hog = torch.empty(1 << 30, dtype=torch.uint8, device=DEV)
+    sink = torch.zeros(16, dtype=torch.int32, device=DEV)
+    side = torch.cuda.Stream()
+
+    def launch(beside: bool):
+        x = lg.detach().requires_grad_(True)
+        torch.cuda.synchronize()
+        if beside:
+            with torch.cuda.stream(side):
+                assert lib.prl_paced_read(ctypes.c_void_p(hog.data_ptr()), hog.numel(), 20.0, 16,
+                                          ctypes.c_void_p(sink.data_ptr()), side.cuda_stream) == 0
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        loss, stats, rows = grpo_loss(x, fields, params)
+        e1.record()
+        torch.cuda.synchronize()
+        loss.backward()
+        return e0.elapsed_time(e1), rows.clone(), stats.clone(), x.grad
+
+    launch(False)
+    t0, rows0, stats0, g0 = launch(False)
+    fallbacks()
+    times = []
+    for _ in range(3):
+        t1, rows1, stats1, g1 = launch(True)
+        times.append(t1)
+        assert torch.equal(rows0, rows1) and torch.equal(stats0, stats1) and torch.equal(g0, g1)
+        del g1
+    fb = fallbacks()
+    t1 = sorted(times)[1]
+    print(f"uncontended {t0:.2f} ms, beside 16 side workgroups {times} ms, SOLO rows {fb}")
+    assert t1 <= 1.35 * t0 + 0.3, (t0, times)
 
 
 def test_claimed_rows_on_concurrent_streams():

@@ -24,6 +24,7 @@ VARIANTS = {  # the loss head's A/B builds (csrc/grpo_loss.hip macros); profiles
     "vec_row_inputs": {"PRL_SCALAR_ROW_INPUTS": "0"},
     "target_select": {"PRL_TARGET_FIXUP": "0"},
     "hyb_off": {"PRL_HYB_NL": "-1"},
+    "pair_perm": {"PRL_PAIR_PERMUTE": "1"},  # the fp32 pair kernel's rows through perm_row (round 6 A/B)
     "fold_off": {"PRL_FOLD_EXP": "0"},  # the bf16 kernel's (x - M) c exponent forms (round 2-5)  # fp32 rows on the streaming kernel instead of the part-resident one
 }
 
