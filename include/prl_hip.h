@@ -134,7 +134,9 @@ typedef struct PrlGrpoParams {
   float value_loss_coef;
   float grad_scale;            /* upstream d(final_loss) assumed for dlogits / dvalues (> 0, finite) */
   int32_t pair_spin_ticks;     /* fp32 pair kernel: realtime ticks (100 MHz) a row half waits for its
-                                  partner's partial before computing it from HBM itself (the same bits);
+                                  partner's partial (or the leader's row claim) before going SOLO for
+                                  the rest of the launch: its own rows claimed, the other half's
+                                  partial and gradient from HBM (the same bits);
                                   0 = the default (20000, 200 us), < 0 = never waits */
   int32_t f32_rows;            /* fp32 logits: 0 = the pair kernel where the row fits two CUs (default),
                                   1 = the part-resident kernel */
@@ -207,10 +209,10 @@ int prl_grpo_backward(const PrlGrpoBatch* batch, const PrlGrpoParams* params,
 /* Number of statistics (PRL_NSTAT) compiled into the library: bindings check it. */
 int prl_grpo_nstat(void);
 
-/* Observability of the pair kernels (fp32 rows, each split over two workgroups): how many row halves
- * of launches with this workspace computed their partner's partial themselves because the partner
- * had not published it in time (PrlGrpoParams.pair_spin_ticks) since the last call; reads and
- * resets the workspace's counter, synchronising the stream. */
+/* Observability of the pair kernels (fp32 rows, each split over two workgroups): how many rows of
+ * launches with this workspace a SOLO half finished alone (its partner's partial or claim had not
+ * arrived within PrlGrpoParams.pair_spin_ticks) since the last call; reads and resets the
+ * workspace's counter, synchronising the stream. */
 int prl_grpo_pair_fallbacks(void* workspace, size_t workspace_bytes, void* stream, uint64_t* count);
 
 /* Weight broadcast staging: copy n tensors (f32 or bf16, contiguous) into one bf16 buffer

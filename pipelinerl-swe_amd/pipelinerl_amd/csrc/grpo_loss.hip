@@ -10,9 +10,12 @@
 //       gradient pass re-reads nothing.  Read / write phases: the row's dlogits stores retire,
 //       then the whole next row (~300 KiB per CU) is loaded at once, so a CU never mixes HBM
 //       reads and writes (3-4 % faster than loading vector k of row r+grid right behind the
-//       store of vector k of row r; PRL_PHASED below).
+//       store of vector k of row r; the phased schedule below).
 //       Row reduction: per-lane online (max, sum 2^y, sum 2^y y) with lazy rebase, wave
 //       shuffles, then one LDS exchange (double-buffered by row parity: one barrier/row).
+//   grpo_fwd_pair_f32<NV>  fp32 logits: each row over a pair of workgroups (one half each, in
+//       VGPRs), one tagged partial exchange per row, rows claimed by the pair's leader.
+//   grpo_fwd_hybrid_f32<NR, NL> fp32 rows past the pair kernel's range: 75 % of the row on chip.
 //   grpo_fwd_stream<T,VEC> any dtype / V: same math, row re-read for the gradient pass.
 //   grpo_bwd_stream<T,VEC> gradient-only pass from the saved per-row coefficients.
 //   grpo_stats_partial     the ~38 masked statistics of rl/__init__.py:315-375 and the
@@ -73,14 +76,8 @@ __device__ __forceinline__ TokGrad row_epilogue(const KArgs& a, int64_t q, const
   return g;
 }
 
-#ifndef PRL_SCALAR_ROW_INPUTS
-#define PRL_SCALAR_ROW_INPUTS 1  // 0: the round-1..3 vector loads (A/B: tools/build_variants.py vec_row_inputs)
-#endif
-#if PRL_SCALAR_ROW_INPUTS
+// the rows' token inputs through the scalar cache (round 3; the vector-load form is retired)
 using RowLd = SclLd;
-#else
-using RowLd = VecLd;
-#endif
 
 // the target logit of a row, read through the scalar cache as the aligned dword holding it (no
 // 16-bit scalar load on gfx950; rows of the streaming kernels may start 2-B aligned); j must be a
@@ -93,18 +90,17 @@ __device__ __forceinline__ float row_logit_scl(const uint16_t* row, int64_t j) {
 }
 __device__ __forceinline__ float row_logit_scl(const float* row, int64_t j) { return SclLd::ld(row, j); }
 __device__ __forceinline__ float row_logit(const uint16_t* row, int64_t j) {
-  return PRL_SCALAR_ROW_INPUTS ? row_logit_scl(row, j) : bf_to_f(row[j]);
+  return row_logit_scl(row, j);
 }
 __device__ __forceinline__ float row_logit(const float* row, int64_t j) {
-  return PRL_SCALAR_ROW_INPUTS ? row_logit_scl(row, j) : row[j];
+  return row_logit_scl(row, j);
 }
 
 // Pin scalar-loaded row inputs to this point of the program: the scheduler otherwise sinks the
 // s_loads to their first use after the row reduction and waits for them in front of the barrier.
 // Here (the row's vector loads just issued) the wait costs nothing: pass 1 waits for the row anyway.
 __device__ __forceinline__ void pin_sgpr(TokIn& t, float& x) {
-  if constexpr (PRL_SCALAR_ROW_INPUTS)
-    asm volatile("" : "+s"(t.label), "+s"(t.reward), "+s"(t.ref), "+s"(t.old), "+s"(t.gt), "+s"(t.ovf),
+  asm volatile("" : "+s"(t.label), "+s"(t.reward), "+s"(t.ref), "+s"(t.old), "+s"(t.gt), "+s"(t.ovf),
                  "+s"(t.advsrc), "+s"(x));
 }
 
@@ -150,54 +146,34 @@ __device__ __forceinline__ void store_row_b128(u32x4 o, __amdgpu_buffer_rsrc_t r
 #endif
 }
 
-#ifndef PRL_PHASED
-// 1: a row's stores retire (vmcnt(0)) before the next row's loads are issued, so this CU never
-// mixes reads and writes: 7.50 -> 7.24 ms per C2 launch on one box (profiles/r02_loss_phase_ab.jsonl;
-// the same schedule on a plain 20 GB copy: profiles/r02_phased_copy.jsonl).  0: the next row's
-// vector k is loaded right behind the store of vector k (round-1 schedule).  2: phased, no wait.
-#define PRL_PHASED 1
-#endif
+// The phased schedule (round 2): a row's stores retire (vmcnt(0)) before the next row's loads are
+// issued, so this CU never mixes reads and writes: 7.50 -> 7.24 ms per C2 launch on one box
+// (profiles/r02_loss_phase_ab.jsonl; the same schedule on a plain 20 GB copy:
+// profiles/r02_phased_copy.jsonl).  Rows above kPhasedMaxNV keep the round-1 interleaved schedule
+// (the next row's vector k loaded right behind the store of vector k).
 // The phased schedule keeps pass 2's gradient vectors and the row in registers at once: above
 // NV = 20 (V > 163 840) it spills row vectors to scratch, so rows that large keep the interleaved
 // schedule.  (Its round-2 wrong dlogits at NV = 24 were the store-data hazard fenced in
 // store_row_b128 below; both schedules are correct at every NV since.)  Qwen2.5's vocabularies are
 // NV = 19, covered by tests/test_grpo_edge_gpu.py::test_multi_row_per_workgroup.
-#ifndef PRL_TARGET_FIXUP
-#define PRL_TARGET_FIXUP 1
-#endif
-#ifndef PRL_NOENT_FORM
-#define PRL_NOENT_FORM 1  // beta == 0 rows (no entropy term) take the form without it
-#endif
 #ifndef PRL_PHASED_MAX_NV
 #define PRL_PHASED_MAX_NV 20
 #endif
 constexpr int kPhasedMaxNV = PRL_PHASED_MAX_NV;
-#ifndef PRL_ROW_PERMUTE
-#define PRL_ROW_PERMUTE 1  // A/B (tools/build_variants.py row_permute): 7.40 vs 7.46 ms per C2 launch, same box
-#endif
-// Order in which the persistent grid visits the rows: iteration i processes row perm(i).  With
-// PRL_ROW_PERMUTE the rows in flight at any moment are scattered over the whole [rows x V]
+// Order in which the persistent grid visits the rows: iteration i processes row perm(i) (7.40 vs
+// 7.46 ms per C2 launch against the identity, same box): the rows in flight at any moment are scattered over the whole [rows x V]
 // tensor (i * P mod n, P a prime > n, so a bijection) instead of one contiguous ~76 MB window;
 // per-row outputs are written per row, so results are bit-identical either way.
 __device__ __forceinline__ int64_t perm_row(int64_t i, int64_t n) {
-#if PRL_ROW_PERMUTE
   return (int64_t)(((uint64_t)i * 2654435761ull) % (uint64_t)n);
-#else
-  (void)n;
-  return i;
-#endif
 }
 
-#ifndef PRL_FOLD_EXP
-// 1: the exponent arguments on element pairs (packed FP32 ops): pass 1 y = (x - m) c with two
+// The exponent arguments on element pairs (packed FP32 ops): pass 1 y = (x - m) c with two
 // partial sums per lane; pass 2 t = (x - M) c + k with a per-row constant k, and without an entropy
 // term d = sign(alpha) 2^((x - M) c + log2|alpha| - log2 S): alpha folded into the exponent, its
 // sign applied to the packed bf16 result, no multiply.  x - M stays an exact subtraction (x c - M c
-// would lose |M c| ulp-scale accuracy at large logits: the scale-2000 edge test).  0: the scalar
-// forms of the other kernels.  Results agree within the fp32 rounding of the exponent's argument.
-#define PRL_FOLD_EXP 1
-#endif
-constexpr bool kFoldExp = PRL_FOLD_EXP != 0;
+// would lose |M c| ulp-scale accuracy at large logits: the scale-2000 edge test).  Results agree with
+// the other kernels' scalar forms within the fp32 rounding of the exponent's argument (round 5).
 
 // Pass 1's online state on element pairs: (max, pairwise sums of 2^y and 2^y y).
 struct Lse2 {
@@ -232,12 +208,10 @@ template <int NV>
 __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
   constexpr int BLOCK = 1024, NW = BLOCK / 64;
   constexpr int VSTRIDE = BLOCK * 16;  // bytes between a lane's consecutive vectors
-  constexpr bool kPhased = PRL_PHASED != 0 && NV <= kPhasedMaxNV;
-  // The target column's extra g_lp/temperature term: the owner lane rewrites that one element
-  // after the row's stores retired (phased schedule), instead of 8 selects per vector in every
-  // lane (190 v_cndmask per row and wave in the ISA).
-  constexpr bool kTargetFixup = PRL_TARGET_FIXUP != 0 && kPhased && PRL_PHASED == 1;
-  constexpr bool kNoEntropyForm = PRL_NOENT_FORM != 0;
+  // the phased schedule; with it the target column's extra g_lp/temperature term is written by the
+  // owner lane after the row's stores retired, instead of 8 selects per vector in every lane (190
+  // v_cndmask per row and wave in the ISA)
+  constexpr bool kPhased = NV <= kPhasedMaxNV;
 #ifdef PRL_COPY_CEILING
   constexpr bool kCopyCeiling = true;
 #else
@@ -299,7 +273,7 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
     const float xt = bad_id ? __builtin_nanf("") : xr;
 
     // ---- pass 1: row statistics from registers
-    Lse st = lse_empty();
+    Lse st;
     Lse2 st2 = {kEmptyMax, {0.f, 0.f}, {0.f, 0.f}};
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
@@ -313,18 +287,17 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
       }
       if constexpr (kNoPass1) {
         st2.s.x += x[0];  // keeps the loads' consumers (one add per vector)
-      } else if constexpr (kFoldExp) {
-        lse2_add<8>(st2, x, c);
       } else {
-        lse_add<8>(st, x, c);
+        lse2_add<8>(st2, x, c);
       }
     }
-    if constexpr (kFoldExp) st = Lse{st2.m, st2.s.x + st2.s.y, st2.w.x + st2.w.y};
+    st = Lse{st2.m, st2.s.x + st2.s.y, st2.w.x + st2.w.y};
     st = wave_reduce_lse(st, c);
-    if (lane == 0) {
-      red[par][wid][0] = st.m;
-      red[par][wid][1] = st.s;
-      red[par][wid][2] = st.w;
+    if (lane == 0) {  // (the wave index as an SGPR: a VGPR copy was the kernel's one scratch reload per row)
+      const int wu = __builtin_amdgcn_readfirstlane(wid);
+      red[par][wu][0] = st.m;
+      red[par][wu][1] = st.s;
+      red[par][wu][2] = st.w;
     }
     if (tid == 0) next_q[par] = a.row_ctr ? (int64_t)gridDim.x + (int64_t)claim : q + gridDim.x;
     __syncthreads();
@@ -358,7 +331,7 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
       const float alpha = -(core.g_lp + core.g_h * H) * inv_t;
       const float beta = -core.g_h * kLn2 * inv_t;
       const float gadd = core.g_lp * inv_t;
-      // folded forms (kFoldExp): t = (x - M) c + k2 (k2 = -log2 S); without an entropy term
+      // folded forms: t = (x - M) c + k2 (k2 = -log2 S); without an entropy term
       // d = sign(alpha) 2^((x - M) c + k1), k1 = log2|alpha| - log2 S (alpha = 0: -inf, d = 0)
       const float k2 = -l2s;
       const float k1 = log2f(fabsf(alpha)) - l2s;
@@ -382,50 +355,24 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
           } else if constexpr (kMode == 0) {
             o = u32x4{0u, 0u, 0u, 0u};
           } else {
-            float d[8];
             // opaque per form, so the unpack shared by forms 1 and 2 is not hoisted above the
             // form branch (8 instead of 4 live VGPRs per vector: spills)
             u32x4 v = buf[k];
             asm volatile("" : "+v"(v));
-            if constexpr (kFoldExp && kTargetFixup) {
-              const f32x2 cc = {c, c}, mm = {M, M}, kk = {kMode == 1 ? k1 : k2, kMode == 1 ? k1 : k2};
-#pragma unroll
-              for (int j = 0; j < 4; ++j) {
-                const f32x2 xv = {bf_lo(v[j]), bf_hi(v[j])};
-                const f32x2 t = (xv - mm) * cc + kk;
-                const f32x2 p = {fexp2(t.x), fexp2(t.y)};
-                if constexpr (kMode == 1) {
-                  o[j] = pack_bf16x2(p.x, p.y) ^ sgn2;
-                } else {
-                  const f32x2 g = t * f32x2{beta, beta} + f32x2{alpha, alpha};
-                  const f32x2 dd = p * g;
-                  o[j] = pack_bf16x2(dd.x, dd.y);
-                }
-              }
-              store_row_b128(o, ws, voff, k * VSTRIDE);
-              continue;
-            }
+            const f32x2 cc = {c, c}, mm = {M, M}, kk = {kMode == 1 ? k1 : k2, kMode == 1 ? k1 : k2};
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-              const float x0 = bf_lo(v[j]), x1 = bf_hi(v[j]);
-              const float t0 = __builtin_fmaf(x0 - M, c, -l2s), t1 = __builtin_fmaf(x1 - M, c, -l2s);
-              const float p0 = fexp2(t0), p1 = fexp2(t1);
+              const f32x2 xv = {bf_lo(v[j]), bf_hi(v[j])};
+              const f32x2 t = (xv - mm) * cc + kk;
+              const f32x2 p = {fexp2(t.x), fexp2(t.y)};
               if constexpr (kMode == 1) {
-                d[2 * j] = p0 * alpha;
-                d[2 * j + 1] = p1 * alpha;
+                o[j] = pack_bf16x2(p.x, p.y) ^ sgn2;
               } else {
-                d[2 * j] = p0 * __builtin_fmaf(beta, t0, alpha);
-                d[2 * j + 1] = p1 * __builtin_fmaf(beta, t1, alpha);
+                const f32x2 g = t * f32x2{beta, beta} + f32x2{alpha, alpha};
+                const f32x2 dd = p * g;
+                o[j] = pack_bf16x2(dd.x, dd.y);
               }
             }
-            if constexpr (!kTargetFixup) {
-              if (k == kt && tid == lt) {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) d[j] += (j == te) ? gadd : 0.f;
-              }
-            }
-#pragma unroll
-            for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(d[2 * j], d[2 * j + 1]);
           }
           store_row_b128(o, ws, voff, k * VSTRIDE);
         }
@@ -460,33 +407,26 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
         }
       } else if (zero_row)
         row_pass(std::integral_constant<int, 0>{});
-      else if (kNoEntropyForm && beta == 0.f)
+      else if (beta == 0.f)
         row_pass(std::integral_constant<int, 1>{});
       else
         row_pass(std::integral_constant<int, 2>{});
       if constexpr (kPhased) {
-        // the whole row's stores retire before the next row's loads start (PRL_PHASED above)
-        if constexpr (PRL_PHASED == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if constexpr (kTargetFixup) {
-          // the target column's g_lp term, by its one owner lane after the row's stores retired
-          // (so this 2-B store lands after the 16-B store of the same bytes): the same operations
-          // as the vector loop on the same bf16 value, rounded the same way (no contraction)
-          if (tid == lt && !zero_row) {
-            float dm;
-            if constexpr (kFoldExp) {
-              if (kNoEntropyForm && beta == 0.f) {
-                const float pt = fexp2(__builtin_fmaf(xt - M, c, k1));
-                dm = alpha < 0.f ? -pt : pt;
-              } else {
-                const float tt = __builtin_fmaf(xt - M, c, k2);
-                dm = __fmul_rn(fexp2(tt), __builtin_fmaf(tt, beta, alpha));
-              }
-            } else {
-              const float tt = __builtin_fmaf(xt - M, c, -l2s);
-              dm = __fmul_rn(fexp2(tt), beta == 0.f ? alpha : __builtin_fmaf(beta, tt, alpha));
-            }
-            dl[lrow * a.ld + tgt] = f_to_bf(__fadd_rn(dm, gadd));
+        // the whole row's stores retire before the next row's loads start (the phased schedule)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // the target column's g_lp term, by its one owner lane after the row's stores retired
+        // (so this 2-B store lands after the 16-B store of the same bytes): the same operations
+        // as the vector loop on the same bf16 value, rounded the same way (no contraction)
+        if (tid == lt && !zero_row) {
+          float dm;
+          if (beta == 0.f) {
+            const float pt = fexp2(__builtin_fmaf(xt - M, c, k1));
+            dm = alpha < 0.f ? -pt : pt;
+          } else {
+            const float tt = __builtin_fmaf(xt - M, c, k2);
+            dm = __fmul_rn(fexp2(tt), __builtin_fmaf(tt, beta, alpha));
           }
+          dl[lrow * a.ld + tgt] = f_to_bf(__fadd_rn(dm, gadd));
         }
         if (has_next) {
 #pragma unroll
@@ -504,19 +444,12 @@ __global__ __launch_bounds__(1024) void grpo_fwd_resident(KArgs a) {
 
 // ---------------------------------------------------------------------------------------
 // generic streaming path: T = float (PRL_F32) or uint16_t (bf16); VEC elements per access
-#ifndef PRL_STREAM_STORE_SC1
-#define PRL_STREAM_STORE_SC1 1  // the 16-B row stores as the resident kernel's (kStoreAux); 0: plain nt
-#endif
 // a 16-B store into a wave-uniform row through a buffer descriptor (soffset 0: the hardware wait
 // state for the store data is emitted), with the resident kernel's cache policy
 __device__ __forceinline__ void store_row16(void* row, int64_t gv, u32x4 o) {
-#if PRL_STREAM_STORE_SC1
   const auto rs = __builtin_amdgcn_make_buffer_rsrc(row, 0, 0x7fffffff, 0x00020000);
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, o), rs,
                                          (int)(gv * 16), 0, kStoreAux);
-#else
-  __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(row) + gv);
-#endif
 }
 template <typename T, int VEC>
 struct RowIO;
@@ -895,20 +828,11 @@ struct PairArgs {
 constexpr int kPairMinNV = 8, kPairMaxNV = 19;  // above 19 the registers spill (hybrid kernel there)
 constexpr int kSc1 = 16;  // aux bit of buffer_load / buffer_store: sc1 (bypass the CU's L1; write through)
 constexpr int kPairSlotStride = 96;
-#ifndef PRL_PAIR_PERMUTE
-#define PRL_PAIR_PERMUTE 0
-#endif
 // The pair kernel visits rows in claim order: perm_row's 64-bit modulo kept two loop invariants
 // (the row count as floats) and a loop-carried value in registers the kernel does not have, so
-// they went to scratch and back every row (2.7 % extra writes, more reads: profiles/r06_fp32_calibration.json)
-__device__ __forceinline__ int64_t pair_row(int64_t i, int64_t n) {
-#if PRL_PAIR_PERMUTE
-  return perm_row(i, n);
-#else
-  (void)n;
-  return i;
-#endif
-}
+// they went to scratch and back every row (2.7 % extra writes; through perm_row 12.66 / 12.85 vs
+// 13.05 / 13.30 ms per C2 launch, alternated on one box)
+__device__ __forceinline__ int64_t pair_row(int64_t i, int64_t) { return i; }
 constexpr uint32_t kSoloTag = 0xFFFFFFFFu;  // a partial slot's tag once its half went SOLO
 
 __device__ __forceinline__ u32x4 load_slot(__amdgpu_buffer_rsrc_t slots, int off) {

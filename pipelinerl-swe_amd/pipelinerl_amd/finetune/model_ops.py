@@ -194,8 +194,8 @@ class RopeFn(torch.autograd.Function):
 # kernel (a [N, K] read-read-write per weight per micro-batch: ~2 % of a 7B C3 step).  The sum is
 # rounded to bf16 once instead of twice.  Not used when a post-accumulate hook must see the
 # gradient (an armed GradBuckets, any other hook) or under FSDP (shard_model switches it off):
-# there autograd accumulates as before.  PRL_FUSE_GRAD_ACCUM=0 turns it off (A/B).
-_FUSE_GRAD_ACCUM = os.environ.get("PRL_FUSE_GRAD_ACCUM", "1") != "0"
+# there autograd accumulates as before.
+_FUSE_GRAD_ACCUM = True
 
 
 def disable_fused_grad_accumulation() -> None:
@@ -731,22 +731,21 @@ def patch_model(model) -> dict:
                     lins[2].weight._prl_follows = lins[1].weight
                 n_group += 1
     # decoder layers (input_layernorm / self_attn / post_attention_layernorm / mlp, Qwen2 / Llama
-    # style): residual adds fused into the norms.  PRL_ADD_NORM=0 keeps the eager adds (A/B)
+    # style): residual adds fused into the norms
     n_addnorm = 0
-    if os.environ.get("PRL_ADD_NORM", "1") != "0":
-        inner = getattr(model, "model", model)
-        layers = list(getattr(inner, "layers", []))
-        final = getattr(inner, "norm", None)
-        if layers and all(type(l).__name__.endswith("DecoderLayer") and all(
-                hasattr(l, a) for a in ("input_layernorm", "self_attn", "post_attention_layernorm", "mlp"))
-                and hasattr(l.post_attention_layernorm, "_prl_orig_forward") for l in layers):
-            for i, l in enumerate(layers):
-                nxt = layers[i + 1].input_layernorm if i + 1 < len(layers) else final
-                l.__dict__["_prl_next_norm"] = nxt if hasattr(nxt, "_prl_orig_forward") else None
-                if "_prl_orig_forward" not in l.__dict__:
-                    l.__dict__["_prl_orig_forward"] = l.forward
-                    l.forward = types.MethodType(_decoder_forward, l)
-                n_addnorm += 1
+    inner = getattr(model, "model", model)
+    layers = list(getattr(inner, "layers", []))
+    final = getattr(inner, "norm", None)
+    if layers and all(type(l).__name__.endswith("DecoderLayer") and all(
+            hasattr(l, a) for a in ("input_layernorm", "self_attn", "post_attention_layernorm", "mlp"))
+            and hasattr(l.post_attention_layernorm, "_prl_orig_forward") for l in layers):
+        for i, l in enumerate(layers):
+            nxt = layers[i + 1].input_layernorm if i + 1 < len(layers) else final
+            l.__dict__["_prl_next_norm"] = nxt if hasattr(nxt, "_prl_orig_forward") else None
+            if "_prl_orig_forward" not in l.__dict__:
+                l.__dict__["_prl_orig_forward"] = l.forward
+                l.forward = types.MethodType(_decoder_forward, l)
+            n_addnorm += 1
     n_rope = 0
     for modname in mods:
         mod = sys.modules.get(modname)

@@ -151,20 +151,24 @@ def fsdp_unit_bytes(model) -> tuple[int, int]:
     return root, layer
 
 
-def fsdp_transient_bytes(model, shard_world: int, act: int, logits: int, head_grad: int) -> int:
+def fsdp_transient_bytes(model, shard_world: int, act: int, logits: int, head_grad: int,
+                         reduce_factor: int = 1) -> int:
     """FSDP2's unsharded working set beyond the activations (upper bound), the larger of its two
     peaks in a step: (a) the start of the backward — every activation, the logits' gradient
     (``logits``: the full-logits loss head writes it beside the logits; 0 for the label-row head,
     which writes it in place), the root unit gathered, the lm_head's unsharded gradient and a
     decoder layer in use plus the next prefetched; (b) the root's
     reduce-scatter at the end of the backward — the root gathered, its unsharded gradients and the
-    reduce-scatter input FSDP copies them into (3 x the root).  Returned as that peak minus ``act``
-    (the plan adds the activations itself).  0 when not sharded."""
+    reduce-scatter input FSDP copies them into (3 x the root).  ``reduce_factor``: the reduce dtype's
+    bytes over the compute dtype's; with 2 (fp32 master shards computed in bf16, reduced in fp32) the
+    input is twice the root and the fp32 output shard exists beside it (the 32B-shaped GPU test's
+    peak, 34.4 GB per rank, needs all of them: tests/test_fsdp_32b_gpu.py).  Returned as that peak
+    minus ``act`` (the plan adds the activations itself).  0 when not sharded."""
     if shard_world <= 1:
         return 0
     root, layer = fsdp_unit_bytes(model)
     start = act + logits + root + head_grad + 2 * layer
-    end = 3 * root
+    end = (2 + reduce_factor) * root + (reduce_factor * root // shard_world if reduce_factor > 1 else 0)
     return max(start, end) - act
 
 
@@ -327,7 +331,8 @@ def _plan_recompute(args, model, device: torch.device, shard_world: int, device_
         a = act if keep >= L else keep * act_layer + 2 * act_layer
         a_bytes = int(a * f_act) + (0 if keep >= L else (L - keep) * saved_input)
         buffers = build_buffer_bytes(config, int(seq), chunk, int(shard_world), pbytes, flat) + \
-            fsdp_transient_bytes(model, int(shard_world), a, 0 if fused else logits, head)
+            fsdp_transient_bytes(model, int(shard_world), a, 0 if fused else logits, head,
+                                 reduce_factor=2 if master and pbytes == 2 else 1)
         need = int(state * f_state) + a_bytes + int(logits * f_logits) + \
             int(buffers * max(f_state, f_act, f_logits)) + int(HEADROOM_FRAC * total) + HEADROOM_BYTES
         return need, a_bytes, buffers

@@ -159,8 +159,11 @@ def shard_model(model, fsdp_cfg=None, grad_reduce: str = "mean", reshard_after_f
     if master:
         pd = load  # compute in the loaded dtype; the fp32 copies are the optimizer's
         rd = rd or torch.float32
-    mp = MixedPrecisionPolicy(param_dtype=pd if pd not in (None, store) else None,
-                              reduce_dtype=rd if rd not in (None, store) else None)
+    param_dtype = pd if pd not in (None, store) else None
+    # FSDP2 reduces in param_dtype when reduce_dtype is None: with fp32 master shards computed in bf16
+    # an fp32 reduce must be named even though it equals the storage dtype
+    reduce_dtype = rd if rd is not None and (rd != store or param_dtype is not None) else None
+    mp = MixedPrecisionPolicy(param_dtype=param_dtype, reduce_dtype=reduce_dtype)
     layers = decoder_layers(model)
     first_gathered = len(layers) - max(0, min(int(keep_gathered), len(layers)))
     for i, layer in enumerate(layers):

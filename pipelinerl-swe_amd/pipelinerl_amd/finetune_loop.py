@@ -129,8 +129,7 @@ def run_data_loader(data_stream: SingleStreamSpec, batch_queue: Queue, device: t
                 ntok = int(b.attention_mask.sum())
                 nseq = batch_sequence_count(b)
                 if device.type == "cuda":
-                    # the label-row lm_head's count, known on the host (PRL_HOST_LABEL_ROWS=0: A/B)
-                    rows = b.label_rows_from_host() if os.environ.get("PRL_HOST_LABEL_ROWS", "1") != "0" else None
+                    rows = b.label_rows_from_host()  # the label-row lm_head's count, known on the host
                     for name in type(b).model_fields:
                         v = getattr(b, name)
                         if isinstance(v, torch.Tensor) and name != "seq_boundaries":  # host metadata
@@ -418,7 +417,7 @@ def rl_finetuning_worker(args, ctx: Dist, model, optimizer, lr_scheduler, grads:
     safe = bool(args.get("use_safetensors", False))  # checkpoints.py:285 default
     loss_scale = micro_batch_loss_scale(args, ctx.world, grad_scale_mode)
     native_step = step_fn is rl_step
-    defer_stats = os.environ.get("PRL_DEFER_STATS", "1") != "0"  # 0: read them before backward (A/B)
+    defer_stats = True  # statistics resolved after the backward is queued (rl_step(defer_stats=True))
     collective_backward = is_sharded(model)  # FSDP: every rank's backward joins all-gathers
     trace = PhaseTrace(ctx.device, bool(args.get("trace_gpu_phases", False)) or os.environ.get("PRL_TRACE_GPU") == "1")
     trace_md: dict[str, float] = {}

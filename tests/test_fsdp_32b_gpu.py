@@ -188,6 +188,10 @@ def _run(rank: int, port: int, tmp: str):
         g = g.to(dev).double()
         parts[name] = [float((g * rows).sum()), float((rows * rows).sum()), float(((g - rows) ** 2).sum()),
                        g.numel()]
+        if name in ("lm_head.weight", "model.layers.0.mlp.down_proj.weight"):
+            _say(rank, t0, f"{name}: local {tuple(g.shape)} {g_local[name][0].dtype}, ref {p.grad.dtype}, "
+                           f"max|g| {float(g.abs().max()):.3e} max|ref| {float(rows.abs().max()):.3e} "
+                           f"max|g-ref| {float((g - rows).abs().max()):.3e} equal {int((g == rows).sum())}/{g.numel()}")
     out["grad_part"] = parts
     del ref
     _say(rank, t0, "unsharded reference gradients compared")
@@ -230,18 +234,23 @@ def test_c5_32b_shapes_fsdp_grads_snapshot_and_memory_plan(tmp_path):
     mp.spawn(_run, args=(free_port(), str(tmp_path)), nprocs=2, join=True)
     r = [json.loads((tmp_path / f"rank{i}.json").read_text()) for i in range(2)]
     # gradients: per tensor, summed over the two ranks' shards
-    errs, numel = {}, {}
+    errs, numel, norms = {}, {}, {}
     for name in r[0]["grad_part"]:
         gr, rr, dd, n = (sum(x["grad_part"][name][k] for x in r) for k in range(4))
         errs[name] = math.sqrt(dd / rr) if rr > 0 else math.sqrt(dd)
         numel[name] = n
+        norms[name] = math.sqrt(rr)
+    # a comparison of zeros with zeros would pass: every reference gradient is non-zero
+    assert min(norms.values()) > 0, sorted(norms.items(), key=lambda kv: kv[1])[:5]
     worst = sorted(errs.items(), key=lambda kv: -kv[1])[:5]
     # weight update: the actor's copy of every tensor == the trainer's (digests of the shards summed)
     want = {n: [r[0]["param_digest_part"][n][k] + r[1]["param_digest_part"][n][k] for k in range(2)]
             for n in r[0]["param_digest_part"]}
     equal = {t: sum(int(d[n] == want[n]) for n in want) for t, d in r[1]["actor_digest"].items()}
     mem = {f"rank{i}": (x["peak_bytes"] / 1e9, x["estimate_bytes"] / 1e9) for i, x in enumerate(r)}
-    print(json.dumps({"worst_grad_rel_err": worst, "tensors": len(errs), "peak_vs_estimate_gb": mem,
+    print(json.dumps({"worst_grad_rel_err": worst, "tensors": len(errs),
+                      "smallest_ref_grad_norms": sorted(norms.items(), key=lambda kv: kv[1])[:3],
+                      "peak_vs_estimate_gb": mem,
                       "plan": r[1]["plan"], "actor_tensors_equal": equal}))
     assert [x["fused_calls"] for x in r] == [2, 2]  # the sharded steps took the label-row head
     assert len(errs) == 3 + LAYERS * 12, len(errs)  # embed, norm, lm_head + 12 per decoder layer

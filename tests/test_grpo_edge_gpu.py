@@ -211,7 +211,7 @@ def test_resident_strided_rows_both_vocabularies(V):
 def test_target_columns_at_vector_edges(ent):
     """Targets on the edges of the register-resident row layout (Qwen2.5's V = 151 936: 19 vectors
     per lane, the last one partial): the target term is added by the owner lane after the row's
-    stores (PRL_TARGET_FIXUP), and entropy 0 takes the form without the entropy term."""
+    stores (the phased schedule's fix-up), and entropy 0 takes the form without the entropy term."""
     T, V = 12, 151936
     b = _batch(T, V, seed=7, lens=[T], prompts=[1])
     cols = [0, 1, 7, 8, 8191, 8192, 147455, 147456, 147457, V - 8, V - 1]

@@ -74,8 +74,8 @@ def test_resident_loss_head_reads_row_inputs_through_the_scalar_cache():
     loads and no `s_waitcnt vmcnt(0)` sits between a row's first load and its stores (the vector
     version waited for the whole row, then for a dependent target-logit load, then for the
     epilogue's inputs); the target column is one 2-B store after the row's stores; the dlogits
-    are stored nt sc1.  (The vector-load build, PRL_SCALAR_ROW_INPUTS=0, has 10 global loads in
-    this function and 2 vmcnt waits between the barrier and the first store: it fails here.)"""
+    are stored nt sc1.  (The retired vector-load build had 10 global loads in this function and 2
+    vmcnt waits between the barrier and the first store: it failed here.)"""
     from isa_store_hazard_scan import compile_isa
 
     isa = _isa("grpo_loss.hip", {})

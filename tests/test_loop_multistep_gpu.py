@@ -74,7 +74,7 @@ def _data(tmp_path):
     return steps
 
 
-def _product_run(tmp_path, init, stale_cache=False):
+def _product_run(tmp_path, init, stale_cache=False, lr=LR, master_weights="auto", tag=None):
     """run_finetuning_loop on the product path; returns (per-step parameter snapshots [fp32 on
     the device], per-micro-batch stats, per-step pre-clip grad norms, per-step pre-clip
     gradients).  PrlAdamW folds the clip multiply into its step, so a step pre-hook sees the
@@ -115,7 +115,7 @@ def _product_run(tmp_path, init, stale_cache=False):
         hit = holder.__dict__.get(slot)
         return hit[1] if hit is not None else orig_fused(holder, ws, slot)
 
-    exp = tmp_path / ("stale" if stale_cache else "product")
+    exp = tmp_path / (tag or ("stale" if stale_cache else "product"))
     exp.mkdir()
     for f in ("streams",):
         os.symlink(tmp_path / f, exp / f)
@@ -123,8 +123,9 @@ def _product_run(tmp_path, init, stale_cache=False):
         os.environ.pop(k, None)
     # the stale-cache control needs the concatenation cache: with the parameters re-homed at load
     # (flat_parameters, the default) the fused gate/up weight is a view and nothing is cached
-    cfg = loop_cfg(exp, exp / "unused", 1, PER_STEP, ROLLOUTS // PER_STEP, dist_backend=None, learning_rate=LR,
+    cfg = loop_cfg(exp, exp / "unused", 1, PER_STEP, ROLLOUTS // PER_STEP, dist_backend=None, learning_rate=lr,
                    save_final_training_state=False, log_each_n_steps=1, flat_parameters=not stale_cache,
+                   master_weights=master_weights,
                    rl=dict(policy_loss="ppo", epsilon=4, kl_coef=0.0, final_kl_coef=0.0,
                            clamp_log_ratio_ref_new_value=5, temperature=1.0, divide_advantage_by_std=False))
     finetune_loop.get_optimizer = get_optimizer
@@ -144,7 +145,7 @@ def _product_run(tmp_path, init, stale_cache=False):
     return snaps, stats, norms, grads
 
 
-def _reference_run(init, steps):
+def _reference_run(init, steps, lr=LR):
     """The reference's step on the same bf16 weights: eager HF ops, library attention, torch
     restatement of rl_step, autograd accumulation, clip_grad_norm_ + torch AdamW + cosine."""
     from cpu_rl_step import cpu_rl_step
@@ -168,7 +169,7 @@ def _reference_run(init, steps):
             def named_parameters(self, *a, **k):
                 return iter(masters.items())
 
-        opt = torch.optim.AdamW(get_grouped_params(_Masters(), 0.01), lr=LR)
+        opt = torch.optim.AdamW(get_grouped_params(_Masters(), 0.01), lr=lr)
         sched = get_scheduler("cosine", opt, 0, len(steps))
         rlc = workloads.rl_config("c1", PER_STEP)
         snaps = [{n: p.detach().float().clone() for n, p in ref.named_parameters()}]
@@ -352,3 +353,36 @@ def test_c1_three_optimizer_steps_match_the_reference_step(tmp_path):
     assert ctl == [bias], ctl
     # ... and the same bound rejects the stale-cache bug at every step from the second on, by 2x
     assert min(bad_upd_mlp[1:]) >= 2 * UPDATE_BOUND, bad_upd_mlp
+
+
+REF_LR = 5e-7  # the reference's learning rate (conf/finetune/base.yaml:35)
+
+
+def test_c1_three_steps_at_the_reference_lr(tmp_path):
+    """The same three C1 optimizer steps at the reference's lr, 5e-7: each step moves a weight by
+    ~5e-7, far below half a bf16 ulp of the N(0, 0.02) weights, so only fp32 masters keep the
+    update.  The product (fp32 masters, finetune.master_weights auto) matches the reference's
+    fp32-master step within the same per-step bounds as at lr 1e-3; the product with
+    ``master_weights: false`` (bf16 weights and moments, the pre-round-6 optimizer) is the negative
+    control: its weights barely move, so its update differs from the reference's by ~100 %."""
+    from pipelinerl_amd.trainer_probe import qwen2_model
+
+    steps = _data(tmp_path)
+    init = {k: v.detach().clone() for k, v in qwen2_model("0.5b", torch.device(DEV), layers=LAYERS).state_dict().items()}
+    ref_snaps, _, ref_norms, _ = _reference_run(init, steps, lr=REF_LR)
+    snaps, _, norms, _ = _product_run(tmp_path, init, lr=REF_LR, tag="product_ref_lr")
+    bf16_snaps, _, _, _ = _product_run(tmp_path, init, lr=REF_LR, master_weights=False, tag="bf16_ref_lr")
+    layer_names = [n for n in snaps[0] if ".layers." in n and not n.endswith("norm.weight")]
+    upd = [_update_error(snaps, ref_snaps, k, layer_names) for k in range(1, len(steps) + 1)]
+    upd_all = [_update_error(snaps, ref_snaps, k, list(snaps[0])) for k in range(1, len(steps) + 1)]
+    upd_bf16 = [_update_error(bf16_snaps, ref_snaps, k, layer_names) for k in range(1, len(steps) + 1)]
+    moved = [float(sum(float((snaps[k][n] - snaps[0][n]).abs().sum()) for n in layer_names))
+             for k in range(1, len(steps) + 1)]
+    gn_err = [abs(a - b) / b for a, b in zip(norms, ref_norms)]
+    print(json.dumps({"lr": REF_LR, "update_rel_err_layers": upd, "update_rel_err_all": upd_all,
+                      "bf16_update_rel_err_layers": upd_bf16, "grad_norm_rel_err": gn_err,
+                      "abs_weight_change_sum": moved}))
+    assert max(gn_err) <= 2e-2, gn_err
+    assert all(u <= b for u, b in zip(upd, STEP_BOUNDS)), (upd, STEP_BOUNDS)
+    assert max(upd_all) <= UPDATE_BOUND, upd_all
+    assert min(upd_bf16) >= 0.5, upd_bf16  # bf16 weights lose most of every update at this lr

@@ -122,3 +122,39 @@ def test_memory_plan_counts_master_state():
                                            device_bytes=200 << 30)
     assert p_bf16.state_bytes == 8 * 1000 * 1000
     assert p_master.state_bytes == 16 * 1000 * 1000
+
+
+def test_fsdp_master_shards_reduce_in_fp32():
+    """fp32 master shards computed in bf16: the gradients are reduce-scattered in fp32 (the reference's
+    fsdp reduce_dtype, conf/base.yaml:97-100).  FSDP2 reduces in param_dtype when reduce_dtype is None,
+    so the policy must name fp32 even though it equals the shards' dtype (a round-6 build left it None
+    and reduced in bf16: the 32B-shaped GPU test then matched a bf16 model's gradients bit for bit)."""
+    import os
+
+    import torch
+    import torch.distributed as dist
+    from transformers import AutoModelForCausalLM, Qwen2Config
+
+    from pipelinerl_amd.finetune.sharding import shard_model
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        cfg = Qwen2Config(hidden_size=64, intermediate_size=128, num_hidden_layers=2, num_attention_heads=4,
+                          num_key_value_heads=2, vocab_size=256)
+        model = shard_model(AutoModelForCausalLM.from_config(cfg, dtype=torch.bfloat16), master_weights=True)
+        assert {p.dtype for p in model.parameters()} == {torch.float32}
+        for unit in [model, *model.model.layers]:
+            mp = unit._get_fsdp_state()._mp_policy
+            assert mp.param_dtype == torch.bfloat16 and mp.reduce_dtype == torch.float32, mp
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]

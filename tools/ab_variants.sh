@@ -1,9 +1,12 @@
 # Alternate the product build with variant builds (tools/build_variants.py) of the bf16 loss head
-# on one box, three rounds: bash tools/ab_variants.sh [arm ...]  (default: product copy_ceiling unphased)
+# on one box, three rounds: bash tools/ab_variants.sh [arm ...]  (default: product copy_ceiling no_math).
+# The variants are built here, on the box (pipelinerl_amd/variants/ is not pushed: .gpurunignore).
 set -u
 B="python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-trainer-step --no-c3 --no-fp32"
 V=pipelinerl-swe_amd/pipelinerl_amd/variants
-ARMS="${*:-product copy_ceiling unphased}"
+ARMS="${*:-product copy_ceiling no_math}"
+BUILD=$(for a in $ARMS; do [ $a = product ] || printf '%s ' $a; done)
+[ -z "$BUILD" ] || timeout -k 10 600 python tools/build_variants.py $BUILD > gpurun_out/ab_variants_build.log 2>&1 || exit $?
 for r in 1 2 3; do
   for arm in $ARMS; do
     if [ $arm = product ]; then lib=""; else lib="PRL_LIB=$V/libprl_hip_$arm.so"; fi
