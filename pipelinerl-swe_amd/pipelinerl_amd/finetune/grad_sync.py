@@ -64,10 +64,15 @@ class GradBuckets:
         self.armed = False
         dev = params[0].device if params else torch.device("cpu")
         self.on_gpu = dev.type == "cuda"
-        # high priority: a hardware queue of its own — a normal-priority stream created here shares the
-        # compute stream's queue (GPU_MAX_HW_QUEUES 4; measured, profiles/r06_queue_probe.json), and the
-        # collectives it orders would wait behind the backward's kernels (tools/queue_probe.py)
-        self.stream = torch.cuda.Stream(device=dev, priority=-1) if self.on_gpu else None
+        # High priority when the collectives it orders run on the device (RCCL, or their emulation:
+        # ``world`` given): a hardware queue of its own — a normal-priority stream created here shares
+        # the compute stream's queue (GPU_MAX_HW_QUEUES 4; measured, profiles/r06_queue_probe.json), and
+        # the collectives would wait behind the backward's kernels (tools/queue_probe.py).  A gloo group
+        # reduces on the host (its device work is two copies), so its stream stays normal: several
+        # ranks sharing one GPU over gloo (the one-GPU rehearsals) each holding high-priority queues
+        # stalled the 4-rank trainer-step probe for minutes (16 s with normal priority).
+        on_device = world is not None or "nccl" in str(dist.get_backend(group))
+        self.stream = torch.cuda.Stream(device=dev, priority=-1 if on_device else 0) if self.on_gpu else None
         self._avg = self.on_gpu and world is None and dist.get_backend(group) == "nccl" and reduce == "mean"
         self._hooks = [p.register_post_accumulate_grad_hook(self._hook) for p in params]
         for p in params:  # model_ops._wgrad may add into .grad in the GEMM while not armed (no hook due)

@@ -319,7 +319,7 @@ class WeightUpdateManager:
         on_gpu = dev.type == "cuda"
         if on_gpu:
             if self._stream is None:
-                self._stream = torch.cuda.Stream(device=dev, priority=side_stream_priority())
+                self._stream = torch.cuda.Stream(device=dev, priority=side_stream_priority(self.group))
             ready = torch.cuda.Event()
             ready.record(torch.cuda.current_stream(dev))
             ctx = torch.cuda.stream(self._stream)
@@ -460,14 +460,25 @@ class WeightUpdateManager:
         self.pool.shutdown(wait=True)
 
 
-def side_stream_priority() -> int:
-    """Priority of the broadcast's side stream (torch: lower is higher): high, so the runtime maps it
-    to a hardware queue of its own (a normal-priority stream may share a hardware queue with the
-    trainer's compute stream, and kernels in one hardware queue run in order;
-    tools/queue_probe.py).  PRL_WU_STREAM_PRIORITY=normal: a pool stream (A/B)."""
+def side_stream_priority(group=None) -> int:
+    """Priority of the broadcast's side stream (torch: lower is higher): high when the broadcast runs
+    on the device (an RCCL group or RcclComm; ``group`` None: assume so), so the runtime maps it to a
+    hardware queue of its own (a normal-priority stream may share a hardware queue with the trainer's
+    compute stream, and kernels in one hardware queue run in order; tools/queue_probe.py).  A gloo
+    group broadcasts from host copies: normal (grad_sync.GradBuckets: several ranks sharing one GPU
+    over gloo, each holding high-priority queues, stalled).  PRL_WU_STREAM_PRIORITY=normal: a pool
+    stream (A/B)."""
     import os
 
-    return 0 if os.environ.get("PRL_WU_STREAM_PRIORITY", "high") == "normal" else -1
+    if os.environ.get("PRL_WU_STREAM_PRIORITY", "high") == "normal":
+        return 0
+    if group is not None and isinstance(group, dist.ProcessGroup):
+        try:
+            if "nccl" not in str(dist.get_backend(group)):
+                return 0
+        except (RuntimeError, ValueError):
+            pass
+    return -1
 
 
 def flat_home(named, layout: FlatLayout) -> torch.Tensor | None:

@@ -49,6 +49,34 @@ def test_weight_update_side_stream_is_high_priority_by_default(monkeypatch):
     assert side_stream_priority() == 0
 
 
+def test_host_collectives_keep_normal_priority_streams(monkeypatch):
+    """A gloo group reduces / broadcasts from host copies: its side streams stay normal priority
+    (several ranks sharing one GPU over gloo, each holding high-priority queues, stalled the 4-rank
+    rehearsal's trainer-step probe); an RCCL group (or none named) gets high priority."""
+    import os
+
+    import torch.distributed as dist
+
+    from pipelinerl_amd.weight_update import side_stream_priority
+
+    monkeypatch.delenv("PRL_WU_STREAM_PRIORITY", raising=False)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        assert side_stream_priority(dist.group.WORLD) == 0
+        assert side_stream_priority(None) == -1
+        from pipelinerl_amd.comm import RcclComm
+
+        assert side_stream_priority(RcclComm(None, 0, 1, None)) == -1
+    finally:
+        dist.destroy_process_group()
+
+
 def test_queue_probe_record_shows_collectives_off_the_compute_queue():
     """The committed rocprofv3 evidence: no collective-carrying stream shares the compute queue,
     while a normal-priority pool stream does (the hazard the options remove)."""
