@@ -151,9 +151,9 @@ static hipError_t adamw_launch(const AdamWGroup& g, const AdamWHyper& h, const v
 // the same bytes, whatever the tensor sizes, and a 7B model's 339 tensors take 11 launches.
 // Per lane, units of 4 elements: one 16-B load of each fp32 stream and one 8-B load of each bf16
 // stream, consecutive lanes on consecutive units (each instruction covers one contiguous span).
-#ifndef PRL_ADAMW_UNROLL
-#define PRL_ADAMW_UNROLL 8
-#endif
+#ifndef PRL_ADAMW_UNROLL  // 4 units per lane (90 VGPRs: 5 waves per SIMD instead of 3 at 8):
+#define PRL_ADAMW_UNROLL 4   // 36.2 vs 37.4 ms per 7B step with nontemporal streams, three alternated
+#endif                       // rounds (profiles/r06_adamw_unroll_ab.jsonl)
 #ifndef PRL_ADAMW_NT  // nontemporal fp32 loads (1) / stores (2) in whole chunks: 3 measured best
 #define PRL_ADAMW_NT 3   // (7B: 37.3 ms vs 38.6 ms plain, profiles/r06_adamw_master_ab.jsonl)
 #endif

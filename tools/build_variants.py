@@ -22,6 +22,8 @@ VARIANTS = {  # the loss head's A/B builds (csrc/grpo_loss.hip macros); profiles
     "nofence": {"PRL_STORE_FENCE": "0"},  # the round-2 store hazard (wrong results: probes only)
     "f32_u2": {"PRL_STREAM_F32_U": "2"},
     "hyb_off": {"PRL_HYB_NL": "-1"},
+    "aw_u8": {"PRL_ADAMW_UNROLL": "8"},  # the fp32-master AdamW with 8 units in flight per thread (the first build)
+    "aw_u2": {"PRL_ADAMW_UNROLL": "2"},
 }
 
 if __name__ == "__main__":
