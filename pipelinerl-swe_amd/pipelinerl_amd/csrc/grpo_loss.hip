@@ -1108,7 +1108,7 @@ __global__ __launch_bounds__(1024) void grpo_fwd_pair_f32(KArgs a, PairArgs pa) 
           r = (int64_t)atomicAdd(pa.row_ctr, 1u);
         }
         next_row[par] = r;
-        if (solo) solo_sh = 1;
+        if (solo) solo_sh = 1;  // (redundant, but without it the allocator spills a row vector: checked in the ISA)
       }
       __syncthreads();
       solo = solo || __builtin_amdgcn_readfirstlane(solo_sh) != 0;
